@@ -1,0 +1,154 @@
+/*
+ * cbgpu.h -- C ABI of the MI355X-native CombBLAS SpGEMM path (libcbgpu.so).
+ *
+ * Plain C: POD structs, raw pointers and sizes, no C++/torch types.  Every entry point is the
+ * device replacement of one reference interface (file:line under gabe-raulet/CombBLAS):
+ *
+ *   cbg_spgemm_local   LocalSpGEMMHash<SR,NTO>(A,B,clearA,clearB,sort)  include/CombBLAS/mtSpGEMM.h:465-470
+ *                      LocalHybridSpGEMM<SR,NTO>(A,B,clearA,clearB,aux)  include/CombBLAS/mtSpGEMM.h:212-217
+ *                      LocalSpGEMM<SR,NTO>(A,B,clearA,clearB)            include/CombBLAS/mtSpGEMM.h:73-78
+ *   cbg_estimate       estimateFLOP + estimateNNZ_Hash                   include/CombBLAS/mtSpGEMM.h:1061-1139, 810-938
+ *                      EstimateLocalFLOP                                 include/CombBLAS/mtSpGEMM.h:667-694
+ *   cbg_merge          MultiwayMerge<SR>(lists, m, n, delarrs)           include/CombBLAS/MultiwayMerge.h:411-412
+ *                      MultiwayMergeHash<SR>(lists, m, n, delarrs, sorted) include/CombBLAS/MultiwayMerge.h:536-537
+ *   cbg_generate_rmat  DistEdgeList::GenGraph500Data + SpParMat(DEL)     include/CombBLAS/DistEdgeList.cpp:223-280,
+ *                                                                        include/CombBLAS/SpParMat.cpp:3082-3196
+ *   cbg_grid_*         CommGrid / CommGrid3D / ProductGrid (rank layout) src/CommGrid.cpp:37-76,164-180,
+ *                                                                        include/CombBLAS/CommGrid3D.h:21-80
+ *
+ * Semantics (SURVEY §8a parity rules):
+ *   - Output columns are row-sorted and duplicate-free when CBG_SORTED_COLS is set (the reference
+ *     intends this but its integerSort mis-sorts, PBBS/radixSort.h:116-120; we sort correctly).
+ *   - Entries whose value equals the semiring zero are kept (returnedSAID() is always false).
+ *   - SELECT2ND keeps the product of the first contributing B nonzero in storage order
+ *     (mtSpGEMM.h:583: SR::add(new, existing) returns `existing`).
+ *   - BOOL_COPY1ST/2ND: a second contribution to one output entry is an error (the reference's
+ *     add() throws, Semirings.h:55-60, 101-106) -> CBG_EADD.
+ *   - Errors never abort the process: DIMMISMATCH (SpDefs.h:73) is returned as CBG_EDIM, etc.
+ *
+ * Memory: views are borrowed (clearA/clearB ownership transfer stays with the C++ caller).
+ * Results are owned by the library until cbg_result_free.  Device pointers are HIP device
+ * pointers on the context's device; host views are staged to the device by the library.
+ */
+#ifndef CBGPU_H
+#define CBGPU_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CBG_ABI_VERSION 1
+
+typedef enum {
+  CBG_OK = 0,
+  CBG_EDIM = 3002,      /* DIMMISMATCH, SpDefs.h:73 */
+  CBG_EALIAS = 3005,    /* MATRIXALIAS, SpDefs.h:76 */
+  CBG_ENOMEM = 10,
+  CBG_EUNSUP = 11,      /* semiring/dtype combination without a device functor */
+  CBG_EDEVICE = 12,     /* HIP runtime error, or no GPU */
+  CBG_EADD = 13,        /* BoolCopy1st/2nd add() would have been called */
+  CBG_EINVAL = 14,      /* malformed view (bad idx_bytes, NULL arrays with nnz>0, ...) */
+  CBG_ECOMM = 15        /* RCCL error */
+} cbg_status;
+
+typedef enum {
+  CBG_SR_PLUS_TIMES = 0,      /* PlusTimesSRing, Semirings.h:212-233 */
+  CBG_SR_MIN_PLUS = 1,        /* MinPlusSRing + inf_plus, Semirings.h:235-255, 40-47 */
+  CBG_SR_SELECT2ND = 2,       /* Select2ndSRing, Semirings.h:143-163 */
+  CBG_SR_SELECT_MAX = 3,      /* SelectMaxSRing<T1,T2>, Semirings.h:165-190 */
+  CBG_SR_SELECT_MAX_BOOL = 4, /* SelectMaxSRing<bool,T2>, Semirings.h:191-210 (A is a pattern) */
+  CBG_SR_BOOL_COPY1ST = 5,    /* BoolCopy1stSRing, Semirings.h:96-141 (B is a pattern) */
+  CBG_SR_BOOL_COPY2ND = 6     /* BoolCopy2ndSRing, Semirings.h:50-94 (A is a pattern) */
+} cbg_semiring;
+
+typedef enum { CBG_BOOL = 0, CBG_I32 = 1, CBG_I64 = 2, CBG_F32 = 3, CBG_F64 = 4 } cbg_dtype;
+
+/* flags for cbg_spgemm_local / cbg_merge */
+#define CBG_SORTED_COLS 1u     /* row-sort every output column (LocalSpGEMMHash sort=true) */
+#define CBG_KEEP_ON_DEVICE 2u  /* leave the result on device only (no host mirror) */
+
+/*
+ * Borrowed view of a local matrix: either a CSC (nzc == ncol, jc == NULL, cp dense ncol+1) or the
+ * reference's DCSC (Dcsc: cp[nzc+1], jc[nzc], ir[nnz], numx[nnz]; dcsc.h:123-130), i.e. exactly the
+ * arrays SpDCCols::GetArrays() hands out (SpDCCols.cpp:817-839).  Row indices ascend within a column.
+ */
+typedef struct {
+  int64_t nrow, ncol, nnz, nzc;
+  const void* cp;       /* nzc+1 entries of idx_bytes */
+  const void* jc;       /* nzc entries of idx_bytes, or NULL for CSC */
+  const void* ir;       /* nnz entries of idx_bytes */
+  int32_t idx_bytes;    /* 4 or 8 */
+  const void* val;      /* nnz values of val_type, or NULL for a pattern (all true / 1) */
+  cbg_dtype val_type;
+  int32_t on_device;    /* 1: HIP device pointers, 0: host pointers */
+} cbg_dcsc_view;
+
+/* Result: CSC with dense colptr (ncol+1). Device arrays always valid; host mirror unless KEEP_ON_DEVICE. */
+typedef struct {
+  int64_t nrow, ncol, nnz;
+  int64_t* colptr;      /* device, ncol+1 */
+  int32_t* row;         /* device, nnz */
+  void* val;            /* device, nnz of val_type */
+  cbg_dtype val_type;
+  int64_t multiplies;   /* estimateFLOP total of the product that made it */
+  void* _owner;         /* library-internal */
+} cbg_csc_result;
+
+typedef struct cbg_ctx cbg_ctx;
+
+/* Per-phase device times (ms) of the last call on a context, from HIP events. */
+typedef struct {
+  double flops_ms, bin_ms, symbolic_ms, scan_ms, numeric_ms, total_ms;
+  int64_t multiplies, nnz_out, bins[16];
+} cbg_profile;
+
+int32_t     cbg_abi_version(void);
+const char* cbg_strerror(cbg_status s);
+
+cbg_status cbg_init(int device, cbg_ctx** ctx);
+cbg_status cbg_destroy(cbg_ctx* ctx);
+/* Use an external HIP stream (hipStream_t) for all subsequent work on ctx; NULL = own stream. */
+cbg_status cbg_set_stream(cbg_ctx* ctx, void* hip_stream);
+cbg_status cbg_synchronize(cbg_ctx* ctx);
+
+/* C = A (x) B over the semiring.  out_type is the value type A, B and C are computed in. */
+cbg_status cbg_spgemm_local(cbg_ctx* ctx, const cbg_dcsc_view* A, const cbg_dcsc_view* B,
+                            cbg_semiring sr, cbg_dtype out_type, uint32_t flags,
+                            cbg_csc_result* C, int64_t* multiplies_out);
+
+/* Symbolic only: total multiplies (estimateFLOP) and exact nnz(C) (estimateNNZ_Hash).
+ * per-column arrays are optional device or host pointers (on_device of B) of length ncol(B). */
+cbg_status cbg_estimate(cbg_ctx* ctx, const cbg_dcsc_view* A, const cbg_dcsc_view* B,
+                        int64_t* multiplies, int64_t* nnz_c);
+
+/* Merge nparts column-sorted partial products of identical shape; duplicates combined with
+ * SR::add in part order (MultiwayMerge.h:184-231 / 320-405). */
+cbg_status cbg_merge(cbg_ctx* ctx, const cbg_csc_result* parts, int32_t nparts, cbg_semiring sr,
+                     cbg_dtype val_type, uint32_t flags, cbg_csc_result* C);
+
+/* Copy a result to caller-owned host arrays (colptr ncol+1, row nnz, val nnz). */
+cbg_status cbg_result_to_host(cbg_ctx* ctx, const cbg_csc_result* C, int64_t* colptr, int32_t* row,
+                              void* val);
+void       cbg_result_free(cbg_ctx* ctx, cbg_csc_result* C);
+
+/* Device-resident CSC owned by the library (inputs kept in HBM across calls, e.g. for benches). */
+cbg_status cbg_upload(cbg_ctx* ctx, const cbg_dcsc_view* host, cbg_csc_result* dev);
+/* A view of a library-owned device CSC, usable as an input of cbg_spgemm_local. */
+cbg_status cbg_result_view(const cbg_csc_result* C, cbg_dcsc_view* view);
+
+cbg_status cbg_last_profile(cbg_ctx* ctx, cbg_profile* prof);
+
+/*
+ * Graph500 Kronecker/R-MAT input (a,b,c,d = .57,.19,.19,.05, clip-and-flip, scrambled vertex
+ * ids, duplicate edges summed into the value = multiplicity), built on the host into a
+ * caller-provided or library-owned CSC.  Deterministic in `seed`.
+ */
+cbg_status cbg_generate_rmat(cbg_ctx* ctx, int32_t scale, int32_t edgefactor, uint64_t seed,
+                             cbg_csc_result* A);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CBGPU_H */
