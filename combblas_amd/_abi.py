@@ -1,0 +1,100 @@
+"""ctypes declarations of include/cbgpu.h (the C ABI of libcbgpu.so).
+
+The product path loads ONLY libcbgpu.so (built in-tree by `make -C combblas_amd/csrc`).  There is
+no CPU fallback: if the library is missing, importing this module raises.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libcbgpu.so")
+
+# cbg_status
+OK, EDIM, EALIAS, ENOMEM, EUNSUP, EDEVICE, EADD, EINVAL, ECOMM = 0, 3002, 3005, 10, 11, 12, 13, 14, 15
+# cbg_semiring
+SR_PLUS_TIMES, SR_MIN_PLUS, SR_SELECT2ND, SR_SELECT_MAX, SR_SELECT_MAX_BOOL, SR_BOOL_COPY1ST, SR_BOOL_COPY2ND = range(7)
+# cbg_dtype
+BOOL, I32, I64, F32, F64 = range(5)
+SORTED_COLS, KEEP_ON_DEVICE = 1, 2
+
+
+class DcscView(ctypes.Structure):
+    _fields_ = [("nrow", ctypes.c_int64), ("ncol", ctypes.c_int64), ("nnz", ctypes.c_int64),
+                ("nzc", ctypes.c_int64), ("cp", ctypes.c_void_p), ("jc", ctypes.c_void_p),
+                ("ir", ctypes.c_void_p), ("idx_bytes", ctypes.c_int32), ("ptr_bytes", ctypes.c_int32),
+                ("val", ctypes.c_void_p), ("val_type", ctypes.c_int), ("on_device", ctypes.c_int32)]
+
+
+class CscResult(ctypes.Structure):
+    _fields_ = [("nrow", ctypes.c_int64), ("ncol", ctypes.c_int64), ("nnz", ctypes.c_int64),
+                ("colptr", ctypes.c_void_p), ("row", ctypes.c_void_p), ("val", ctypes.c_void_p),
+                ("val_type", ctypes.c_int), ("multiplies", ctypes.c_int64), ("_owner", ctypes.c_void_p)]
+
+
+class Profile(ctypes.Structure):
+    _fields_ = [("flops_ms", ctypes.c_double), ("bin_ms", ctypes.c_double), ("symbolic_ms", ctypes.c_double),
+                ("scan_ms", ctypes.c_double), ("numeric_ms", ctypes.c_double), ("total_ms", ctypes.c_double),
+                ("multiplies", ctypes.c_int64), ("nnz_out", ctypes.c_int64), ("bins", ctypes.c_int64 * 16)]
+
+
+class HostCsc(ctypes.Structure):
+    _fields_ = [("nrow", ctypes.c_int64), ("ncol", ctypes.c_int64), ("nnz", ctypes.c_int64),
+                ("colptr", ctypes.c_void_p), ("row", ctypes.c_void_p), ("val", ctypes.c_void_p)]
+
+
+# name -> (restype, argtypes); must match include/cbgpu.h exactly
+SIGNATURES = {
+    "cbg_abi_version": (ctypes.c_int32, []),
+    "cbg_strerror": (ctypes.c_char_p, [ctypes.c_int]),
+    "cbg_init": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
+    "cbg_destroy": (ctypes.c_int, [ctypes.c_void_p]),
+    "cbg_set_stream": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "cbg_synchronize": (ctypes.c_int, [ctypes.c_void_p]),
+    "cbg_spgemm_local": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(DcscView), ctypes.POINTER(DcscView),
+                                        ctypes.c_int, ctypes.c_int, ctypes.c_uint32, ctypes.POINTER(CscResult),
+                                        ctypes.POINTER(ctypes.c_int64)]),
+    "cbg_estimate": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(DcscView), ctypes.POINTER(DcscView),
+                                    ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]),
+    "cbg_merge": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(CscResult), ctypes.c_int32, ctypes.c_int,
+                                 ctypes.c_int, ctypes.c_uint32, ctypes.POINTER(CscResult)]),
+    "cbg_result_to_host": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(CscResult), ctypes.c_void_p,
+                                          ctypes.c_void_p, ctypes.c_void_p]),
+    "cbg_result_free": (None, [ctypes.c_void_p, ctypes.POINTER(CscResult)]),
+    "cbg_upload": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(DcscView), ctypes.POINTER(CscResult)]),
+    "cbg_result_view": (ctypes.c_int, [ctypes.POINTER(CscResult), ctypes.POINTER(DcscView)]),
+    "cbg_last_profile": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(Profile)]),
+    "cbg_generate_rmat": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint64,
+                                         ctypes.POINTER(CscResult)]),
+    "cbg_rmat_host": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_uint64, ctypes.POINTER(HostCsc)]),
+    "cbg_host_free": (None, [ctypes.POINTER(HostCsc)]),
+}
+
+_lib = None
+
+
+def lib():
+    """Load libcbgpu.so (raises OSError if it was not built: the product has no fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise OSError(f"{LIB_PATH} missing: build it with `make -C combblas_amd/csrc` "
+                          "(or __graft_entry__.build()); there is no CPU fallback")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+class CbgError(RuntimeError):
+    def __init__(self, status, where=""):
+        self.status = status
+        msg = lib().cbg_strerror(status).decode()
+        super().__init__(f"{where}: cbgpu status {status} ({msg})" if where else f"cbgpu status {status} ({msg})")
+
+
+def check(status, where=""):
+    if status != OK:
+        raise CbgError(status, where)

@@ -76,10 +76,11 @@ typedef enum { CBG_BOOL = 0, CBG_I32 = 1, CBG_I64 = 2, CBG_F32 = 3, CBG_F64 = 4 
  */
 typedef struct {
   int64_t nrow, ncol, nnz, nzc;
-  const void* cp;       /* nzc+1 entries of idx_bytes */
+  const void* cp;       /* nzc+1 entries of ptr_bytes */
   const void* jc;       /* nzc entries of idx_bytes, or NULL for CSC */
   const void* ir;       /* nnz entries of idx_bytes */
-  int32_t idx_bytes;    /* 4 or 8 */
+  int32_t idx_bytes;    /* 4 or 8: row (ir) and column-id (jc) index width (the reference's IT) */
+  int32_t ptr_bytes;    /* 4 or 8: column pointer (cp) width; 0 = same as idx_bytes */
   const void* val;      /* nnz values of val_type, or NULL for a pattern (all true / 1) */
   cbg_dtype val_type;
   int32_t on_device;    /* 1: HIP device pointers, 0: host pointers */
@@ -140,6 +141,14 @@ cbg_status cbg_result_view(const cbg_csc_result* C, cbg_dcsc_view* view);
 
 cbg_status cbg_last_profile(cbg_ctx* ctx, cbg_profile* prof);
 
+/* Host-only CSC (malloc'd by the library, freed with cbg_host_free). */
+typedef struct {
+  int64_t nrow, ncol, nnz;
+  int64_t* colptr;
+  int32_t* row;
+  double* val;
+} cbg_host_csc;
+
 /*
  * Graph500 Kronecker/R-MAT input (a,b,c,d = .57,.19,.19,.05, clip-and-flip, scrambled vertex
  * ids, duplicate edges summed into the value = multiplicity), built on the host into a
@@ -147,6 +156,9 @@ cbg_status cbg_last_profile(cbg_ctx* ctx, cbg_profile* prof);
  */
 cbg_status cbg_generate_rmat(cbg_ctx* ctx, int32_t scale, int32_t edgefactor, uint64_t seed,
                              cbg_csc_result* A);
+/* The same matrix built on the host only (no GPU needed). */
+cbg_status cbg_rmat_host(int32_t scale, int32_t edgefactor, uint64_t seed, cbg_host_csc* out);
+void       cbg_host_free(cbg_host_csc* m);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,219 @@
+"""GPU parity: libcbgpu.so (via the C ABI) against the reference fixtures and the oracle.
+
+Bars: structure exact; integer/bool semirings bit-exact; PlusTimes<double> within
+1e-12 relative (|c - r| <= 1e-12 * max(|r|, sum|a*b|)); R-MAT multiplicity values are exact.
+"""
+import numpy as np
+import pytest
+
+import combblas_amd as cb
+from helpers import (Csc, abs_product_sums, assert_same_product, canonical_sha256, fixture_inputs,
+                     fixture_product, load_fixture, oracle_spgemm, sorted_dedup_ok)
+
+pytestmark = pytest.mark.gpu
+
+SRCLS = {"plus_times": cb.PlusTimesSRing, "min_plus": cb.MinPlusSRing, "select2nd": cb.Select2ndSRing,
+         "select_max": cb.SelectMaxSRing, "select_max_bool": cb.SelectMaxBoolSRing,
+         "bool_copy1st": cb.BoolCopy1stSRing, "bool_copy2nd": cb.BoolCopy2ndSRing}
+
+
+def upload(ctx, M, dtype=None):
+    return cb.SpDCCols.from_csc(ctx, M.nrow, M.ncol, M.cp, M.ir, M.val, dtype=dtype)
+
+
+def gpu_product(ctx, A, B, sr, dt, sort=True):
+    dA, dB = upload(ctx, A), upload(ctx, B)
+    C = cb.LocalSpGEMMHash(SRCLS[sr](dt), dA, dB, sort=sort)
+    cp, ir, val = C.to_host()
+    return Csc(A.nrow, B.ncol, cp, ir, val), C.multiplies
+
+
+def f64_scale(A, B, C):
+    S = abs_product_sums(A, B)
+    cols = np.repeat(np.arange(C.ncol), np.diff(C.cp))
+    return np.asarray(S[C.ir, cols]).ravel()
+
+
+FULL = [("bcsstk01", "pt_f64_hash"), ("hepth", "pt_f64_hash"), ("largeseq", "pt_f64_hash"),
+        ("largeseq", "mp_f64_hash"), ("pow2", "pt_f64_hash"), ("rect", "pt_f64_hash")] + \
+       [("g500_s10", t) for t in ("pt_f64_hash", "pt_i64_hash", "mp_i64_hash", "s2_i64_hash",
+                                  "sm_i64_hash", "smb_i64_hash")]
+HASHED = [("g500_s12", t) for t in ("pt_f64_hash", "pt_i64_hash", "mp_i64_hash", "s2_i64_hash",
+                                    "sm_i64_hash", "smb_i64_hash")]
+
+
+@pytest.mark.parametrize("name,tag", FULL)
+def test_gpu_matches_reference_fixture(gpu_ctx, name, tag):
+    z = load_fixture(name)
+    A, B, sr, dt = fixture_inputs(z, tag)
+    C, mults = gpu_product(gpu_ctx, A, B, sr, dt)
+    assert mults == int(z[f"C_{tag}_flops"])
+    R = fixture_product(z, tag)
+    scale = f64_scale(A, B, R) if (dt == "f64" and sr == "plus_times") else None
+    assert_same_product(C, R, dt, scale=scale, what=f"{name}/{tag}")
+
+
+@pytest.mark.parametrize("name,tag", HASHED)
+def test_gpu_matches_reference_hash(gpu_ctx, name, tag):
+    z = load_fixture(name)
+    A, B, sr, dt = fixture_inputs(z, tag)
+    C, mults = gpu_product(gpu_ctx, A, B, sr, dt)
+    assert mults == int(z[f"C_{tag}_flops"])
+    assert C.nnz == int(z[f"C_{tag}_nnz"])
+    assert canonical_sha256(C.cp, C.ir, C.val) == str(z[f"C_{tag}_sha256"])
+
+
+def test_matlab_golden(gpu_ctx):
+    z = load_fixture("bcsstk01")
+    A, B, sr, dt = fixture_inputs(z, "pt_f64_hash")
+    C, _ = gpu_product(gpu_ctx, A, B, sr, dt)
+    assert np.array_equal(C.cp, z["M_matlab_cp"]) and np.array_equal(C.ir, z["M_matlab_ir"])
+    M = z["M_matlab_val"]
+    assert np.max(np.abs(C.val - M) / np.abs(M)) < 1e-6
+
+
+# ------------------------------------------------------------------ random cases vs the oracle
+def rand_csc(rng, m, n, density, dtype, pattern=False, lo=-5, hi=6):
+    import scipy.sparse as sp
+    S = sp.random(m, n, density=density, format="csc", random_state=rng,
+                  data_rvs=lambda k: np.ones(k)).astype(np.float64)
+    S.sort_indices()
+    nnz = S.nnz
+    if pattern:
+        val = None
+    elif dtype in ("f64", "f32"):
+        val = rng.uniform(-2, 2, nnz).astype(np.float64 if dtype == "f64" else np.float32)
+    elif dtype == "bool":
+        val = np.ones(nnz, np.uint8)
+    else:
+        val = rng.integers(lo, hi, nnz).astype(np.int64 if dtype == "i64" else np.int32)
+    return Csc(m, n, S.indptr, S.indices, val)
+
+
+CASES = [("plus_times", "f64"), ("plus_times", "f32"), ("plus_times", "i64"), ("plus_times", "i32"),
+         ("plus_times", "bool"), ("min_plus", "f64"), ("min_plus", "i64"), ("min_plus", "i32"),
+         ("select2nd", "i64"), ("select2nd", "f64"), ("select_max", "i64"), ("select_max", "f64"),
+         ("select_max_bool", "i64")]
+
+
+@pytest.mark.parametrize("sr,dt", CASES)
+@pytest.mark.parametrize("shape", [(50, 40, 60, 0.05), (300, 200, 250, 0.02), (2000, 1500, 1800, 0.004)])
+def test_gpu_random_vs_oracle(gpu_ctx, sr, dt, shape):
+    m, k, n, d = shape
+    rng = np.random.default_rng(abs(hash((sr, dt, shape))) % 2**32)
+    A = rand_csc(rng, m, k, d, dt, pattern=(sr == "select_max_bool"))
+    B = rand_csc(rng, k, n, d, dt)
+    R, rmults, rc = oracle_spgemm(A, B, sr, dt)
+    assert rc == 0
+    C, mults = gpu_product(gpu_ctx, A, B, sr, dt)
+    assert mults == rmults
+    assert sorted_dedup_ok(C)
+    if dt == "f32":
+        assert_same_product(C, R, dt, rtol=1e-5, scale=f64_scale(A, B, R), what=f"{sr}/{dt}")
+    else:
+        scale = f64_scale(A, B, R) if dt == "f64" and sr == "plus_times" else None
+        assert_same_product(C, R, dt, scale=scale, what=f"{sr}/{dt}")
+
+
+def test_gpu_min_plus_infinity(gpu_ctx):
+    """inf_plus: max() is infinity and absorbs (Semirings.h:40-47)."""
+    big = np.iinfo(np.int64).max
+    A = Csc(3, 2, [0, 2, 3], [0, 2, 1], np.array([big, 5, 7], np.int64))
+    B = Csc(2, 2, [0, 2, 3], [0, 1, 1], np.array([1, big, 2], np.int64))
+    R, _, rc = oracle_spgemm(A, B, "min_plus", "i64")
+    C, _ = gpu_product(gpu_ctx, A, B, "min_plus", "i64")
+    assert_same_product(C, R, "i64")
+
+
+def test_gpu_boolcopy(gpu_ctx):
+    A = Csc(3, 2, [0, 1, 2], [0, 2], None)
+    B = Csc(2, 2, [0, 1, 2], [1, 0], np.array([3.5, 4.5]))
+    C, _ = gpu_product(gpu_ctx, A, B, "bool_copy2nd", "f64")
+    assert C.ir.tolist() == [2, 0] and C.val.tolist() == [3.5, 4.5]
+    Bdup = Csc(2, 1, [0, 2], [0, 1], np.array([3.0, 4.0]))
+    Adup = Csc(1, 2, [0, 1, 2], [0, 0], None)
+    with pytest.raises(cb.CbgError) as ei:
+        gpu_product(gpu_ctx, Adup, Bdup, "bool_copy2nd", "f64")
+    assert ei.value.status == 13
+
+
+def test_gpu_empty_and_dim_errors(gpu_ctx):
+    A = Csc(4, 3, np.zeros(4, np.int64), np.zeros(0, np.int32), np.zeros(0))
+    B = Csc(3, 5, [0, 1, 1, 1, 1, 1], [2], np.ones(1))
+    C, m = gpu_product(gpu_ctx, A, B, "plus_times", "f64")
+    assert C.nnz == 0 and m == 0 and len(C.cp) == 6
+    Bbad = Csc(4, 5, np.zeros(6, np.int64), np.zeros(0, np.int32), np.zeros(0))
+    with pytest.raises(cb.CbgError) as ei:
+        gpu_product(gpu_ctx, A, Bbad, "plus_times", "f64")
+    assert ei.value.status == 3002
+
+
+def _check_vs_oracle(ctx, A, B, sr="plus_times", dt="f64"):
+    R, rm, rc = oracle_spgemm(A, B, sr, dt)
+    assert rc == 0
+    C, m = gpu_product(ctx, A, B, sr, dt)
+    assert m == rm
+    assert_same_product(C, R, dt, scale=f64_scale(A, B, R) if dt == "f64" else None)
+    return C
+
+
+def test_gpu_hash_overflow_fallback(gpu_ctx):
+    """Rows clustered at the top of a wide span defeat the order-preserving hash; the column must be
+    re-done by the windowed dense kernel (fallback list), still exact."""
+    n = 1 << 20
+    rows = np.r_[0, np.arange(n - 3000, n)].astype(np.int32)
+    A = Csc(n, 1, [0, len(rows)], rows, np.arange(1, len(rows) + 1, dtype=np.float64))
+    B = Csc(1, 1, [0, 1], [0], np.array([2.0]))
+    C = _check_vs_oracle(gpu_ctx, A, B)
+    assert gpu_ctx.last_profile()["bins"][15] >= 1
+
+
+def test_gpu_heavy_column_window_kernel(gpu_ctx):
+    """One output column with ~60k entries spread over 2^21 rows -> windowed kernel, many windows,
+    long segments (wavefront path) and short segments (lane path) mixed."""
+    rng = np.random.default_rng(7)
+    n = 1 << 21
+    cols = []
+    cp = [0]
+    for j in range(40):
+        L = int(rng.integers(1, 4000)) if j % 3 else int(rng.integers(1, 20))
+        cols.append(np.sort(rng.choice(n, L, replace=False)).astype(np.int32))
+        cp.append(cp[-1] + L)
+    A = Csc(n, 40, cp, np.concatenate(cols), rng.uniform(-1, 1, cp[-1]))
+    B = Csc(40, 3, [0, 40, 45, 60], np.r_[np.arange(40), np.arange(5), np.arange(10, 25)].astype(np.int32),
+            rng.uniform(-1, 1, 60))
+    _check_vs_oracle(gpu_ctx, A, B)
+
+
+@pytest.mark.parametrize("scale", [12, 14, 16])
+def test_gpu_rmat_vs_oracle(gpu_ctx, scale):
+    n, cp, ir, val = cb.generate_rmat_host(scale, 16, seed=scale)
+    A = Csc(n, n, cp, ir, val)
+    R, rm, rc = oracle_spgemm(A, A, "plus_times", "f64")
+    C, m = gpu_product(gpu_ctx, A, A, "plus_times", "f64")
+    assert m == rm
+    # multiplicity values -> exact sums
+    assert np.array_equal(C.cp, R.cp) and np.array_equal(C.ir, R.ir) and np.array_equal(C.val, R.val)
+
+
+def test_gpu_dcsc_input_view(gpu_ctx):
+    """The reference's DCSC arrays (cp[nzc+1], jc[nzc], ir, numx; int64 IT) go straight in."""
+    import ctypes
+    from combblas_amd import _abi
+    z = load_fixture("g500_s10")
+    A, B, sr, dt = fixture_inputs(z, "pt_f64_hash")
+    nzc_cols = np.flatnonzero(np.diff(B.cp) > 0).astype(np.int64)
+    dcp = np.r_[B.cp[nzc_cols], B.cp[-1]].astype(np.int64)
+    ir64 = B.ir.astype(np.int64)
+    vb = _abi.DcscView(B.nrow, B.ncol, B.nnz, len(nzc_cols), dcp.ctypes.data, nzc_cols.ctypes.data,
+                       ir64.ctypes.data, 8, 8, B.val.ctypes.data, _abi.F64, 0)
+    dA = upload(gpu_ctx, A)
+    va = dA._view()
+    res = _abi.CscResult()
+    m = ctypes.c_int64()
+    _abi.check(gpu_ctx._lib.cbg_spgemm_local(gpu_ctx._ptr, ctypes.byref(va), ctypes.byref(vb), 0, _abi.F64, 1,
+                                             ctypes.byref(res), ctypes.byref(m)))
+    C = cb.SpTuples._from_result(gpu_ctx, res)
+    cp, irc, v = C.to_host()
+    R = fixture_product(z, "pt_f64_hash")
+    assert np.array_equal(cp, R.cp) and np.array_equal(irc, R.ir) and np.array_equal(v, R.val)
