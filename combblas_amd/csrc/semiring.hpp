@@ -76,7 +76,7 @@ template <typename V> struct Semiring<SR_PLUS_TIMES, V> {        // Semirings.h:
   using Acc = typename AccOf<V>::type;
   static constexpr bool kAddIsError = false, kNeedsBPos = false;
   __device__ static Acc identity() { return Acc(0); }
-  __device__ static Acc mul(V a, V b, int64_t) {
+  __device__ static Acc mul(V a, V b, int64_t, int64_t) {
     if constexpr (sizeof(V) == 1) return Acc((a != 0) & (b != 0));   // PlusTimes<bool,bool> = AND
     else return Acc(a) * Acc(b);
   }
@@ -84,66 +84,93 @@ template <typename V> struct Semiring<SR_PLUS_TIMES, V> {        // Semirings.h:
     if constexpr (sizeof(V) == 1) lds_max(s, x);                     // bool '+' = OR
     else lds_add(s, x);
   }
-  __device__ static V out(Acc a, const V*) { return V(a); }
+  __device__ static V out(Acc a, const V*, const V*) { return V(a); }
 };
 
 template <typename V> struct Semiring<SR_MIN_PLUS, V> {           // Semirings.h:235-255, inf_plus 40-47
   using Acc = typename AccOf<V>::type;
   static constexpr bool kAddIsError = false, kNeedsBPos = false;
   __device__ static Acc identity() { return Lim<Acc>::max(); }
-  __device__ static Acc mul(V a, V b, int64_t) {
+  __device__ static Acc mul(V a, V b, int64_t, int64_t) {
     const Acc inf = Lim<Acc>::max();
     Acc x = Acc(a), y = Acc(b);
     if (x == inf || y == inf) return inf;
     return x + y;
   }
   __device__ static void acc(Acc* s, Acc x) { lds_min(s, x); }
-  __device__ static V out(Acc a, const V*) { return V(a); }
+  __device__ static V out(Acc a, const V*, const V*) { return V(a); }
 };
 
 template <typename V> struct Semiring<SR_SELECT_MAX, V> {         // Semirings.h:165-190
   using Acc = typename AccOf<V>::type;
   static constexpr bool kAddIsError = false, kNeedsBPos = false;
   __device__ static Acc identity() { return Lim<Acc>::lowest(); }
-  __device__ static Acc mul(V a, V b, int64_t) { return Acc(a) * Acc(b); }
+  __device__ static Acc mul(V a, V b, int64_t, int64_t) { return Acc(a) * Acc(b); }
   __device__ static void acc(Acc* s, Acc x) { lds_max(s, x); }
-  __device__ static V out(Acc a, const V*) { return V(a); }
+  __device__ static V out(Acc a, const V*, const V*) { return V(a); }
 };
 
 template <typename V> struct Semiring<SR_SELECT_MAX_BOOL, V> {    // SelectMaxSRing<bool,T2>, Semirings.h:191-210
   using Acc = typename AccOf<V>::type;
   static constexpr bool kAddIsError = false, kNeedsBPos = false;
   __device__ static Acc identity() { return Lim<Acc>::lowest(); }
-  __device__ static Acc mul(V, V b, int64_t) { return Acc(b); }
+  __device__ static Acc mul(V, V b, int64_t, int64_t) { return Acc(b); }
   __device__ static void acc(Acc* s, Acc x) { lds_max(s, x); }
-  __device__ static V out(Acc a, const V*) { return V(a); }
+  __device__ static V out(Acc a, const V*, const V*) { return V(a); }
 };
 
 template <typename V> struct Semiring<SR_SELECT2ND, V> {          // Semirings.h:143-163
   using Acc = int32_t;                                            // min B position (first insert)
   static constexpr bool kAddIsError = false, kNeedsBPos = true;
   __device__ static Acc identity() { return INT32_MAX; }
-  __device__ static Acc mul(V, V, int64_t pos) { return Acc(pos); }
+  __device__ static Acc mul(V, V, int64_t, int64_t pos) { return Acc(pos); }
   __device__ static void acc(Acc* s, Acc x) { lds_min(s, x); }
-  __device__ static V out(Acc a, const V* bval) { return bval ? bval[a] : V(1); }
+  __device__ static V out(Acc a, const V*, const V* bval) { return bval ? bval[a] : V(1); }
 };
 
 template <typename V> struct Semiring<SR_BOOL_COPY2ND, V> {       // Semirings.h:50-94 (A is bool)
   using Acc = int32_t;                                            // B position, single contributor
   static constexpr bool kAddIsError = true, kNeedsBPos = true;
   __device__ static Acc identity() { return INT32_MAX; }
-  __device__ static Acc mul(V, V, int64_t pos) { return Acc(pos); }
+  __device__ static Acc mul(V, V, int64_t, int64_t pos) { return Acc(pos); }
   __device__ static void acc(Acc* s, Acc x) { lds_min(s, x); }
-  __device__ static V out(Acc a, const V* bval) { return bval ? bval[a] : V(1); }
+  __device__ static V out(Acc a, const V*, const V* bval) { return bval ? bval[a] : V(1); }
 };
 
 template <typename V> struct Semiring<SR_BOOL_COPY1ST, V> {       // Semirings.h:96-141 (B is bool)
   using Acc = typename AccOf<V>::type;
   static constexpr bool kAddIsError = true, kNeedsBPos = false;
   __device__ static Acc identity() { return Lim<Acc>::lowest(); }
-  __device__ static Acc mul(V a, V, int64_t) { return Acc(a); }
+  __device__ static Acc mul(V a, V, int64_t, int64_t) { return Acc(a); }
   __device__ static void acc(Acc* s, Acc x) { lds_max(s, x); }
-  __device__ static V out(Acc a, const V*) { return V(a); }
+  __device__ static V out(Acc a, const V*, const V*) { return V(a); }
+};
+
+// ---- multiway merge as a product ------------------------------------------------------------
+// MultiwayMerge(lists) (MultiwayMerge.h:411-526) is run as Acat * Sel, where Acat holds the k
+// partial products side by side (column l*ncol + j) and Sel(:, j) selects rows {l*ncol + j}.  The
+// "multiply" copies the partial's value; "add" is the wrapped semiring's add.  Duplicates are
+// combined in list order (SerialMerge keeps SR::add(acc, next)); for SELECT2ND the first list that
+// holds the entry wins: Acc packs (Sel position << 40 | Acat position) and the minimum is kept.
+template <class SR> struct MergeOf;
+template <int SRI, typename V> struct MergeOf<Semiring<SRI, V>> {
+  using Base = Semiring<SRI, V>;
+  using Acc = typename Base::Acc;
+  static constexpr bool kAddIsError = Base::kAddIsError, kNeedsBPos = false;
+  __device__ static Acc identity() { return Base::identity(); }
+  __device__ static Acc mul(V a, V, int64_t, int64_t) { return Acc(a); }
+  __device__ static void acc(Acc* s, Acc x) { Base::acc(s, x); }
+  __device__ static V out(Acc a, const V*, const V*) { return V(a); }
+};
+template <typename V> struct MergeOf<Semiring<SR_SELECT2ND, V>> {
+  using Acc = int64_t;
+  static constexpr bool kAddIsError = false, kNeedsBPos = true;
+  __device__ static Acc identity() { return INT64_MAX; }
+  __device__ static Acc mul(V, V, int64_t q, int64_t bpos) { return (bpos << 40) | q; }
+  __device__ static void acc(Acc* s, Acc x) { lds_min(s, x); }
+  __device__ static V out(Acc a, const V* aval, const V*) {
+    return aval ? aval[a & ((1LL << 40) - 1)] : V(1);
+  }
 };
 
 }  // namespace cbg

@@ -1,4 +1,5 @@
-// cbgpu.hip -- C ABI (include/cbgpu.h) + host orchestration of the local SpGEMM on one MI355X.
+#pragma once
+// spgemm_host.hpp -- host orchestration of the local SpGEMM on one MI355X (templates + workspace).
 //
 // Pipeline per cbg_spgemm_local call (all on the context's stream):
 //   stage inputs -> k_col_stats -> k_bin(symbolic) -> k_sym_{wave,block,window} -> scan -> alloc C
@@ -26,7 +27,7 @@ using namespace cbg;
     }                                                                                               \
   } while (0)
 
-namespace {
+namespace cbg { namespace host {
 
 // symbolic classes: wave T = 64..1024 words, block T = 2048..32768 words, then window
 constexpr int kSymWave = 5, kSymBlock = 5;
@@ -50,7 +51,7 @@ struct DevBuf {
   template <typename T> T* as() const { return (T*)p; }
 };
 
-size_t dt_size(cbg_dtype t) {
+inline size_t dt_size(cbg_dtype t) {
   switch (t) { case CBG_BOOL: return 1; case CBG_I32: case CBG_F32: return 4; default: return 8; }
 }
 
@@ -65,7 +66,10 @@ struct Owner {                 // device storage behind a cbg_csc_result
   DevBuf cp, ir, val;
 };
 
-}  // namespace
+}  // namespace host
+}  // namespace cbg
+
+using namespace cbg::host;
 
 struct cbg_ctx {
   int device = 0;
@@ -77,13 +81,13 @@ struct cbg_ctx {
   DevBuf flop, span, cnt, list, hist, cursor, scan_tiles, scalars, cur, nxt, ovf_list, stageA[5], stageB[5];
 };
 
-static hipError_t launch_cfg_lds(const void* fn, size_t lds) {
+inline hipError_t launch_cfg_lds(const void* fn, size_t lds) {
   if (lds > 64 * 1024) return hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   return hipSuccess;
 }
 
 // ------------------------------------------------------------------------------- input staging
-namespace {
+namespace cbg { namespace host {
 template <typename V>
 cbg_status stage(cbg_ctx* ctx, const cbg_dcsc_view* v, DevBuf* sb, DevCsc<V>* out) {
   const int pb = v->ptr_bytes ? v->ptr_bytes : v->idx_bytes;
@@ -170,7 +174,7 @@ struct Classes {
   std::vector<unsigned long long> off;    // exclusive offsets
 };
 
-cbg_status bin_columns(cbg_ctx* ctx, int64_t ncol, const int64_t* cnt, const int2* span, BinParams bp,
+inline cbg_status bin_columns(cbg_ctx* ctx, int64_t ncol, const int64_t* cnt, const int2* span, BinParams bp,
                        int32_t* list, Classes* cl) {
   hipStream_t st = ctx->stream;
   const int ncls = bp.nwave + bp.nblock + 2;
@@ -235,10 +239,10 @@ hipError_t launch_window(hipStream_t st, const int32_t* l, const int* count_dev,
 }
 
 // ------------------------------------------------------------------------------- the product
-template <int SRI, typename V>
+template <class SRT, typename V>
 cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_view* Bv, uint32_t flags,
                        cbg_csc_result* C, int64_t* mult_out) {
-  using SRT = Semiring<SRI, V>;
+  (void)flags;   // output columns are always row-sorted (sorting is free in the compaction)
   hipStream_t st = ctx->stream;
   cbg_profile& pf = ctx->prof;
   memset(&pf, 0, sizeof(pf));
@@ -386,201 +390,95 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
   return CBG_OK;
 }
 
-template <typename V>
+template <int SRI, typename V, bool MERGE>
+using Pick = std::conditional_t<MERGE, MergeOf<Semiring<SRI, V>>, Semiring<SRI, V>>;
+
+template <typename V, bool MERGE = false>
 cbg_status dispatch_sr(cbg_ctx* ctx, const cbg_dcsc_view* A, const cbg_dcsc_view* B, cbg_semiring sr, uint32_t f,
                        cbg_csc_result* C, int64_t* m) {
   switch (sr) {
-    case CBG_SR_PLUS_TIMES: return spgemm_impl<SR_PLUS_TIMES, V>(ctx, A, B, f, C, m);
-    case CBG_SR_MIN_PLUS: return spgemm_impl<SR_MIN_PLUS, V>(ctx, A, B, f, C, m);
-    case CBG_SR_SELECT2ND: return spgemm_impl<SR_SELECT2ND, V>(ctx, A, B, f, C, m);
-    case CBG_SR_SELECT_MAX: return spgemm_impl<SR_SELECT_MAX, V>(ctx, A, B, f, C, m);
-    case CBG_SR_SELECT_MAX_BOOL: return spgemm_impl<SR_SELECT_MAX_BOOL, V>(ctx, A, B, f, C, m);
-    case CBG_SR_BOOL_COPY1ST: return spgemm_impl<SR_BOOL_COPY1ST, V>(ctx, A, B, f, C, m);
-    case CBG_SR_BOOL_COPY2ND: return spgemm_impl<SR_BOOL_COPY2ND, V>(ctx, A, B, f, C, m);
+    case CBG_SR_PLUS_TIMES: return spgemm_impl<Pick<SR_PLUS_TIMES, V, MERGE>, V>(ctx, A, B, f, C, m);
+    case CBG_SR_MIN_PLUS: return spgemm_impl<Pick<SR_MIN_PLUS, V, MERGE>, V>(ctx, A, B, f, C, m);
+    case CBG_SR_SELECT2ND: return spgemm_impl<Pick<SR_SELECT2ND, V, MERGE>, V>(ctx, A, B, f, C, m);
+    case CBG_SR_SELECT_MAX: return spgemm_impl<Pick<SR_SELECT_MAX, V, MERGE>, V>(ctx, A, B, f, C, m);
+    case CBG_SR_SELECT_MAX_BOOL: return spgemm_impl<Pick<SR_SELECT_MAX_BOOL, V, MERGE>, V>(ctx, A, B, f, C, m);
+    case CBG_SR_BOOL_COPY1ST: return spgemm_impl<Pick<SR_BOOL_COPY1ST, V, MERGE>, V>(ctx, A, B, f, C, m);
+    case CBG_SR_BOOL_COPY2ND: return spgemm_impl<Pick<SR_BOOL_COPY2ND, V, MERGE>, V>(ctx, A, B, f, C, m);
   }
   return CBG_EUNSUP;
 }
 
-}  // namespace
-
-// =============================================================================== C ABI
-extern "C" {
-
-int32_t cbg_abi_version(void) { return CBG_ABI_VERSION; }
-
-const char* cbg_strerror(cbg_status s) {
-  switch (s) {
-    case CBG_OK: return "ok";
-    case CBG_EDIM: return "dimension mismatch (DIMMISMATCH 3002)";
-    case CBG_EALIAS: return "matrix alias (MATRIXALIAS 3005)";
-    case CBG_ENOMEM: return "out of device memory";
-    case CBG_EUNSUP: return "unsupported semiring/dtype";
-    case CBG_EDEVICE: return "HIP device error or no GPU";
-    case CBG_EADD: return "semiring add() called on BoolCopy1st/2nd (reference throws)";
-    case CBG_EINVAL: return "invalid matrix view";
-    case CBG_ECOMM: return "RCCL communication error";
+// concatenated partials: colptr[l*ncol + j] = off_l + cp_l[j]; selector: Sel(:, j) = {l*ncol + j}
+static __global__ void k_merge_cat_cp(int64_t ncol, const int64_t* __restrict__ cp, int64_t off, int64_t* __restrict__ out) {
+  for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < ncol; j += (int64_t)gridDim.x * blockDim.x)
+    out[j] = off + cp[j];
+}
+static __global__ void k_merge_selector(int64_t ncol, int32_t k, int64_t* __restrict__ scp, int32_t* __restrict__ sir) {
+  for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j <= ncol; j += (int64_t)gridDim.x * blockDim.x) {
+    scp[j] = j * k;
+    if (j < ncol)
+      for (int32_t l = 0; l < k; ++l) sir[j * k + l] = (int32_t)(l * ncol + j);
   }
-  return "unknown status";
 }
 
-cbg_status cbg_init(int device, cbg_ctx** out) {
-  if (!out) return CBG_EINVAL;
-  *out = nullptr;
-  int n = 0;
-  if (hipGetDeviceCount(&n) != hipSuccess || n <= device || device < 0) return CBG_EDEVICE;
-  HIPCHK(hipSetDevice(device));
-  cbg_ctx* c = new cbg_ctx;
-  c->device = device;
-  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) { delete c; return CBG_EDEVICE; }
-  c->own_stream = true;
-  for (auto& e : c->ev)
-    if (hipEventCreate(&e) != hipSuccess) { delete c; return CBG_EDEVICE; }
-  *out = c;
-  return CBG_OK;
-}
-
-cbg_status cbg_destroy(cbg_ctx* c) {
-  if (!c) return CBG_OK;
-  (void)hipSetDevice(c->device);
-  (void)hipStreamSynchronize(c->stream);
-  for (auto& e : c->ev) if (e) (void)hipEventDestroy(e);
-  if (c->own_stream) (void)hipStreamDestroy(c->stream);
-  delete c;
-  return CBG_OK;
-}
-
-cbg_status cbg_set_stream(cbg_ctx* c, void* s) {
-  if (!c) return CBG_EINVAL;
-  if (c->own_stream) { (void)hipStreamSynchronize(c->stream); (void)hipStreamDestroy(c->stream); }
-  if (s) { c->stream = (hipStream_t)s; c->own_stream = false; }
-  else { HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)); c->own_stream = true; }
-  return CBG_OK;
-}
-
-cbg_status cbg_synchronize(cbg_ctx* c) {
-  if (!c) return CBG_EINVAL;
-  HIPCHK(hipStreamSynchronize(c->stream));
-  return CBG_OK;
-}
-
-cbg_status cbg_spgemm_local(cbg_ctx* ctx, const cbg_dcsc_view* A, const cbg_dcsc_view* B, cbg_semiring sr,
-                            cbg_dtype out_type, uint32_t flags, cbg_csc_result* C, int64_t* multiplies_out) {
-  if (!ctx || !A || !B || !C) return CBG_EINVAL;
-  HIPCHK(hipSetDevice(ctx->device));
-  switch (out_type) {
-    case CBG_F64: return dispatch_sr<double>(ctx, A, B, sr, flags, C, multiplies_out);
-    case CBG_F32: return dispatch_sr<float>(ctx, A, B, sr, flags, C, multiplies_out);
-    case CBG_I64: return dispatch_sr<int64_t>(ctx, A, B, sr, flags, C, multiplies_out);
-    case CBG_I32: return dispatch_sr<int32_t>(ctx, A, B, sr, flags, C, multiplies_out);
-    case CBG_BOOL: return dispatch_sr<uint8_t>(ctx, A, B, sr, flags, C, multiplies_out);
+template <typename V>
+cbg_status merge_impl(cbg_ctx* ctx, const cbg_csc_result* parts, int32_t k, cbg_semiring sr, uint32_t flags,
+                      cbg_csc_result* C) {
+  const int64_t nrow = parts[0].nrow, ncol = parts[0].ncol;
+  int64_t tot = 0;
+  for (int32_t l = 0; l < k; ++l) {
+    if (parts[l].nrow != nrow || parts[l].ncol != ncol) return CBG_EDIM;   // MultiwayMerge.h:443-450
+    if (parts[l].val_type != DtOf<V>::value) return CBG_EINVAL;
+    tot += parts[l].nnz;
   }
-  return CBG_EUNSUP;
-}
-
-cbg_status cbg_estimate(cbg_ctx* ctx, const cbg_dcsc_view* A, const cbg_dcsc_view* B, int64_t* mults,
-                        int64_t* nnzc) {
-  // symbolic == the first half of the product; run the pattern product and read its size
-  cbg_dcsc_view a = *A, b = *B;
-  a.val = nullptr; b.val = nullptr;
-  a.val_type = b.val_type = CBG_BOOL;
-  cbg_csc_result C;
-  cbg_status s = cbg_spgemm_local(ctx, &a, &b, CBG_SR_PLUS_TIMES, CBG_BOOL, 0, &C, mults);
-  if (s != CBG_OK) return s;
-  if (nnzc) *nnzc = C.nnz;
-  cbg_result_free(ctx, &C);
-  return CBG_OK;
-}
-
-cbg_status cbg_result_to_host(cbg_ctx* ctx, const cbg_csc_result* C, int64_t* colptr, int32_t* row, void* val) {
-  if (!ctx || !C) return CBG_EINVAL;
-  HIPCHK(hipSetDevice(ctx->device));
-  if (colptr) HIPCHK(hipMemcpyAsync(colptr, C->colptr, sizeof(int64_t) * (C->ncol + 1), hipMemcpyDeviceToHost, ctx->stream));
-  if (row && C->nnz) HIPCHK(hipMemcpyAsync(row, C->row, sizeof(int32_t) * C->nnz, hipMemcpyDeviceToHost, ctx->stream));
-  if (val && C->nnz) HIPCHK(hipMemcpyAsync(val, C->val, dt_size(C->val_type) * C->nnz, hipMemcpyDeviceToHost, ctx->stream));
-  HIPCHK(hipStreamSynchronize(ctx->stream));
-  return CBG_OK;
-}
-
-void cbg_result_free(cbg_ctx* ctx, cbg_csc_result* C) {
-  if (!C) return;
-  if (ctx) { (void)hipSetDevice(ctx->device); (void)hipStreamSynchronize(ctx->stream); }
-  delete (Owner*)C->_owner;
-  memset(C, 0, sizeof(*C));
-}
-
-cbg_status cbg_upload(cbg_ctx* ctx, const cbg_dcsc_view* v, cbg_csc_result* out) {
-  if (!ctx || !v || !out) return CBG_EINVAL;
-  const int pb = v->ptr_bytes ? v->ptr_bytes : v->idx_bytes;
-  if (v->jc || (v->idx_bytes != 8 && v->idx_bytes != 4) || (pb != 8 && pb != 4)) return CBG_EINVAL;
-  HIPCHK(hipSetDevice(ctx->device));
-  std::unique_ptr<Owner> own(new Owner);
+  if ((int64_t)k * ncol >= INT32_MAX) return CBG_EUNSUP;
   hipStream_t st = ctx->stream;
-  const hipMemcpyKind kind = v->on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
-  HIPCHK(own->cp.reserve(8 * (v->ncol + 1)));
-  HIPCHK(own->ir.reserve(4 * (v->nnz + 1)));
-  const size_t vs = v->val ? dt_size(v->val_type) : 0;
-  HIPCHK(own->val.reserve(vs * (v->nnz + 1) + 8));
-  DevBuf tmp;
-  DevBuf tmp2;
-  if (pb == 8) {
-    HIPCHK(hipMemcpyAsync(own->cp.p, v->cp, 8 * (v->ncol + 1), kind, st));
-  } else {
-    HIPCHK(tmp2.reserve(4 * (v->ncol + 2)));
-    HIPCHK(hipMemcpyAsync(tmp2.p, v->cp, 4 * (v->ncol + 1), kind, st));
-    k_i32_to_i64<<<256, 256, 0, st>>>(v->ncol + 1, tmp2.as<int32_t>(), own->cp.as<int64_t>());
+  DevBuf cat_cp, cat_ir, cat_val, sel_cp, sel_ir;
+  HIPCHK(cat_cp.reserve(sizeof(int64_t) * (k * ncol + 1)));
+  HIPCHK(cat_ir.reserve(sizeof(int32_t) * (tot + 1)));
+  HIPCHK(cat_val.reserve(sizeof(V) * (tot + 1)));
+  HIPCHK(sel_cp.reserve(sizeof(int64_t) * (ncol + 1)));
+  HIPCHK(sel_ir.reserve(sizeof(int32_t) * (k * ncol + 1)));
+  int64_t off = 0;
+  for (int32_t l = 0; l < k; ++l) {
+    const int64_t n = parts[l].nnz;
+    if (n) {
+      HIPCHK(hipMemcpyAsync(cat_ir.as<int32_t>() + off, parts[l].row, sizeof(int32_t) * n, hipMemcpyDeviceToDevice, st));
+      HIPCHK(hipMemcpyAsync(cat_val.as<V>() + off, parts[l].val, sizeof(V) * n, hipMemcpyDeviceToDevice, st));
+    }
+    k_merge_cat_cp<<<(int)grid_for(ncol, 256, kMaxGrid), 256, 0, st>>>(ncol, parts[l].colptr, off,
+                                                                      cat_cp.as<int64_t>() + l * ncol);
+    off += n;
   }
-  if (v->idx_bytes == 8) {
-    HIPCHK(tmp.reserve(8 * (v->nnz + 1)));
-    HIPCHK(hipMemcpyAsync(tmp.p, v->ir, 8 * v->nnz, kind, st));
-    k_widen_idx<<<1024, 256, 0, st>>>(v->nnz, tmp.as<int64_t>(), own->ir.as<int32_t>());
-  } else {
-    HIPCHK(hipMemcpyAsync(own->ir.p, v->ir, 4 * v->nnz, kind, st));
-  }
-  if (v->val && v->nnz) HIPCHK(hipMemcpyAsync(own->val.p, v->val, vs * v->nnz, kind, st));
-  HIPCHK(hipStreamSynchronize(st));
-  memset(out, 0, sizeof(*out));
-  out->nrow = v->nrow; out->ncol = v->ncol; out->nnz = v->nnz;
-  out->colptr = own->cp.as<int64_t>(); out->row = own->ir.as<int32_t>();
-  out->val = v->val ? own->val.p : nullptr;
-  out->val_type = v->val_type;
-  out->_owner = own.release();
-  return CBG_OK;
-}
-
-cbg_status cbg_result_view(const cbg_csc_result* C, cbg_dcsc_view* v) {
-  if (!C || !v) return CBG_EINVAL;
-  memset(v, 0, sizeof(*v));
-  v->nrow = C->nrow; v->ncol = C->ncol; v->nnz = C->nnz; v->nzc = C->ncol;
-  v->cp = C->colptr; v->jc = nullptr; v->ir = C->row; v->idx_bytes = 4; v->ptr_bytes = 8;
-  v->val = C->val; v->val_type = C->val_type; v->on_device = 1;
-  return CBG_OK;
-}
-
-cbg_status cbg_last_profile(cbg_ctx* ctx, cbg_profile* p) {
-  if (!ctx || !p) return CBG_EINVAL;
-  *p = ctx->prof;
-  return CBG_OK;
-}
-
-}  // extern "C"
-
-extern "C" cbg_status cbg_generate_rmat(cbg_ctx* ctx, int32_t scale, int32_t edgefactor, uint64_t seed,
-                                        cbg_csc_result* A) {
-  if (!ctx || !A) return CBG_EINVAL;
-  cbg_host_csc h;
-  cbg_status s = cbg_rmat_host(scale, edgefactor, seed, &h);
-  if (s != CBG_OK) return s;
-  cbg_dcsc_view v{};
-  v.nrow = h.nrow; v.ncol = h.ncol; v.nnz = h.nnz; v.nzc = h.ncol;
-  v.cp = h.colptr; v.ir = h.row; v.idx_bytes = 4; v.ptr_bytes = 8;
-  v.val = h.val; v.val_type = CBG_F64; v.on_device = 0;
-  s = cbg_upload(ctx, &v, A);
-  cbg_host_free(&h);
+  HIPCHK(hipMemcpyAsync(cat_cp.as<int64_t>() + (int64_t)k * ncol, &tot, sizeof(int64_t), hipMemcpyHostToDevice, st));
+  k_merge_selector<<<(int)grid_for(ncol + 1, 256, kMaxGrid), 256, 0, st>>>(ncol, k, sel_cp.as<int64_t>(),
+                                                                           sel_ir.as<int32_t>());
+  HIPCHK(hipGetLastError());
+  cbg_dcsc_view a{}, b{};
+  a.nrow = nrow; a.ncol = (int64_t)k * ncol; a.nnz = tot; a.nzc = a.ncol;
+  a.cp = cat_cp.p; a.ir = cat_ir.p; a.idx_bytes = 4; a.ptr_bytes = 8; a.val = cat_val.p;
+  a.val_type = DtOf<V>::value; a.on_device = 1;
+  b.nrow = a.ncol; b.ncol = ncol; b.nnz = (int64_t)k * ncol; b.nzc = ncol;
+  b.cp = sel_cp.p; b.ir = sel_ir.p; b.idx_bytes = 4; b.ptr_bytes = 8; b.val = nullptr;
+  b.val_type = DtOf<V>::value; b.on_device = 1;
+  int64_t m = 0;
+  cbg_status s = dispatch_sr<V, true>(ctx, &a, &b, sr, flags, C, &m);
+  HIPCHK(hipStreamSynchronize(st));   // the DevBufs above are released on return
   return s;
 }
 
-extern "C" cbg_status cbg_merge(cbg_ctx* ctx, const cbg_csc_result* parts, int32_t nparts, cbg_semiring sr,
-                                cbg_dtype val_type, uint32_t flags, cbg_csc_result* C) {
-  (void)ctx; (void)parts; (void)nparts; (void)sr; (void)val_type; (void)flags; (void)C;
-  return CBG_EUNSUP;   // device multiway merge: see DESIGN.md (next milestone)
-}
+}  // namespace host
+}  // namespace cbg
+
+
+
+// per-dtype entry points (defined in inst_<dtype>.hip, one translation unit each)
+#define CBG_DECLARE_DT(SUF)                                                                            \
+  cbg_status cbg_dispatch_##SUF(cbg_ctx*, const cbg_dcsc_view*, const cbg_dcsc_view*, cbg_semiring, uint32_t, \
+                                cbg_csc_result*, int64_t*);                                            \
+  cbg_status cbg_merge_##SUF(cbg_ctx*, const cbg_csc_result*, int32_t, cbg_semiring, uint32_t, cbg_csc_result*);
+CBG_DECLARE_DT(f64)
+CBG_DECLARE_DT(f32)
+CBG_DECLARE_DT(i64)
+CBG_DECLARE_DT(i32)
+CBG_DECLARE_DT(b8)

@@ -33,6 +33,7 @@
 #include "semiring.hpp"
 
 namespace cbg {
+namespace {  // internal linkage: every translation unit instantiates its own kernels
 
 constexpr int kWave = 64;
 constexpr int32_t kEmpty = -1;
@@ -486,7 +487,7 @@ struct NumOut {
 template <int NT, class SRT, typename V>
 __device__ __forceinline__ void compact_hash_runs(const int32_t* keys, const typename SRT::Acc* vals, int Tcap,
                                                   int tid, int occ_before_chunk, int c0, int c1, int64_t outbase,
-                                                  const V* bval, int32_t* orow, V* oval) {
+                                                  const V* aval, const V* bval, int32_t* orow, V* oval) {
   int occ = occ_before_chunk;
   for (int s = c0; s < c1; ++s) {
     const int32_t key = keys[s];
@@ -501,7 +502,7 @@ __device__ __forceinline__ void compact_hash_runs(const int32_t* keys, const typ
     }
     const int64_t o = outbase + (occ - (s - rs)) + smaller;
     orow[o] = key;
-    oval[o] = SRT::out(vals[s], bval);
+    oval[o] = SRT::out(vals[s], aval, bval);
     ++occ;
   }
 }
@@ -533,7 +534,7 @@ __global__ void __launch_bounds__(256) k_num_wave(const int32_t* __restrict__ li
     int ovf = 0, aerr = 0;
     for_each_multiply<kWave, true>(B.cp[j], B.cp[j + 1], A.cp, B.ir, s_lq[w], nullptr, [&](int64_t q, int64_t b) {
       const int32_t r = A.ir[q];
-      const Acc x = SRT::mul(load_val(A.val, q), load_val(B.val, b), b);
+      const Acc x = SRT::mul(load_val(A.val, q), load_val(B.val, b), q, b);
       if (dense) {
         const int32_t o = r - sp.x;
         const uint32_t bit = 1u << (o & 31);
@@ -562,7 +563,7 @@ __global__ void __launch_bounds__(256) k_num_wave(const int32_t* __restrict__ li
         wd &= wd - 1;
         const int rr = l * 32 + bpos;
         out.row[ob + o] = sp.x + rr;
-        out.val[ob + o] = SRT::out(t.vals[rr], B.val);
+        out.val[ob + o] = SRT::out(t.vals[rr], A.val, B.val);
         ++o;
       }
     } else {
@@ -572,7 +573,7 @@ __global__ void __launch_bounds__(256) k_num_wave(const int32_t* __restrict__ li
       int occ = 0;
       for (int s = c0; s < c1; ++s) occ += (t.keys[s] != kEmpty);
       const int ex = wave_incl_scan(occ) - occ;
-      compact_hash_runs<kWave, SRT, V>(t.keys, t.vals, TC, l, ex, c0, c1, ob, B.val, out.row, out.val);
+      compact_hash_runs<kWave, SRT, V>(t.keys, t.vals, TC, l, ex, c0, c1, ob, A.val, B.val, out.row, out.val);
     }
     wave_sync();
   }
@@ -604,7 +605,7 @@ __global__ void __launch_bounds__(NT) k_num_block(const int32_t* __restrict__ li
     int ovf = 0, aerr = 0;
     for_each_multiply<NT, false>(B.cp[j], B.cp[j + 1], A.cp, B.ir, lq, &misc[0], [&](int64_t q, int64_t b) {
       const int32_t r = A.ir[q];
-      const Acc x = SRT::mul(load_val(A.val, q), load_val(B.val, b), b);
+      const Acc x = SRT::mul(load_val(A.val, q), load_val(B.val, b), q, b);
       if (dense) {
         const int32_t o = r - sp.x;
         const uint32_t bit = 1u << (o & 31);
@@ -632,7 +633,7 @@ __global__ void __launch_bounds__(NT) k_num_block(const int32_t* __restrict__ li
         wd &= wd - 1;
         const int rr = threadIdx.x * 32 + bpos;
         out.row[ob + o] = sp.x + rr;
-        out.val[ob + o] = SRT::out(vals[rr], B.val);
+        out.val[ob + o] = SRT::out(vals[rr], A.val, B.val);
         ++o;
       }
     } else {
@@ -642,7 +643,7 @@ __global__ void __launch_bounds__(NT) k_num_block(const int32_t* __restrict__ li
       for (int s = c0; s < c1; ++s) occ += (keys[s] != kEmpty);
       int tot;
       const int ex = block_excl_scan<NT>(occ, misc + 3, &tot);
-      compact_hash_runs<NT, SRT, V>(keys, vals, TC, threadIdx.x, ex, c0, c1, ob, B.val, out.row, out.val);
+      compact_hash_runs<NT, SRT, V>(keys, vals, TC, threadIdx.x, ex, c0, c1, ob, A.val, B.val, out.row, out.val);
     }
     if (threadIdx.x == 0 && misc[2]) atomicOr(out.adderr, 1);
     __syncthreads();
@@ -718,7 +719,7 @@ __global__ void __launch_bounds__(NT) k_window(const int32_t* __restrict__ list,
             } else {
               const uint32_t old = atomicOr(&bits[o >> 5], bit);
               if (SRT::kAddIsError && (old & bit)) aerr = 1;
-              SRT::acc(&vals[o], SRT::mul(load_val(A.val, q), bv, b));
+              SRT::acc(&vals[o], SRT::mul(load_val(A.val, q), bv, q, b));
             }
             ++q;
             if (q >= qe) { r = INT32_MAX; break; }
@@ -751,7 +752,7 @@ __global__ void __launch_bounds__(NT) k_window(const int32_t* __restrict__ list,
               } else {
                 const uint32_t old = atomicOr(&bits[o >> 5], bit);
                 if (SRT::kAddIsError && (old & bit)) aerr = 1;
-                SRT::acc(&vals[o], SRT::mul(load_val(A.val, qq), bv, sb));
+                SRT::acc(&vals[o], SRT::mul(load_val(A.val, qq), bv, qq, sb));
               }
             }
             const unsigned long long m = __ballot(in);
@@ -794,7 +795,7 @@ __global__ void __launch_bounds__(NT) k_window(const int32_t* __restrict__ list,
             wd &= wd - 1;
             const int rr = (threadIdx.x * PW + s) * 32 + bpos;
             out.row[outpos + o] = (int32_t)r0 + rr;
-            out.val[outpos + o] = SRT::out(vals[rr], B.val);
+            out.val[outpos + o] = SRT::out(vals[rr], A.val, B.val);
             ++o;
           }
         }
@@ -834,4 +835,5 @@ __global__ void k_dcsc_to_csc(int64_t ncol, int64_t nzc, const int64_t* __restri
   }
 }
 
+}  // namespace
 }  // namespace cbg

@@ -1,0 +1,98 @@
+"""CPU-only checks of the C ABI library: it loads without a GPU, exports exactly what include/cbgpu.h
+declares, and its host-side pieces (status strings, generator) work without a device."""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from helpers import REPO
+
+HEADER = os.path.join(REPO, "include", "cbgpu.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(cbg_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_loads_and_exports_every_declared_symbol():
+    from combblas_amd import _abi
+    lib = _abi.lib()
+    names = declared_functions()
+    assert len(names) >= 15
+    out = subprocess.run(["nm", "-D", "--defined-only", _abi.LIB_PATH], capture_output=True, text=True).stdout
+    exported = set(re.findall(r" T (cbg_\w+)", out))
+    missing = [n for n in names if n not in exported]
+    assert not missing, f"declared in cbgpu.h but not exported: {missing}"
+    for n in names:
+        assert hasattr(lib, n)
+    # the python binding declares every entry point with a signature
+    assert set(names) == set(_abi.SIGNATURES), set(names) ^ set(_abi.SIGNATURES)
+
+
+def test_no_oracle_in_product_library():
+    """The product library must not link or contain the oracle (no CPU fallback path)."""
+    from combblas_amd import _abi
+    out = subprocess.run(["nm", "-D", _abi.LIB_PATH], capture_output=True, text=True).stdout
+    assert "orc_" not in out
+    ldd = subprocess.run(["ldd", _abi.LIB_PATH], capture_output=True, text=True).stdout
+    assert "oracle" not in ldd
+
+
+def test_abi_version_and_strerror():
+    from combblas_amd import _abi
+    lib = _abi.lib()
+    assert lib.cbg_abi_version() == 1
+    assert b"3002" in lib.cbg_strerror(3002)
+    assert b"BoolCopy" in lib.cbg_strerror(13)
+
+
+def test_struct_layouts_match_header():
+    from combblas_amd import _abi
+    # cbg_dcsc_view: 4 int64, 3 pointers, 2 int32, pointer, enum, int32 -> 80 bytes on LP64
+    assert ctypes.sizeof(_abi.DcscView) == 80
+    assert ctypes.sizeof(_abi.CscResult) == 72
+    assert ctypes.sizeof(_abi.Profile) == 6 * 8 + 2 * 8 + 16 * 8
+
+
+def test_init_without_gpu_fails_loudly():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    import combblas_amd as cb
+    with pytest.raises(cb.CbgError) as ei:
+        cb.Context(0)
+    assert ei.value.status == 12
+
+
+def test_rmat_generator_properties():
+    import combblas_amd as cb
+    n, cp, ir, val = cb.generate_rmat_host(12, 16, seed=3)
+    assert n == 4096 and len(cp) == n + 1 and cp[0] == 0
+    assert val.sum() == 16 * 4096                          # multiplicities add up to all edges
+    assert np.all(np.diff(cp) >= 0)
+    for j in range(0, n, 97):
+        seg = ir[cp[j]:cp[j + 1]]
+        assert np.all(np.diff(seg) > 0)                    # rows sorted, duplicates merged
+    n2, cp2, ir2, val2 = cb.generate_rmat_host(12, 16, seed=3)
+    assert np.array_equal(cp, cp2) and np.array_equal(ir, ir2) and np.array_equal(val, val2)
+    n3, cp3, _, _ = cb.generate_rmat_host(12, 16, seed=4)
+    assert not np.array_equal(cp, cp3)
+
+
+def test_rmat_statistics_match_reference_generator():
+    """Our counter-based stream must reproduce the reference generator's product statistics
+    (G500 s12 ef16 A*A has 2,300,751 multiplies and 762,183 nnz, within a few %)."""
+    import combblas_amd as cb
+    from helpers import Csc, oracle_spgemm
+    n, cp, ir, val = cb.generate_rmat_host(12, 16, seed=1)
+    A = Csc(n, n, cp, ir, val)
+    C, mults, rc = oracle_spgemm(A, A, "plus_times", "f64")
+    assert rc == 0
+    assert abs(len(ir) / 48_574 - 1) < 0.05              # nnz(A) of the reference G500 s12
+    assert abs(mults / 2_300_751 - 1) < 0.15
+    assert abs(C.nnz / 762_183 - 1) < 0.15
