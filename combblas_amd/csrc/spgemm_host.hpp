@@ -79,6 +79,7 @@ struct cbg_ctx {
   cbg_profile prof{};
   // workspace (grow-only)
   DevBuf flop, span, cnt, list, hist, cursor, scan_tiles, scalars, cur, nxt, ovf_list, stageA[5], stageB[5];
+  DevBuf split_idx, long_cols, split_tab, heavy_cols, sub, units, ucnt, uspan, ulist, fb_units, fb_list, uovf_list;
 };
 
 inline hipError_t launch_cfg_lds(const void* fn, size_t lds) {
@@ -169,73 +170,102 @@ inline int64_t grid_for(int64_t items, int64_t per_block, int64_t cap) {
   return std::max<int64_t>(1, std::min<int64_t>((items + per_block - 1) / per_block, cap));
 }
 
+// ------------------------------------------------------------------------------- binning
 struct Classes {
-  std::vector<unsigned long long> hist;   // per class counts
+  std::vector<unsigned long long> hist;   // per class counts (+ [31] = items above the heavy bound)
   std::vector<unsigned long long> off;    // exclusive offsets
 };
 
-inline cbg_status bin_columns(cbg_ctx* ctx, int64_t ncol, const int64_t* cnt, const int2* span, BinParams bp,
-                       int32_t* list, Classes* cl) {
-  hipStream_t st = ctx->stream;
+// pass 0 of a binning into hist_dev[0..63] (no sync)
+inline void bin_count(hipStream_t st, int64_t n, const int64_t* cnt, const int2* span, BinParams bp,
+                      unsigned long long* hist_dev, int32_t* list) {
+  const int64_t g = (n + 255) / 256;
+  if (g > 0) k_bin<<<(int)g, 256, 0, st>>>(n, cnt, span, bp, 0, kHeavy, hist_dev, hist_dev + 32, list);
+}
+// after the host has hist: offsets, cursors, pass 1
+inline cbg_status bin_fill(hipStream_t st, int64_t n, const int64_t* cnt, const int2* span, BinParams bp,
+                           unsigned long long* hist_dev, const unsigned long long* hist_host, int32_t* list,
+                           Classes* cl) {
   const int ncls = bp.nwave + bp.nblock + 2;
-  HIPCHK(ctx->hist.reserve(sizeof(unsigned long long) * 64));
-  unsigned long long* hist = ctx->hist.as<unsigned long long>();
-  unsigned long long* cursor = hist + 32;
-  HIPCHK(hipMemsetAsync(hist, 0, sizeof(unsigned long long) * 64, st));
-  const int64_t g = (ncol + 255) / 256;
-  k_bin<<<(int)g, 256, 0, st>>>(ncol, cnt, span, bp, 0, hist, cursor, list);
-  cl->hist.assign(ncls, 0);
-  HIPCHK(hipMemcpyAsync(cl->hist.data(), hist, sizeof(unsigned long long) * ncls, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipStreamSynchronize(st));
+  cl->hist.assign(hist_host, hist_host + 32);
   cl->off.assign(ncls + 1, 0);
   for (int c = 0; c < ncls; ++c) cl->off[c + 1] = cl->off[c] + cl->hist[c];
-  HIPCHK(hipMemcpyAsync(cursor, cl->off.data(), sizeof(unsigned long long) * ncls, hipMemcpyHostToDevice, st));
-  k_bin<<<(int)g, 256, 0, st>>>(ncol, cnt, span, bp, 1, hist, cursor, list);
+  HIPCHK(hipMemcpyAsync(hist_dev + 32, cl->off.data(), sizeof(unsigned long long) * ncls, hipMemcpyHostToDevice, st));
+  const int64_t g = (n + 255) / 256;
+  if (g > 0) k_bin<<<(int)g, 256, 0, st>>>(n, cnt, span, bp, 1, kHeavy, hist_dev, hist_dev + 32, list);
   return CBG_OK;
 }
 
-// ------------------------------------------------------------------------------- symbolic launch
+// ------------------------------------------------------------------------------- launch helpers
 template <int LOGT>
-void launch_sym_wave(hipStream_t st, const int32_t* l, int64_t n, const DevCsc<int32_t>& A, const int64_t* Bcp,
-                     const int32_t* Bir, const int2* span, int64_t* nnz) {
-  k_sym_wave<LOGT><<<(int)grid_for(n, 4, kMaxGrid * 2), 256, 0, st>>>(l, n, A.cp, A.ir, Bcp, Bir, span, nnz);
+void launch_sym_wave(hipStream_t st, const int32_t* l, int64_t n, const int64_t* Acp, const int32_t* Air,
+                     const int64_t* Bcp, const int32_t* Bir, const int2* span, int64_t* nnz) {
+  k_sym_wave<LOGT><<<(int)grid_for(n, 4, kMaxGrid * 2), 256, 0, st>>>(l, n, Acp, Air, Bcp, Bir, span, nnz);
 }
-template <int LOGT>
+template <int LOGT, int NT>
 hipError_t launch_sym_block(hipStream_t st, const int32_t* l, int64_t n, const int64_t* Acp, const int32_t* Air,
-                            const int64_t* Bcp, const int32_t* Bir, const int2* span, int64_t* nnz) {
-  const size_t lds = (size_t)(1 << LOGT) * 4 + kBlockNT * 4 + 64;
-  hipError_t e = launch_cfg_lds((const void*)k_sym_block<LOGT, kBlockNT>, lds);
+                            const int64_t* Bcp, const int32_t* Bir, const int2* span, int64_t* nnz,
+                            const HeavyOut& ho) {
+  const size_t lds = (size_t)(1 << LOGT) * 4 + (size_t)NT * 17 + (size_t)(kMaxSub + 2) * 4 + 64;
+  hipError_t e = launch_cfg_lds((const void*)k_sym_block<LOGT, NT>, lds);
   if (e != hipSuccess) return e;
-  k_sym_block<LOGT, kBlockNT><<<(int)grid_for(n, 1, kMaxGrid), kBlockNT, lds, st>>>(l, n, Acp, Air, Bcp, Bir, span, nnz);
+  k_sym_block<LOGT, NT><<<(int)grid_for(n, 1, kMaxGrid), NT, lds, st>>>(l, n, Acp, Air, Bcp, Bir, span, nnz, ho);
   return hipGetLastError();
 }
-
-template <int LOGT, class SRT, typename V>
-void launch_num_wave(hipStream_t st, const int32_t* l, int64_t n, const DevCsc<V>& A, const DevCsc<V>& B,
-                     const int2* span, const NumOut<V>& o) {
-  k_num_wave<SRT, V, LOGT><<<(int)grid_for(n, 4, kMaxGrid * 2), 256, 0, st>>>(l, n, A, B, span, o);
+template <int LOGT, class SRT, typename V, bool UNIT>
+void launch_num_wave(hipStream_t st, const int32_t* l, int64_t n, const Unit* units, const DevCsc<V>& A,
+                     const DevCsc<V>& B, const int2* span, const int64_t* colptr, const Split& spl,
+                     const NumOut<V>& o) {
+  k_num_wave<SRT, V, LOGT, UNIT><<<(int)grid_for(n, 4, kMaxGrid * 2), 256, 0, st>>>(l, n, units, A, B, span, colptr,
+                                                                                    spl, o);
 }
-template <int LOGT, class SRT, typename V>
-hipError_t launch_num_block(hipStream_t st, const int32_t* l, int64_t n, const DevCsc<V>& A, const DevCsc<V>& B,
-                            const int2* span, const NumOut<V>& o) {
-  using Acc = typename SRT::Acc;
-  const size_t TC = (size_t)(1 << LOGT) + kBlockNT;
-  const size_t lds = TC * (sizeof(Acc) + 4) + kBlockNT * 4 + 64;
-  hipError_t e = launch_cfg_lds((const void*)k_num_block<SRT, V, LOGT, kBlockNT>, lds);
+template <int LOGT, int NT, class SRT, typename V, bool UNIT>
+hipError_t launch_num_block(hipStream_t st, const int32_t* l, const int* n_dev, int64_t n, int64_t grid,
+                            const Unit* units, const DevCsc<V>& A, const DevCsc<V>& B, const int2* span,
+                            const int64_t* colptr, const Split& spl, const NumOut<V>& o) {
+  const size_t lds = num_block_lds<SRT, V, LOGT, NT>();
+  hipError_t e = launch_cfg_lds((const void*)k_num_block<SRT, V, LOGT, NT, UNIT>, lds);
   if (e != hipSuccess) return e;
-  k_num_block<SRT, V, LOGT, kBlockNT><<<(int)grid_for(n, 1, kMaxGrid), kBlockNT, lds, st>>>(l, n, A, B, span, o);
+  k_num_block<SRT, V, LOGT, NT, UNIT><<<(int)grid, NT, lds, st>>>(l, n_dev, n, units, A, B, span, colptr, spl, o);
   return hipGetLastError();
 }
 template <int MODE, class SRT, typename V, int W>
 hipError_t launch_window(hipStream_t st, const int32_t* l, const int* count_dev, int64_t count_host, int64_t grid,
-                         const DevCsc<V>& A, const DevCsc<V>& B, const int2* span, int64_t* cur, int32_t* nxt,
-                         int64_t* nnz, const NumOut<V>& o) {
-  using Acc = typename SRT::Acc;
-  const size_t lds = (MODE == 1 ? (size_t)W * sizeof(Acc) : 0) + (size_t)(W / 32) * 4 + kWinNT * 4 + 64;
+                         const DevCsc<V>& A, const DevCsc<V>& B, const int2* span, const int64_t* colptr,
+                         int64_t* cur, int32_t* nxt, int64_t* nnz, const HeavyOut& ho, const NumOut<V>& o) {
+  const size_t lds = window_lds<MODE, SRT, V, kWinNT, W>();
   hipError_t e = launch_cfg_lds((const void*)k_window<MODE, SRT, V, kWinNT, W>, lds);
   if (e != hipSuccess) return e;
-  k_window<MODE, SRT, V, kWinNT, W><<<(int)grid, kWinNT, lds, st>>>(l, count_dev, count_host, A, B, span, cur, nxt, nnz, o);
+  k_window<MODE, SRT, V, kWinNT, W><<<(int)grid, kWinNT, lds, st>>>(l, count_dev, count_host, A, B, span, colptr, cur,
+                                                                    nxt, nnz, ho, o);
   return hipGetLastError();
+}
+
+// numeric kernels over one binned list (columns, or units when UNIT)
+template <class SRT, typename V, bool UNIT>
+hipError_t launch_numeric_classes(hipStream_t st, const Classes& cl, const int32_t* list, const Unit* units,
+                                  const DevCsc<V>& A, const DevCsc<V>& B, const int2* span, const int64_t* colptr,
+                                  const Split& spl, const NumOut<V>& o) {
+  auto L = [&](int c) { return list + cl.off[c]; };
+  auto n = [&](int c) { return (int64_t)cl.hist[c]; };
+  if (n(1)) launch_num_wave<6, SRT, V, UNIT>(st, L(1), n(1), units, A, B, span, colptr, spl, o);
+  if (n(2)) launch_num_wave<7, SRT, V, UNIT>(st, L(2), n(2), units, A, B, span, colptr, spl, o);
+  if (n(3)) launch_num_wave<8, SRT, V, UNIT>(st, L(3), n(3), units, A, B, span, colptr, spl, o);
+  if (n(4)) launch_num_wave<9, SRT, V, UNIT>(st, L(4), n(4), units, A, B, span, colptr, spl, o);
+  hipError_t e = hipSuccess;
+  if (n(5) && e == hipSuccess)
+    e = launch_num_block<10, 256, SRT, V, UNIT>(st, L(5), nullptr, n(5), grid_for(n(5), 1, kMaxGrid), units, A, B,
+                                                span, colptr, spl, o);
+  if (n(6) && e == hipSuccess)
+    e = launch_num_block<11, 256, SRT, V, UNIT>(st, L(6), nullptr, n(6), grid_for(n(6), 1, kMaxGrid), units, A, B,
+                                                span, colptr, spl, o);
+  if (n(7) && e == hipSuccess)
+    e = launch_num_block<12, 512, SRT, V, UNIT>(st, L(7), nullptr, n(7), grid_for(n(7), 1, kMaxGrid), units, A, B,
+                                                span, colptr, spl, o);
+  if (n(8) && e == hipSuccess)
+    e = launch_num_block<13, 1024, SRT, V, UNIT>(st, L(8), nullptr, n(8), grid_for(n(8), 1, kMaxGrid), units, A, B,
+                                                 span, colptr, spl, o);
+  return e;
 }
 
 // ------------------------------------------------------------------------------- the product
@@ -271,52 +301,74 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
   if ((s = stage<V>(ctx, Av, ctx->stageA, &A)) != CBG_OK) return s;
   if ((s = stage<V>(ctx, Bv, ctx->stageB, &B)) != CBG_OK) return s;
 
+  // subwindow geometry of the row space (heavy-column units)
+  int32_t slog = 13;
+  while (((M - 1) >> slog) + 1 > kMaxSub) ++slog;
+  const int32_t nsub = (int32_t)(((M - 1) >> slog) + 1);
+
   // 1. column statistics
   HIPCHK(ctx->flop.reserve(sizeof(int64_t) * (N + 1)));
   HIPCHK(ctx->span.reserve(sizeof(int2) * (N + 1)));
   HIPCHK(ctx->cnt.reserve(sizeof(int64_t) * (N + 1)));
   HIPCHK(ctx->list.reserve(sizeof(int32_t) * (N + 1)));
-  HIPCHK(ctx->scalars.reserve(64));
-  HIPCHK(ctx->cur.reserve(sizeof(int64_t) * (B.nnz + 1)));
-  HIPCHK(ctx->nxt.reserve(sizeof(int32_t) * (B.nnz + 1)));
+  HIPCHK(ctx->hist.reserve(sizeof(unsigned long long) * 256));
+  HIPCHK(ctx->scalars.reserve(128));
   HIPCHK(ctx->ovf_list.reserve(sizeof(int32_t) * (N + 1)));
+  HIPCHK(ctx->split_idx.reserve(sizeof(int32_t) * (A.ncol + 1)));
+  HIPCHK(ctx->long_cols.reserve(sizeof(int32_t) * (A.ncol + 1)));
   int64_t* flop = ctx->flop.as<int64_t>();
   int2* span = ctx->span.as<int2>();
   int64_t* nnz = ctx->cnt.as<int64_t>();
   int32_t* list = ctx->list.as<int32_t>();
-  unsigned long long* sc = ctx->scalars.as<unsigned long long>();   // [0] mults, [1] nnzC, [2] adderr|ovf
-  int* adderr = (int*)(sc + 2);
-  int* ovf_n = adderr + 1;
-  HIPCHK(hipMemsetAsync(sc, 0, 64, st));
+  unsigned long long* hist = ctx->hist.as<unsigned long long>();
+  // scalars: [0] multiplies, [1] nnz(C); ints from byte 16: heavy n, nlong, adderr, col ovf, unit ovf,
+  // fallback units, fallback-unit ovf
+  unsigned long long* sc = ctx->scalars.as<unsigned long long>();
+  int* si = (int*)(sc + 2);
+  int *heavy_n = si + 0, *nlong = si + 1, *adderr = si + 2, *ovf_n = si + 3, *uovf_n = si + 4, *fb_n = si + 5,
+      *fb_ovf_n = si + 6;
+  HIPCHK(hipMemsetAsync(sc, 0, 128, st));
   HIPCHK(hipMemsetAsync(nnz, 0, sizeof(int64_t) * N, st));
-  k_col_stats<V><<<(int)((N * 16 + 255) / 256), 256, 0, st>>>(N, A.cp, A.ir, B.cp, B.ir, flop, span, sc);
+  k_col_stats<<<(int)((N * 16 + 255) / 256), 256, 0, st>>>(N, A.cp, A.ir, B.cp, B.ir, flop, span, sc);
+  k_split_assign<<<(int)grid_for(A.ncol, 256, kMaxGrid), 256, 0, st>>>(A.ncol, A.cp, ctx->split_idx.as<int32_t>(),
+                                                                        ctx->long_cols.as<int32_t>(), nlong);
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(ctx->ev[1], st));
 
   // 2. symbolic binning + kernels
   Classes cs;
   BinParams sbp{kSymWave, kSymBlock, 64, 1};
-  if ((s = bin_columns(ctx, N, flop, span, sbp, list, &cs)) != CBG_OK) return s;
+  unsigned long long hh[64];
+  HIPCHK(hipMemsetAsync(hist, 0, sizeof(unsigned long long) * 64, st));
+  bin_count(st, N, flop, span, sbp, hist, list);
+  HIPCHK(hipMemcpyAsync(hh, hist, sizeof(unsigned long long) * 32, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  if ((s = bin_fill(st, N, flop, span, sbp, hist, hh, list, &cs)) != CBG_OK) return s;
+  const int64_t hcap = (int64_t)cs.hist[31];
+  HIPCHK(ctx->heavy_cols.reserve(sizeof(int32_t) * (hcap + 1)));
+  HIPCHK(ctx->sub.reserve(sizeof(int32_t) * (hcap * nsub + 1)));
+  HeavyOut ho{heavy_n, ctx->heavy_cols.as<int32_t>(), ctx->sub.as<int32_t>(), nsub, slog};
   HIPCHK(hipEventRecord(ctx->ev[2], st));
   {
     auto L = [&](int c) { return list + cs.off[c]; };
     auto n = [&](int c) { return (int64_t)cs.hist[c]; };
-    DevCsc<int32_t> Ai{A.nrow, A.ncol, A.nnz, A.cp, A.ir, nullptr};
-    if (n(1)) launch_sym_wave<6>(st, L(1), n(1), Ai, B.cp, B.ir, span, nnz);
-    if (n(2)) launch_sym_wave<7>(st, L(2), n(2), Ai, B.cp, B.ir, span, nnz);
-    if (n(3)) launch_sym_wave<8>(st, L(3), n(3), Ai, B.cp, B.ir, span, nnz);
-    if (n(4)) launch_sym_wave<9>(st, L(4), n(4), Ai, B.cp, B.ir, span, nnz);
-    if (n(5)) launch_sym_wave<10>(st, L(5), n(5), Ai, B.cp, B.ir, span, nnz);
+    if (n(1)) launch_sym_wave<6>(st, L(1), n(1), A.cp, A.ir, B.cp, B.ir, span, nnz);
+    if (n(2)) launch_sym_wave<7>(st, L(2), n(2), A.cp, A.ir, B.cp, B.ir, span, nnz);
+    if (n(3)) launch_sym_wave<8>(st, L(3), n(3), A.cp, A.ir, B.cp, B.ir, span, nnz);
+    if (n(4)) launch_sym_wave<9>(st, L(4), n(4), A.cp, A.ir, B.cp, B.ir, span, nnz);
+    if (n(5)) launch_sym_wave<10>(st, L(5), n(5), A.cp, A.ir, B.cp, B.ir, span, nnz);
     hipError_t e = hipSuccess;
-    if (n(6) && e == hipSuccess) e = launch_sym_block<11>(st, L(6), n(6), A.cp, A.ir, B.cp, B.ir, span, nnz);
-    if (n(7) && e == hipSuccess) e = launch_sym_block<12>(st, L(7), n(7), A.cp, A.ir, B.cp, B.ir, span, nnz);
-    if (n(8) && e == hipSuccess) e = launch_sym_block<13>(st, L(8), n(8), A.cp, A.ir, B.cp, B.ir, span, nnz);
-    if (n(9) && e == hipSuccess) e = launch_sym_block<14>(st, L(9), n(9), A.cp, A.ir, B.cp, B.ir, span, nnz);
-    if (n(10) && e == hipSuccess) e = launch_sym_block<15>(st, L(10), n(10), A.cp, A.ir, B.cp, B.ir, span, nnz);
+    if (n(6) && e == hipSuccess) e = launch_sym_block<11, 256>(st, L(6), n(6), A.cp, A.ir, B.cp, B.ir, span, nnz, ho);
+    if (n(7) && e == hipSuccess) e = launch_sym_block<12, 256>(st, L(7), n(7), A.cp, A.ir, B.cp, B.ir, span, nnz, ho);
+    if (n(8) && e == hipSuccess) e = launch_sym_block<13, 512>(st, L(8), n(8), A.cp, A.ir, B.cp, B.ir, span, nnz, ho);
+    if (n(9) && e == hipSuccess) e = launch_sym_block<14, 1024>(st, L(9), n(9), A.cp, A.ir, B.cp, B.ir, span, nnz, ho);
+    if (n(10) && e == hipSuccess) e = launch_sym_block<15, 1024>(st, L(10), n(10), A.cp, A.ir, B.cp, B.ir, span, nnz, ho);
     if (n(11) && e == hipSuccess) {
-      NumOut<V> dummy{};
+      HIPCHK(ctx->cur.reserve(sizeof(int64_t) * (B.nnz + 1)));
+      HIPCHK(ctx->nxt.reserve(sizeof(int32_t) * (B.nnz + 1)));
       e = launch_window<0, SRT, V, kSymWinRows>(st, L(11), nullptr, n(11), grid_for(n(11), 1, 1024), A, B, span,
-                                                ctx->cur.as<int64_t>(), ctx->nxt.as<int32_t>(), nnz, dummy);
+                                                nullptr, ctx->cur.as<int64_t>(), ctx->nxt.as<int32_t>(), nnz, ho,
+                                                NumOut<V>{});
     }
     if (e != hipSuccess) { fprintf(stderr, "cbgpu: symbolic launch: %s\n", hipGetErrorString(e)); return CBG_EDEVICE; }
     HIPCHK(hipGetLastError());
@@ -330,46 +382,87 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
   k_scan_sums<<<1, 1024, 0, st>>>(ntiles, ctx->scan_tiles.as<int64_t>(), (int64_t*)(sc + 1));
   k_scan_apply<<<(int)ntiles, 256, 0, st>>>(N, nnz, ctx->scan_tiles.as<int64_t>(), colptr);
   HIPCHK(hipGetLastError());
-  unsigned long long hsc[2];
-  HIPCHK(hipMemcpyAsync(hsc, sc, 16, hipMemcpyDeviceToHost, st));
+  unsigned long long hsc[4];
+  HIPCHK(hipMemcpyAsync(hsc, sc, 32, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
   HIPCHK(hipEventRecord(ctx->ev[4], st));
   const int64_t mults = (int64_t)hsc[0], nnzc = (int64_t)hsc[1];
+  const int H = ((int*)&hsc[2])[0], NL = ((int*)&hsc[2])[1];
   pf.multiplies = mults; pf.nnz_out = nnzc;
   HIPCHK(own->ir.reserve(sizeof(int32_t) * (nnzc + 1)));
   HIPCHK(own->val.reserve(sizeof(V) * (nnzc + 1)));
 
-  // 4. numeric binning + kernels
-  Classes cn;
+  // 4. heavy columns -> units (split table + greedy subwindow grouping)
+  Split spl{ctx->split_idx.as<int32_t>(), nullptr, nsub, slog};
+  const int64_t nunit_cap = (int64_t)H * nsub;
+  Unit* units = nullptr;
+  if (H > 0) {
+    HIPCHK(ctx->split_tab.reserve(sizeof(int32_t) * ((int64_t)NL * (nsub + 1) + 1)));
+    spl.tab = ctx->split_tab.as<int32_t>();
+    if (NL > 0)
+      k_split_fill<<<(int)grid_for(NL, 4, kMaxGrid * 2), 256, 0, st>>>(NL, ctx->long_cols.as<int32_t>(), A.cp, A.ir,
+                                                                        ctx->split_tab.as<int32_t>(), nsub, slog);
+    HIPCHK(ctx->units.reserve(sizeof(Unit) * (nunit_cap + 1)));
+    HIPCHK(ctx->ucnt.reserve(sizeof(int64_t) * (nunit_cap + 1)));
+    HIPCHK(ctx->uspan.reserve(sizeof(int2) * (nunit_cap + 1)));
+    HIPCHK(ctx->ulist.reserve(sizeof(int32_t) * (nunit_cap + 1)));
+    HIPCHK(ctx->fb_units.reserve(sizeof(Unit) * (nunit_cap + 1)));
+    HIPCHK(ctx->fb_list.reserve(sizeof(int32_t) * (nunit_cap + 1)));
+    HIPCHK(ctx->uovf_list.reserve(sizeof(int32_t) * (nunit_cap + 1)));
+    HIPCHK(hipMemsetAsync(ctx->ucnt.p, 0, sizeof(int64_t) * nunit_cap, st));
+    units = ctx->units.as<Unit>();
+    k_build_units<<<(H + 255) / 256, 256, 0, st>>>(H, ctx->heavy_cols.as<int32_t>(), ctx->sub.as<int32_t>(), nsub,
+                                                   slog, span, colptr, units, ctx->ucnt.as<int64_t>(),
+                                                   ctx->uspan.as<int2>(), nnz);
+    HIPCHK(hipGetLastError());
+  }
+
+  // 5. numeric binning (columns and units, one host sync) + kernels
+  Classes cn, cu;
   BinParams nbp{kNumWave, kNumBlock, 64, 0};
-  if ((s = bin_columns(ctx, N, nnz, span, nbp, list, &cn)) != CBG_OK) return s;
-  for (int c = 0; c < (int)cn.hist.size() && c < 16; ++c) pf.bins[c] = (int64_t)cn.hist[c];
-  NumOut<V> o{colptr, own->ir.as<int32_t>(), own->val.as<V>(), adderr, ovf_n, ctx->ovf_list.as<int32_t>()};
+  HIPCHK(hipMemsetAsync(hist, 0, sizeof(unsigned long long) * 128, st));
+  bin_count(st, N, nnz, span, nbp, hist, list);
+  if (H > 0) bin_count(st, nunit_cap, ctx->ucnt.as<int64_t>(), ctx->uspan.as<int2>(), nbp, hist + 64,
+                       ctx->ulist.as<int32_t>());
+  unsigned long long hn[128];
+  HIPCHK(hipMemcpyAsync(hn, hist, sizeof(unsigned long long) * 128, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  if ((s = bin_fill(st, N, nnz, span, nbp, hist, hn, list, &cn)) != CBG_OK) return s;
+  if (H > 0 && (s = bin_fill(st, nunit_cap, ctx->ucnt.as<int64_t>(), ctx->uspan.as<int2>(), nbp, hist + 64, hn + 64,
+                             ctx->ulist.as<int32_t>(), &cu)) != CBG_OK)
+    return s;
+  for (int c = 0; c < 12; ++c) pf.bins[c] = (int64_t)cn.hist[c];
+  pf.bins[12] = H;
+  for (int c = 1; c < 12 && H > 0; ++c) pf.bins[13] += (int64_t)cu.hist[c];
+  NumOut<V> oc{own->ir.as<int32_t>(), own->val.as<V>(), adderr, ovf_n, ctx->ovf_list.as<int32_t>()};
   {
-    auto L = [&](int c) { return list + cn.off[c]; };
-    auto n = [&](int c) { return (int64_t)cn.hist[c]; };
-    if (n(1)) launch_num_wave<6, SRT, V>(st, L(1), n(1), A, B, span, o);
-    if (n(2)) launch_num_wave<7, SRT, V>(st, L(2), n(2), A, B, span, o);
-    if (n(3)) launch_num_wave<8, SRT, V>(st, L(3), n(3), A, B, span, o);
-    if (n(4)) launch_num_wave<9, SRT, V>(st, L(4), n(4), A, B, span, o);
-    hipError_t e = hipSuccess;
-    if (n(5) && e == hipSuccess) e = launch_num_block<10, SRT, V>(st, L(5), n(5), A, B, span, o);
-    if (n(6) && e == hipSuccess) e = launch_num_block<11, SRT, V>(st, L(6), n(6), A, B, span, o);
-    if (n(7) && e == hipSuccess) e = launch_num_block<12, SRT, V>(st, L(7), n(7), A, B, span, o);
-    if (n(8) && e == hipSuccess) e = launch_num_block<13, SRT, V>(st, L(8), n(8), A, B, span, o);
-    if (n(9) && e == hipSuccess)
-      e = launch_window<1, SRT, V, kWinRows>(st, L(9), nullptr, n(9), grid_for(n(9), 1, 2048), A, B, span,
-                                             ctx->cur.as<int64_t>(), ctx->nxt.as<int32_t>(), nnz, o);
-    // overflow fallback: columns whose order-preserving hash ran past its tail
-    if (e == hipSuccess)
-      e = launch_window<1, SRT, V, kWinRows>(st, ctx->ovf_list.as<int32_t>(), ovf_n, 0, 512, A, B, span,
-                                             ctx->cur.as<int64_t>(), ctx->nxt.as<int32_t>(), nnz, o);
+    hipError_t e = launch_numeric_classes<SRT, V, false>(st, cn, list, nullptr, A, B, span, colptr, spl, oc);
+    if (e == hipSuccess && H > 0) {
+      NumOut<V> ou{own->ir.as<int32_t>(), own->val.as<V>(), adderr, uovf_n, ctx->uovf_list.as<int32_t>()};
+      e = launch_numeric_classes<SRT, V, true>(st, cu, ctx->ulist.as<int32_t>(), units, A, B, span, colptr, spl, ou);
+      // overflowed hash units -> single-subwindow (dense) units
+      if (e == hipSuccess) {
+        k_split_overflow_units<<<(int)grid_for(nunit_cap, 256, 1 << 20), 256, 0, st>>>(
+            uovf_n, ctx->uovf_list.as<int32_t>(), units, ctx->sub.as<int32_t>(), nsub, ctx->fb_units.as<Unit>(), fb_n,
+            ctx->fb_list.as<int32_t>());
+        NumOut<V> of{own->ir.as<int32_t>(), own->val.as<V>(), adderr, fb_ovf_n, ctx->uovf_list.as<int32_t>()};
+        e = launch_num_block<13, 1024, SRT, V, true>(st, ctx->fb_list.as<int32_t>(), fb_n, 0, 256,
+                                                     ctx->fb_units.as<Unit>(), A, B, span, colptr, spl, of);
+      }
+    }
+    // overflowed hash columns -> windowed dense sweep
+    if (e == hipSuccess) {
+      HIPCHK(ctx->cur.reserve(sizeof(int64_t) * (B.nnz + 1)));
+      HIPCHK(ctx->nxt.reserve(sizeof(int32_t) * (B.nnz + 1)));
+      e = launch_window<1, SRT, V, kWinRows>(st, ctx->ovf_list.as<int32_t>(), ovf_n, 0, 512, A, B, span, colptr,
+                                             ctx->cur.as<int64_t>(), ctx->nxt.as<int32_t>(), nnz, ho, oc);
+    }
     if (e != hipSuccess) { fprintf(stderr, "cbgpu: numeric launch: %s\n", hipGetErrorString(e)); return CBG_EDEVICE; }
     HIPCHK(hipGetLastError());
   }
   HIPCHK(hipEventRecord(ctx->ev[5], st));
-  int herr[2];
-  HIPCHK(hipMemcpyAsync(herr, adderr, 8, hipMemcpyDeviceToHost, st));
+  int herr[8];
+  HIPCHK(hipMemcpyAsync(herr, si, sizeof(herr), hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
   float t;
   (void)hipEventElapsedTime(&t, ctx->ev[0], ctx->ev[1]); pf.flops_ms = t;
@@ -378,7 +471,8 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
   (void)hipEventElapsedTime(&t, ctx->ev[3], ctx->ev[4]); pf.scan_ms = t;
   (void)hipEventElapsedTime(&t, ctx->ev[4], ctx->ev[5]); pf.numeric_ms = t;
   (void)hipEventElapsedTime(&t, ctx->ev[0], ctx->ev[5]); pf.total_ms = t;
-  pf.bins[15] = herr[1];   // overflow-fallback columns
+  pf.bins[14] = herr[4];   // overflowed units (re-run dense per subwindow)
+  pf.bins[15] = herr[3];   // overflowed columns (windowed fallback)
   C->nnz = nnzc;
   C->colptr = colptr;
   C->row = own->ir.as<int32_t>();
@@ -386,7 +480,11 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
   C->multiplies = mults;
   C->_owner = own.release();
   if (mult_out) *mult_out = mults;
-  if (herr[0]) return CBG_EADD;
+  if (herr[6]) {   // a fallback unit overflowed: only possible when SUBW > 8192 rows (nrow > 2^24)
+    fprintf(stderr, "cbgpu: %d dense fallback units overflowed\n", herr[6]);
+    return CBG_EUNSUP;
+  }
+  if (herr[2]) return CBG_EADD;
   return CBG_OK;
 }
 

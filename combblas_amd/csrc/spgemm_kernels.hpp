@@ -7,26 +7,28 @@
 // scan, and a numeric pass that emits row-sorted columns straight into the CSC result.
 //
 // Layout in HBM: A and B are CSC (int64 colptr[ncol+1], int32 row[nnz], V val[nnz]); C is CSC of the
-// same form.  Work unit = one output column j (= one column of B).
+// same form.  Work item = one output column j (= one column of B), or, for heavy columns, one UNIT:
+// a row range of column j aligned to SUBW-row subwindows, holding at most kUnitCap outputs.
 //
-// Accumulators live in LDS, one of two modes per (column, row window):
-//   dense  : direct addressing over a row window of at most T rows (value slots + presence bitmap);
+// Accumulators live in LDS, one of two modes per work item:
+//   dense  : direct addressing over a row range of at most T rows (value slots + presence bitmap);
 //            compaction is a bitmap scan, so output is sorted for free.
 //   hash   : open addressing with linear probing.  Numeric uses an ORDER-PRESERVING hash
 //            h(r) = ((r - lo) * T) / span so that every probe run holds keys whose home slots are in
 //            the run: sorting each run locally (run-rank) yields globally sorted output.  Symbolic
 //            (keys only, order irrelevant) uses a multiplicative hash.
 // Every table is sized >= 2x its key count (load <= 0.5).  A numeric hash that would probe past its
-// last slot (adversarial row clustering) reports the column to a fallback list that the windowed
-// dense kernel processes (always correct).
+// last slot (adversarial row clustering) hands the work item to a fallback that is always correct.
 //
-// Parallel decomposition:
-//   wave kernels  : one 64-lane wavefront per column (small columns), per-wave LDS table.
-//   block kernels : one workgroup per column (medium columns), one LDS table.
-//   window kernel : one workgroup per heavy column, sweeping dense row windows of 8192 rows with
-//                   per-B-nonzero cursors (no re-scan, no binary search).
-// Inside a column the multiplies are the union of A-column segments A(:,k), k in B(:,j).  Segments
-// are processed "lane per segment" when short and "wavefront per segment" (coalesced) when long.
+// Heavy columns (nnz > kHeavy): the symbolic pass records the column's nnz per SUBW-row subwindow;
+// units are formed from consecutive subwindows (exact counts -> exact output offsets), and the A
+// segment of a unit is found without search through a split table (relative offsets of every
+// subwindow boundary inside each long A column).  Units are independent, so a column with 250k
+// outputs spreads over ~60 workgroups instead of one.
+//
+// Inside a work item the multiplies are the union of A-column segments A(:,k), k in B(:,j).  Short
+// segments are walked by one lane, long ones by a whole wavefront (coalesced); both issue kUnroll
+// independent loads before their LDS inserts so that each lane keeps several misses in flight.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -37,6 +39,12 @@ namespace {  // internal linkage: every translation unit instantiates its own ke
 
 constexpr int kWave = 64;
 constexpr int32_t kEmpty = -1;
+constexpr int kLong = 64;          // segment length handed to a whole wavefront
+constexpr int kUnroll = 4;         // independent loads in flight per lane
+constexpr int64_t kHeavy = 4096;   // nnz(C(:,j)) above which a column is split into units
+constexpr int64_t kUnitCap = 4096; // max outputs of a multi-subwindow unit (T = 8192, load <= 0.5)
+constexpr int kSplitMin = 64;      // A columns at least this long get split-table rows
+constexpr int kMaxSub = 2048;      // max subwindows per column (SUBW chosen so nrow/SUBW <= kMaxSub)
 
 template <typename V>
 struct DevCsc {
@@ -44,6 +52,29 @@ struct DevCsc {
   const int64_t* cp;
   const int32_t* ir;
   const V* val;   // nullptr => pattern, all values 1/true
+};
+
+// split table: for long A columns, tab[idx[k]*(nsub+1) + s] = (first entry with row >= s*SUBW) - cp[k]
+struct Split {
+  const int32_t* idx;   // per A column: row of tab, or -1
+  const int32_t* tab;
+  int32_t nsub;         // subwindows in the row space
+  int32_t log;          // log2(SUBW)
+};
+
+struct Unit {
+  int32_t j;            // output column
+  int32_t s0, s1;       // subwindows [s0, s1)
+  int32_t cnt;          // outputs
+  int64_t outoff;       // position of the first output in C
+};
+
+// per-item description shared by all numeric/symbolic kernels
+struct Work {
+  int32_t j;
+  int32_t lo, hi;       // row range [lo, hi]
+  int32_t s0, s1;       // unit subwindows, s0 < 0 for a whole column
+  int64_t ob;           // output offset (numeric)
 };
 
 template <typename V>
@@ -93,11 +124,34 @@ __device__ __forceinline__ int block_excl_scan(int v, int* scratch, int* total) 
   return ex;
 }
 
+// first position in [lo, hi) with ir[pos] >= r (ir ascending)
+__device__ __forceinline__ int64_t lower_bound_rows(const int32_t* __restrict__ ir, int64_t lo, int64_t hi, int64_t r) {
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if ((int64_t)ir[mid] < r) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+
+// A segment of unit (s0, s1) inside column k
+__device__ __forceinline__ void unit_bounds(const int64_t* __restrict__ Acp, const int32_t* __restrict__ Air,
+                                            const Split& sp, int32_t k, int32_t s0, int32_t s1, int64_t& a0,
+                                            int64_t& a1) {
+  const int64_t c0 = Acp[k], c1 = Acp[k + 1];
+  if (c1 - c0 >= kSplitMin) {
+    const int32_t* t = sp.tab + (int64_t)sp.idx[k] * (sp.nsub + 1);
+    a0 = c0 + t[s0];
+    a1 = c0 + t[s1];
+  } else {
+    a0 = lower_bound_rows(Air, c0, c1, (int64_t)s0 << sp.log);
+    a1 = lower_bound_rows(Air, a0, c1, (int64_t)s1 << sp.log);
+  }
+}
+
 // ============================================================================ 1. column statistics
 // flop[j] = sum_{k in B(:,j)} nnz(A(:,k))   (estimateFLOP, mtSpGEMM.h:1117-1135)
 // span[j] = [min, max] row index any of those A columns holds (A columns are row-sorted).
 // 16 lanes per column.
-template <typename VB>
 __global__ void __launch_bounds__(256) k_col_stats(int64_t ncol, const int64_t* __restrict__ Acp,
                                                    const int32_t* __restrict__ Air,
                                                    const int64_t* __restrict__ Bcp,
@@ -144,14 +198,14 @@ __global__ void __launch_bounds__(256) k_col_stats(int64_t ncol, const int64_t* 
 
 // ============================================================================ 2. binning
 // Class ids (shared by symbolic and numeric binning, different size meaning):
-//   0              : empty column (nothing to do)
+//   0              : empty item (nothing to do)
 //   1..NWC         : wave classes, table T = 64 << (c-1)
 //   NWC+1..NWC+NBC : block classes, table T = (64 << NWC) << (c-1-NWC)
 //   NWC+NBC+1      : windowed (heavy) class
 struct BinParams {
   int nwave, nblock;     // number of wave / block classes
   int64_t wave_min_T;    // 64
-  int sym;               // 1: symbolic (need = min(2*flop, ceil(span/32)) words); 0: numeric (need = min(2*nnz, span) slots)
+  int sym;               // 1: symbolic (need = min(2*flop, span words)); 0: numeric (need = min(2*nnz, span))
 };
 
 __device__ __forceinline__ int class_of(int64_t need, const BinParams& bp) {
@@ -163,17 +217,19 @@ __device__ __forceinline__ int class_of(int64_t need, const BinParams& bp) {
   return ntot + 1;
 }
 
+// symbolic bitmaps start at a 32-aligned row, hence the extra word
 __device__ __forceinline__ int64_t need_of(int64_t cnt, int2 sp, int sym) {
   if (cnt <= 0 || sp.y < sp.x) return 0;
   const int64_t span = (int64_t)sp.y - sp.x + 1;
-  if (sym) return min(2 * cnt, (span + 31) / 32);
+  if (sym) return min(2 * cnt, (span + 31) / 32 + 1);
   return min(2 * cnt, span);
 }
 
-// pass 0: histogram; pass 1: scatter into class-contiguous list using device cursors
-__global__ void __launch_bounds__(256) k_bin(int64_t ncol, const int64_t* __restrict__ cnt,
+// pass 0: histogram; pass 1: scatter into class-contiguous list using device cursors.
+// hist[31] counts items with cnt > heavy (capacity of the heavy lists).
+__global__ void __launch_bounds__(256) k_bin(int64_t n, const int64_t* __restrict__ cnt,
                                              const int2* __restrict__ span, BinParams bp, int pass,
-                                             unsigned long long* __restrict__ hist,
+                                             int64_t heavy, unsigned long long* __restrict__ hist,
                                              unsigned long long* __restrict__ cursor,
                                              int32_t* __restrict__ list) {
   __shared__ unsigned int s_h[32];
@@ -184,13 +240,16 @@ __global__ void __launch_bounds__(256) k_bin(int64_t ncol, const int64_t* __rest
   const int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   int c = -1;
   unsigned int rank = 0;
-  if (j < ncol) {
-    c = class_of(need_of(cnt[j], span[j], bp.sym), bp);
+  if (j < n) {
+    const int64_t cj = cnt[j];
+    c = class_of(need_of(cj, span[j], bp.sym), bp);
     rank = atomicAdd(&s_h[c], 1u);
+    if (pass == 0 && cj > heavy) atomicAdd(&s_h[31], 1u);
   }
   __syncthreads();
   if (pass == 0) {
-    if (threadIdx.x < ncls && s_h[threadIdx.x]) atomicAdd(&hist[threadIdx.x], (unsigned long long)s_h[threadIdx.x]);
+    if ((threadIdx.x < ncls || threadIdx.x == 31) && s_h[threadIdx.x])
+      atomicAdd(&hist[threadIdx.x], (unsigned long long)s_h[threadIdx.x]);
     return;
   }
   if (threadIdx.x < ncls) s_base[threadIdx.x] = s_h[threadIdx.x] ? atomicAdd(&cursor[threadIdx.x], (unsigned long long)s_h[threadIdx.x]) : 0;
@@ -198,13 +257,101 @@ __global__ void __launch_bounds__(256) k_bin(int64_t ncol, const int64_t* __rest
   if (c >= 0) list[s_base[c] + rank] = (int32_t)j;
 }
 
+// ============================================================================ segment expansion
+// Visit every multiply (q in A segment of b, b in B(:,j)[bs, be)) with NT lanes (a wavefront when
+// WAVE, else the block).  seg(b, a0, a1, bv) gives the A segment and B value of nonzero b;
+// ld(q) loads what an insert needs; ins(item, bv, q, b) inserts it.
+template <typename V>
+struct LongQ {          // LDS queue of long segments (block mode)
+  int64_t* a0;
+  int32_t* len;
+  int32_t* b;           // relative to bs
+  V* bv;
+  int* n;
+};
+
+template <int NT, bool WAVE, typename V, class SegF, class LdF, class InsF>
+__device__ __forceinline__ void for_each_multiply(int64_t bs, int64_t be, int32_t* wq, LongQ<V> lq, SegF seg,
+                                                  LdF ld, InsF ins) {
+  using Item = decltype(ld(int64_t(0)));
+  const int tid = WAVE ? lane_id() : (int)threadIdx.x;
+  for (int64_t base = bs; base < be; base += NT) {
+    const int64_t b = base + tid;
+    int64_t a0 = 0, a1 = 0;
+    V bv = V(0);
+    if (b < be) seg(b, a0, a1, bv);
+    const bool islong = (a1 - a0) >= kLong;
+    if (!islong) {
+      for (int64_t q = a0; q < a1; q += kUnroll) {
+        Item it[kUnroll];
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u)
+          if (q + u < a1) it[u] = ld(q + u);
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u)
+          if (q + u < a1) ins(it[u], bv, q + u, b);
+      }
+    }
+    if constexpr (WAVE) {
+      const unsigned long long m = __ballot(islong);
+      const int pos = __popcll(m & ((1ull << lane_id()) - 1));
+      if (islong) wq[pos] = tid;
+      wave_sync();
+      const int nl = __popcll(m);
+      for (int i = 0; i < nl; ++i) {
+        const int src = wq[i];
+        const int64_t sb = base + src;
+        const int64_t s0 = __shfl(a0, src, kWave), s1 = __shfl(a1, src, kWave);
+        const V sbv = __shfl(bv, src, kWave);
+        for (int64_t q = s0 + lane_id(); q < s1; q += kWave * kUnroll) {
+          Item it[kUnroll];
+#pragma unroll
+          for (int u = 0; u < kUnroll; ++u)
+            if (q + u * kWave < s1) it[u] = ld(q + u * kWave);
+#pragma unroll
+          for (int u = 0; u < kUnroll; ++u)
+            if (q + u * kWave < s1) ins(it[u], sbv, q + u * kWave, sb);
+        }
+      }
+      wave_sync();
+    } else {
+      if (threadIdx.x == 0) *lq.n = 0;
+      __syncthreads();
+      if (islong) {
+        const int e = atomicAdd(lq.n, 1);
+        lq.a0[e] = a0;
+        lq.len[e] = (int32_t)(a1 - a0);
+        lq.b[e] = tid;
+        lq.bv[e] = bv;
+      }
+      __syncthreads();
+      const int nl = *lq.n;
+      constexpr int NW = NT / kWave;
+      for (int e = threadIdx.x / kWave; e < nl; e += NW) {
+        const int64_t sb = base + lq.b[e];
+        const int64_t s0 = lq.a0[e], s1 = s0 + lq.len[e];
+        const V sbv = lq.bv[e];
+        for (int64_t q = s0 + lane_id(); q < s1; q += kWave * kUnroll) {
+          Item it[kUnroll];
+#pragma unroll
+          for (int u = 0; u < kUnroll; ++u)
+            if (q + u * kWave < s1) it[u] = ld(q + u * kWave);
+#pragma unroll
+          for (int u = 0; u < kUnroll; ++u)
+            if (q + u * kWave < s1) ins(it[u], sbv, q + u * kWave, sb);
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
 // ============================================================================ accumulation helpers
-// Table views in LDS
 template <typename Acc>
 struct Table {
   int32_t* keys;   // hash: keys[Tcap]; dense: presence bitmap (T/32 words)
   Acc* vals;       // T (dense) or Tcap (hash) slots
-  int32_t T;       // home range (hash) / window rows (dense)
+  int32_t T;       // home range (hash) / rows (dense)
   int32_t Tcap;    // hash: T + tail pad
 };
 
@@ -250,70 +397,17 @@ __device__ __forceinline__ int hash_insert_sym(int32_t* keys, int32_t r, int32_t
   }
 }
 
-// ============================================================================ segment expansion
-// Visit every multiply (q in A(:,k), b in B(:,j)) of column j with a group of NT lanes
-// (NT = 64 for a wavefront, or the block size).  Short segments (< kLong entries): one lane walks
-// the segment.  Long segments: a whole wavefront walks it in coalesced 64-entry strides.
-// F(q, b) is called once per multiply.  The caller provides LDS for the long-segment queue.
-constexpr int kLong = 64;
-
-template <int NT, bool WAVE_ONLY, typename F>
-__device__ __forceinline__ void for_each_multiply(int64_t bs, int64_t be, const int64_t* __restrict__ Acp,
-                                                  const int32_t* __restrict__ Bir, int32_t* lq, int* lq_n,
-                                                  F&& f) {
-  const int tid = WAVE_ONLY ? lane_id() : (int)threadIdx.x;
-  for (int64_t base = bs; base < be; base += NT) {
-    const int64_t b = base + tid;
-    int64_t a0 = 0, a1 = 0;
-    if (b < be) {
-      const int32_t k = Bir[b];
-      a0 = Acp[k];
-      a1 = Acp[k + 1];
-    }
-    const bool islong = (a1 - a0) >= kLong;
-    if (!islong) {
-      for (int64_t q = a0; q < a1; ++q) f(q, b);
-    }
-    // long segments: queue them (LDS), then each wavefront takes queue entries round-robin
-    if constexpr (WAVE_ONLY) {
-      const unsigned long long m = __ballot(islong);
-      const int pos = __popcll(m & ((1ull << lane_id()) - 1));
-      if (islong) lq[pos] = tid;   // store lane index; segment recomputed below
-      wave_sync();
-      const int nl = __popcll(m);
-      for (int i = 0; i < nl; ++i) {
-        const int src = lq[i];
-        const int64_t sb = base + src;
-        const int64_t s0 = __shfl(a0, src, kWave), s1 = __shfl(a1, src, kWave);
-        for (int64_t q = s0 + lane_id(); q < s1; q += kWave) f(q, sb);
-      }
-      wave_sync();
-    } else {
-      if (threadIdx.x == 0) *lq_n = 0;
-      __syncthreads();
-      if (islong) lq[atomicAdd(lq_n, 1)] = tid;
-      __syncthreads();
-      const int nl = *lq_n;
-      const int w = threadIdx.x / kWave;
-      constexpr int NW = NT / kWave;
-      for (int i = w; i < nl; i += NW) {
-        const int64_t sb = base + lq[i];
-        const int32_t k = Bir[sb];
-        const int64_t s0 = Acp[k], s1 = Acp[k + 1];
-        for (int64_t q = s0 + lane_id(); q < s1; q += kWave) f(q, sb);
-      }
-      __syncthreads();
-    }
-  }
-}
-
 // ============================================================================ 3. symbolic
 // Exact nnz of C(:,j) (estimateNNZ_Hash, mtSpGEMM.h:866-933).  Mode per column: presence bitmap over
-// the column's row span when it fits the class table, else a keys-only hash with T >= 2*flop.
-template <int LOGT>
-struct SymWaveCfg { static constexpr int T = 1 << LOGT; };
+// the column's row span (from a 32-aligned base) when it fits the table, else a keys-only hash with
+// T >= 2*flop.
+struct HeavyOut {       // columns with nnz > kHeavy: list + nnz per subwindow
+  int* n;
+  int32_t* cols;
+  int32_t* sub;         // [h * nsub + s]
+  int32_t nsub, log;
+};
 
-// wave kernel: 4 wavefronts per 256-thread block, one column per wavefront at a time
 template <int LOGT>
 __global__ void __launch_bounds__(256) k_sym_wave(const int32_t* __restrict__ list, int64_t count,
                                                   const int64_t* __restrict__ Acp, const int32_t* __restrict__ Air,
@@ -321,68 +415,116 @@ __global__ void __launch_bounds__(256) k_sym_wave(const int32_t* __restrict__ li
                                                   const int2* __restrict__ span, int64_t* __restrict__ nnz) {
   constexpr int T = 1 << LOGT;
   __shared__ int32_t s_tab[4][T];
-  __shared__ int32_t s_lq[4][kWave];
+  __shared__ int32_t s_wq[4][kWave];
   const int w = threadIdx.x / kWave, l = lane_id();
   int32_t* tab = s_tab[w];
   const int64_t nwaves = (int64_t)gridDim.x * 4;
   for (int64_t i = blockIdx.x * 4 + w; i < count; i += nwaves) {
     const int32_t j = list[i];
     const int2 sp = span[j];
-    const int64_t spn = (int64_t)sp.y - sp.x + 1;
-    const bool bitmap = spn <= 32LL * T;
+    const int32_t base = sp.x & ~31;
+    const bool bitmap = ((sp.y - base) >> 5) + 1 <= T;
     for (int s = l; s < T; s += kWave) tab[s] = bitmap ? 0 : kEmpty;
     wave_sync();
     int cnt = 0;
-    for_each_multiply<kWave, true>(Bcp[j], Bcp[j + 1], Acp, Bir, s_lq[w], nullptr, [&](int64_t q, int64_t) {
-      const int32_t r = Air[q];
-      if (bitmap) {
-        const int32_t o = r - sp.x;
-        const uint32_t bit = 1u << (o & 31);
-        if (!(tab[o >> 5] & bit)) cnt += (atomicOr((uint32_t*)&tab[o >> 5], bit) & bit) ? 0 : 1;
-      } else {
-        cnt += hash_insert_sym(tab, r, LOGT);
-      }
-    });
+    for_each_multiply<kWave, true, uint8_t>(
+        Bcp[j], Bcp[j + 1], s_wq[w], LongQ<uint8_t>{},
+        [&](int64_t b, int64_t& a0, int64_t& a1, uint8_t& bv) {
+          const int32_t k = Bir[b];
+          a0 = Acp[k];
+          a1 = Acp[k + 1];
+          bv = 0;
+        },
+        [&](int64_t q) { return Air[q]; },
+        [&](int32_t r, uint8_t, int64_t, int64_t) {
+          if (bitmap) {
+            const int32_t o = r - base;
+            const uint32_t bit = 1u << (o & 31);
+            if (!(tab[o >> 5] & bit)) cnt += (atomicOr((uint32_t*)&tab[o >> 5], bit) & bit) ? 0 : 1;
+          } else {
+            cnt += hash_insert_sym(tab, r, LOGT);
+          }
+        });
     int64_t tot = wave_sum64(cnt);
     if (l == 0) nnz[j] = tot;
     wave_sync();
   }
 }
 
-// block kernel: one column per workgroup
+// block kernel: one column per workgroup; heavy columns also report nnz per subwindow
 template <int LOGT, int NT>
 __global__ void __launch_bounds__(NT) k_sym_block(const int32_t* __restrict__ list, int64_t count,
                                                   const int64_t* __restrict__ Acp, const int32_t* __restrict__ Air,
                                                   const int64_t* __restrict__ Bcp, const int32_t* __restrict__ Bir,
-                                                  const int2* __restrict__ span, int64_t* __restrict__ nnz) {
+                                                  const int2* __restrict__ span, int64_t* __restrict__ nnz,
+                                                  HeavyOut ho) {
   constexpr int T = 1 << LOGT;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  int32_t* tab = (int32_t*)smem;
-  int32_t* lq = tab + T;          // NT
-  int* misc = lq + NT;            // [0] queue count, [1] total
+  int32_t* tab = (int32_t*)smem;                  // T
+  int64_t* q_a0 = (int64_t*)(tab + T);            // NT
+  int32_t* q_len = (int32_t*)(q_a0 + NT);         // NT
+  int32_t* q_b = q_len + NT;                      // NT
+  int32_t* scnt = q_b + NT;                       // kMaxSub + 2
+  uint8_t* q_bv = (uint8_t*)(scnt + kMaxSub + 2); // NT
+  int* misc = (int*)(q_bv + NT);                  // [0] queue n, [1] total, [2] heavy id
+  LongQ<uint8_t> lq{q_a0, q_len, q_b, q_bv, &misc[0]};
   for (int64_t i = blockIdx.x; i < count; i += gridDim.x) {
     const int32_t j = list[i];
     const int2 sp = span[j];
-    const int64_t spn = (int64_t)sp.y - sp.x + 1;
-    const bool bitmap = spn <= 32LL * T;
+    const int32_t base = sp.x & ~31;
+    const bool bitmap = ((sp.y - base) >> 5) + 1 <= T;
     for (int s = threadIdx.x; s < T; s += NT) tab[s] = bitmap ? 0 : kEmpty;
     if (threadIdx.x == 0) misc[1] = 0;
     __syncthreads();
     int cnt = 0;
-    for_each_multiply<NT, false>(Bcp[j], Bcp[j + 1], Acp, Bir, lq, &misc[0], [&](int64_t q, int64_t) {
-      const int32_t r = Air[q];
-      if (bitmap) {
-        const int32_t o = r - sp.x;
-        const uint32_t bit = 1u << (o & 31);
-        if (!(tab[o >> 5] & bit)) cnt += (atomicOr((uint32_t*)&tab[o >> 5], bit) & bit) ? 0 : 1;
-      } else {
-        cnt += hash_insert_sym(tab, r, LOGT);
-      }
-    });
+    for_each_multiply<NT, false, uint8_t>(
+        Bcp[j], Bcp[j + 1], nullptr, lq,
+        [&](int64_t b, int64_t& a0, int64_t& a1, uint8_t& bv) {
+          const int32_t k = Bir[b];
+          a0 = Acp[k];
+          a1 = Acp[k + 1];
+          bv = 0;
+        },
+        [&](int64_t q) { return Air[q]; },
+        [&](int32_t r, uint8_t, int64_t, int64_t) {
+          if (bitmap) {
+            const int32_t o = r - base;
+            const uint32_t bit = 1u << (o & 31);
+            if (!(tab[o >> 5] & bit)) cnt += (atomicOr((uint32_t*)&tab[o >> 5], bit) & bit) ? 0 : 1;
+          } else {
+            cnt += hash_insert_sym(tab, r, LOGT);
+          }
+        });
     int64_t wc = wave_sum64(cnt);
     if (lane_id() == 0 && wc) atomicAdd(&misc[1], (int)wc);
     __syncthreads();
-    if (threadIdx.x == 0) nnz[j] = misc[1];
+    const int total = misc[1];
+    if (threadIdx.x == 0) nnz[j] = total;
+    if (total > kHeavy) {   // uniform branch
+      const int32_t sf = sp.x >> ho.log, sl = sp.y >> ho.log;
+      if (threadIdx.x == 0) {
+        const int h = atomicAdd(ho.n, 1);
+        misc[2] = h;
+        ho.cols[h] = j;
+      }
+      for (int s = threadIdx.x; s <= sl - sf; s += NT) scnt[s] = 0;
+      __syncthreads();
+      if (bitmap) {
+        const int nw = ((sp.y - base) >> 5) + 1;
+        for (int w = threadIdx.x; w < nw; w += NT) {
+          const uint32_t word = (uint32_t)tab[w];
+          if (word) atomicAdd(&scnt[((base + 32 * w) >> ho.log) - sf], __popc(word));
+        }
+      } else {
+        for (int s = threadIdx.x; s < T; s += NT) {
+          const int32_t key = tab[s];
+          if (key != kEmpty) atomicAdd(&scnt[(key >> ho.log) - sf], 1);
+        }
+      }
+      __syncthreads();
+      int32_t* dst = ho.sub + (int64_t)misc[2] * ho.nsub;
+      for (int s = threadIdx.x; s <= sl - sf; s += NT) dst[sf + s] = scnt[s];
+    }
     __syncthreads();
   }
 }
@@ -439,7 +581,6 @@ __global__ void __launch_bounds__(256) k_scan_apply(int64_t n, const int64_t* __
                                                     int64_t* __restrict__ out) {
   __shared__ int64_t s[5];
   const int64_t base = blockIdx.x * (int64_t)kScanTile;
-  // each thread owns 4 consecutive elements
   int64_t v[4], t = 0;
   for (int e = 0; e < 4; ++e) {
     const int64_t i = base + threadIdx.x * 4 + e;
@@ -470,23 +611,139 @@ __global__ void __launch_bounds__(256) k_scan_apply(int64_t n, const int64_t* __
   }
 }
 
-// ============================================================================ 5. numeric
+// ============================================================================ 5. heavy-column units
+// split table rows for long A columns
+__global__ void k_split_assign(int64_t ncol, const int64_t* __restrict__ Acp, int32_t* __restrict__ idx,
+                               int32_t* __restrict__ longcols, int* __restrict__ nlong) {
+  for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < ncol; k += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t len = Acp[k + 1] - Acp[k];
+    if (len >= kSplitMin) {
+      const int e = atomicAdd(nlong, 1);
+      idx[k] = e;
+      longcols[e] = (int32_t)k;
+    } else {
+      idx[k] = -1;
+    }
+  }
+}
+// one wavefront per long column: every subwindow boundary by binary search
+__global__ void __launch_bounds__(256) k_split_fill(int nlong, const int32_t* __restrict__ longcols,
+                                                    const int64_t* __restrict__ Acp, const int32_t* __restrict__ Air,
+                                                    int32_t* __restrict__ tab, int32_t nsub, int32_t log) {
+  const int w = threadIdx.x / kWave, l = lane_id();
+  for (int64_t e = blockIdx.x * 4 + w; e < nlong; e += (int64_t)gridDim.x * 4) {
+    const int32_t k = longcols[e];
+    const int64_t c0 = Acp[k], c1 = Acp[k + 1];
+    int32_t* t = tab + e * (nsub + 1);
+    for (int s = l; s <= nsub; s += kWave) t[s] = (int32_t)(lower_bound_rows(Air, c0, c1, (int64_t)s << log) - c0);
+  }
+}
+// units of a heavy column: consecutive subwindows while the running count stays <= kUnitCap
+__global__ void k_build_units(int H, const int32_t* __restrict__ cols, const int32_t* __restrict__ sub, int32_t nsub,
+                              int32_t log, const int2* __restrict__ span, const int64_t* __restrict__ colptr,
+                              Unit* __restrict__ units, int64_t* __restrict__ ucnt, int2* __restrict__ uspan,
+                              int64_t* __restrict__ nnz) {
+  const int h = blockIdx.x * blockDim.x + threadIdx.x;
+  if (h >= H) return;
+  const int32_t j = cols[h];
+  const int2 sp = span[j];
+  const int32_t sf = sp.x >> log, sl = sp.y >> log;
+  const int32_t* c = sub + (int64_t)h * nsub;
+  const int64_t slot = (int64_t)h * nsub;
+  int64_t out = colptr[j];
+  int u = 0, st = sf;
+  int64_t acc = 0;
+  auto emit = [&](int32_t s0, int32_t s1, int64_t n) {
+    units[slot + u] = Unit{j, s0, s1, (int32_t)n, out};
+    ucnt[slot + u] = n;
+    const int64_t lo = max((int64_t)sp.x, (int64_t)s0 << log);
+    const int64_t hi = min((int64_t)sp.y, ((int64_t)s1 << log) - 1);
+    uspan[slot + u] = make_int2((int32_t)lo, (int32_t)hi);
+    ++u;
+    out += n;
+  };
+  for (int32_t s = sf; s <= sl; ++s) {
+    const int64_t n = c[s];
+    if (acc > 0 && acc + n > kUnitCap) {
+      emit(st, s, acc);
+      st = s;
+      acc = 0;
+    }
+    acc += n;
+  }
+  if (acc > 0) emit(st, sl + 1, acc);
+  nnz[j] = 0;   // the whole column is now covered by units
+}
+// overflowed (hash) units -> single-subwindow units, which run in dense mode
+__global__ void k_split_overflow_units(const int* __restrict__ n_ovf, const int32_t* __restrict__ ovf,
+                                       const Unit* __restrict__ units, const int32_t* __restrict__ sub, int32_t nsub,
+                                       Unit* __restrict__ out_units,
+                                       int* __restrict__ n_out, int32_t* __restrict__ out_list) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= *n_ovf) return;
+  const int32_t uid = ovf[i];
+  const Unit u = units[uid];
+  const int64_t h = uid / nsub;   // units of heavy column h live at [h*nsub, (h+1)*nsub)
+  int64_t off = u.outoff;
+  for (int32_t s = u.s0; s < u.s1; ++s) {
+    const int32_t n = sub[h * nsub + s];
+    if (n > 0) {
+      const int e = atomicAdd(n_out, 1);
+      out_units[e] = Unit{u.j, s, s + 1, n, off};
+      out_list[e] = e;
+      off += n;
+    }
+  }
+}
+
+// ============================================================================ 6. numeric
 // Output: C.row / C.val at colptr[j] .. colptr[j+1], rows ascending.
 template <typename V>
 struct NumOut {
-  const int64_t* colptr;
   int32_t* row;
   V* val;
   int* adderr;            // BoolCopy add() attempted
-  int* overflow_n;        // fallback list length
-  int32_t* overflow_list; // columns whose order-preserving hash overflowed
+  int* ovf_n;             // fallback list length
+  int32_t* ovf_list;      // items whose order-preserving hash overflowed (columns, or unit ids)
 };
 
-// Compaction of an order-preserving hash table of Tcap slots by `NT` lanes (tid in [0,NT)).
+template <bool UNIT>
+__device__ __forceinline__ Work get_work(const int32_t* __restrict__ list, int64_t i, const Unit* __restrict__ units,
+                                         const int2* __restrict__ span, const int64_t* __restrict__ colptr,
+                                         int32_t log) {
+  Work w;
+  if constexpr (UNIT) {
+    const Unit u = units[list[i]];
+    const int2 sp = span[u.j];
+    w.j = u.j;
+    w.s0 = u.s0;
+    w.s1 = u.s1;
+    w.lo = (int32_t)max((int64_t)sp.x, (int64_t)u.s0 << log);
+    w.hi = (int32_t)min((int64_t)sp.y, ((int64_t)u.s1 << log) - 1);
+    w.ob = u.outoff;
+  } else {
+    const int32_t j = list[i];
+    const int2 sp = span[j];
+    w.j = j;
+    w.s0 = w.s1 = -1;
+    w.lo = sp.x;
+    w.hi = sp.y;
+    w.ob = colptr ? colptr[j] : 0;
+  }
+  return w;
+}
+
+template <typename V>
+struct NumItem {
+  int32_t r;
+  V a;
+};
+
+// Compaction of an order-preserving hash table of Tcap slots by NT lanes.
 // out position of an occupied slot s = (#occupied before its run start) + (#keys in its run smaller).
-template <int NT, class SRT, typename V>
+template <class SRT, typename V>
 __device__ __forceinline__ void compact_hash_runs(const int32_t* keys, const typename SRT::Acc* vals, int Tcap,
-                                                  int tid, int occ_before_chunk, int c0, int c1, int64_t outbase,
+                                                  int occ_before_chunk, int c0, int c1, int64_t outbase,
                                                   const V* aval, const V* bval, int32_t* orow, V* oval) {
   int occ = occ_before_chunk;
   for (int s = c0; s < c1; ++s) {
@@ -507,132 +764,155 @@ __device__ __forceinline__ void compact_hash_runs(const int32_t* keys, const typ
   }
 }
 
-// ---- wave numeric: one column per wavefront, table T slots (+kTail) per wave
+// ---- wave numeric: one item per wavefront, table T slots (+kTail) per wave
 constexpr int kTail = 64;
 
-template <class SRT, typename V, int LOGT>
+template <class SRT, typename V, int LOGT, bool UNIT>
 __global__ void __launch_bounds__(256) k_num_wave(const int32_t* __restrict__ list, int64_t count,
-                                                  DevCsc<V> A, DevCsc<V> B, const int2* __restrict__ span,
-                                                  NumOut<V> out) {
+                                                  const Unit* __restrict__ units, DevCsc<V> A, DevCsc<V> B,
+                                                  const int2* __restrict__ span, const int64_t* __restrict__ colptr,
+                                                  Split spl, NumOut<V> out) {
   using Acc = typename SRT::Acc;
   constexpr int T = 1 << LOGT;
   constexpr int TC = T + kTail;
   __shared__ int32_t s_keys[4][TC];
   __shared__ Acc s_vals[4][TC];
-  __shared__ int32_t s_lq[4][kWave];
+  __shared__ int32_t s_wq[4][kWave];
   const int w = threadIdx.x / kWave, l = lane_id();
   Table<Acc> t{s_keys[w], s_vals[w], T, TC};
   const int64_t nwaves = (int64_t)gridDim.x * 4;
   for (int64_t i = blockIdx.x * 4 + w; i < count; i += nwaves) {
-    const int32_t j = list[i];
-    const int2 sp = span[j];
-    const int64_t spn = (int64_t)sp.y - sp.x + 1;
+    const Work wk = get_work<UNIT>(list, i, units, span, colptr, spl.log);
+    const int64_t spn = (int64_t)wk.hi - wk.lo + 1;
     const bool dense = spn <= T;
     const uint32_t mult = dense ? 0u : (uint32_t)(((uint64_t)T << 32) / (uint64_t)spn);
     for (int s = l; s < TC; s += kWave) { t.keys[s] = dense ? 0 : kEmpty; t.vals[s] = SRT::identity(); }
     wave_sync();
     int ovf = 0, aerr = 0;
-    for_each_multiply<kWave, true>(B.cp[j], B.cp[j + 1], A.cp, B.ir, s_lq[w], nullptr, [&](int64_t q, int64_t b) {
-      const int32_t r = A.ir[q];
-      const Acc x = SRT::mul(load_val(A.val, q), load_val(B.val, b), q, b);
-      if (dense) {
-        const int32_t o = r - sp.x;
-        const uint32_t bit = 1u << (o & 31);
-        const uint32_t old = atomicOr((uint32_t*)&t.keys[o >> 5], bit);
-        if (SRT::kAddIsError && (old & bit)) aerr = 1;
-        SRT::acc(&t.vals[o], x);
-      } else {
-        if (!hash_insert_num<SRT>(t, r, mono_home(r, sp.x, mult), x, &aerr)) ovf = 1;
-      }
-    });
+    for_each_multiply<kWave, true, V>(
+        B.cp[wk.j], B.cp[wk.j + 1], s_wq[w], LongQ<V>{},
+        [&](int64_t b, int64_t& a0, int64_t& a1, V& bv) {
+          const int32_t k = B.ir[b];
+          if constexpr (UNIT) unit_bounds(A.cp, A.ir, spl, k, wk.s0, wk.s1, a0, a1);
+          else { a0 = A.cp[k]; a1 = A.cp[k + 1]; }
+          bv = load_val(B.val, b);
+        },
+        [&](int64_t q) { return NumItem<V>{A.ir[q], load_val(A.val, q)}; },
+        [&](const NumItem<V>& it, V bv, int64_t q, int64_t b) {
+          const Acc x = SRT::mul(it.a, bv, q, b);
+          if (dense) {
+            const int32_t o = it.r - wk.lo;
+            const uint32_t bit = 1u << (o & 31);
+            const uint32_t old = atomicOr((uint32_t*)&t.keys[o >> 5], bit);
+            if (SRT::kAddIsError && (old & bit)) aerr = 1;
+            SRT::acc(&t.vals[o], x);
+          } else {
+            if (!hash_insert_num<SRT>(t, it.r, mono_home(it.r, wk.lo, mult), x, &aerr)) ovf = 1;
+          }
+        });
     wave_sync();
     const bool wov = __any(ovf);
     if (__any(aerr) && l == 0) atomicOr(out.adderr, 1);
-    const int64_t ob = out.colptr[j];
+    const int64_t ob = wk.ob;
     if (wov) {
-      if (l == 0) out.overflow_list[atomicAdd(out.overflow_n, 1)] = j;
+      if (l == 0) out.ovf_list[atomicAdd(out.ovf_n, 1)] = list[i];
     } else if (dense) {
-      // bitmap words: T/32 <= 16 for T <= 512 -> lanes 0..T/32-1
-      constexpr int NWORD = T / 32;
+      constexpr int NWORD = T / 32;   // <= 16 for T <= 512
       uint32_t wd = (l < NWORD) ? (uint32_t)t.keys[l] : 0u;
       const int pc = __popc(wd);
-      const int ex = wave_incl_scan(pc) - pc;
-      int o = ex;
+      int o = wave_incl_scan(pc) - pc;
       while (wd) {
         const int bpos = __ffs(wd) - 1;
         wd &= wd - 1;
         const int rr = l * 32 + bpos;
-        out.row[ob + o] = sp.x + rr;
+        out.row[ob + o] = wk.lo + rr;
         out.val[ob + o] = SRT::out(t.vals[rr], A.val, B.val);
         ++o;
       }
     } else {
-      // chunk of TC/64 slots per lane (TC multiple of 64)
       constexpr int CH = TC / kWave;
       const int c0 = l * CH, c1 = c0 + CH;
       int occ = 0;
       for (int s = c0; s < c1; ++s) occ += (t.keys[s] != kEmpty);
       const int ex = wave_incl_scan(occ) - occ;
-      compact_hash_runs<kWave, SRT, V>(t.keys, t.vals, TC, l, ex, c0, c1, ob, A.val, B.val, out.row, out.val);
+      compact_hash_runs<SRT, V>(t.keys, t.vals, TC, ex, c0, c1, ob, A.val, B.val, out.row, out.val);
     }
     wave_sync();
   }
 }
 
-// ---- block numeric: one column per workgroup; LDS = TC*(4+sizeof(Acc)) + small
+// ---- block numeric: one item per workgroup
 template <class SRT, typename V, int LOGT, int NT>
-__global__ void __launch_bounds__(NT) k_num_block(const int32_t* __restrict__ list, int64_t count,
-                                                  DevCsc<V> A, DevCsc<V> B, const int2* __restrict__ span,
-                                                  NumOut<V> out) {
+constexpr size_t num_block_lds() {
+  return (size_t)((1 << LOGT) + NT) * (sizeof(typename SRT::Acc) + 4) + (size_t)NT * (16 + sizeof(V)) + 64 * 4;
+}
+
+template <class SRT, typename V, int LOGT, int NT, bool UNIT>
+__global__ void __launch_bounds__(NT) k_num_block(const int32_t* __restrict__ list, const int* __restrict__ count_dev,
+                                                  int64_t count_host, const Unit* __restrict__ units, DevCsc<V> A,
+                                                  DevCsc<V> B, const int2* __restrict__ span,
+                                                  const int64_t* __restrict__ colptr, Split spl, NumOut<V> out) {
   using Acc = typename SRT::Acc;
   constexpr int T = 1 << LOGT;
   constexpr int TC = T + NT;      // tail = one slot per thread keeps chunks uniform
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  Acc* vals = (Acc*)smem;
-  int32_t* keys = (int32_t*)(vals + TC);
-  int32_t* lq = keys + TC;        // NT
-  int* misc = lq + NT;            // [0] lq count, [1] overflow, [2] adderr, [3..] scan scratch
+  Acc* vals = (Acc*)smem;                        // TC
+  int64_t* q_a0 = (int64_t*)(vals + TC);         // NT
+  V* q_bv = (V*)(q_a0 + NT);                     // NT
+  int32_t* keys = (int32_t*)(q_bv + NT);         // TC
+  int32_t* q_len = keys + TC;                    // NT
+  int32_t* q_b = q_len + NT;                     // NT
+  int* misc = q_b + NT;                          // [0] queue n, [1] overflow, [2] adderr, [8..] scan
+  LongQ<V> lq{q_a0, q_len, q_b, q_bv, &misc[0]};
   Table<Acc> t{keys, vals, T, TC};
+  const int64_t count = count_dev ? (int64_t)*count_dev : count_host;
   for (int64_t i = blockIdx.x; i < count; i += gridDim.x) {
-    const int32_t j = list[i];
-    const int2 sp = span[j];
-    const int64_t spn = (int64_t)sp.y - sp.x + 1;
+    const Work wk = get_work<UNIT>(list, i, units, span, colptr, spl.log);
+    const int64_t spn = (int64_t)wk.hi - wk.lo + 1;
     const bool dense = spn <= T;
     const uint32_t mult = dense ? 0u : (uint32_t)(((uint64_t)T << 32) / (uint64_t)spn);
     for (int s = threadIdx.x; s < TC; s += NT) { keys[s] = dense ? 0 : kEmpty; vals[s] = SRT::identity(); }
     if (threadIdx.x == 0) { misc[1] = 0; misc[2] = 0; }
     __syncthreads();
     int ovf = 0, aerr = 0;
-    for_each_multiply<NT, false>(B.cp[j], B.cp[j + 1], A.cp, B.ir, lq, &misc[0], [&](int64_t q, int64_t b) {
-      const int32_t r = A.ir[q];
-      const Acc x = SRT::mul(load_val(A.val, q), load_val(B.val, b), q, b);
-      if (dense) {
-        const int32_t o = r - sp.x;
-        const uint32_t bit = 1u << (o & 31);
-        const uint32_t old = atomicOr((uint32_t*)&keys[o >> 5], bit);
-        if (SRT::kAddIsError && (old & bit)) aerr = 1;
-        SRT::acc(&vals[o], x);
-      } else {
-        if (!hash_insert_num<SRT>(t, r, mono_home(r, sp.x, mult), x, &aerr)) ovf = 1;
-      }
-    });
+    for_each_multiply<NT, false, V>(
+        B.cp[wk.j], B.cp[wk.j + 1], nullptr, lq,
+        [&](int64_t b, int64_t& a0, int64_t& a1, V& bv) {
+          const int32_t k = B.ir[b];
+          if constexpr (UNIT) unit_bounds(A.cp, A.ir, spl, k, wk.s0, wk.s1, a0, a1);
+          else { a0 = A.cp[k]; a1 = A.cp[k + 1]; }
+          bv = load_val(B.val, b);
+        },
+        [&](int64_t q) { return NumItem<V>{A.ir[q], load_val(A.val, q)}; },
+        [&](const NumItem<V>& it, V bv, int64_t q, int64_t b) {
+          const Acc x = SRT::mul(it.a, bv, q, b);
+          if (dense) {
+            const int32_t o = it.r - wk.lo;
+            const uint32_t bit = 1u << (o & 31);
+            const uint32_t old = atomicOr((uint32_t*)&keys[o >> 5], bit);
+            if (SRT::kAddIsError && (old & bit)) aerr = 1;
+            SRT::acc(&vals[o], x);
+          } else {
+            if (!hash_insert_num<SRT>(t, it.r, mono_home(it.r, wk.lo, mult), x, &aerr)) ovf = 1;
+          }
+        });
     if (ovf) misc[1] = 1;
     if (aerr) misc[2] = 1;
     __syncthreads();
-    const int64_t ob = out.colptr[j];
+    const int64_t ob = wk.ob;
     if (misc[1]) {
-      if (threadIdx.x == 0) out.overflow_list[atomicAdd(out.overflow_n, 1)] = j;
+      if (threadIdx.x == 0) out.ovf_list[atomicAdd(out.ovf_n, 1)] = list[i];
     } else if (dense) {
-      // presence bitmap: T/32 words; word w owned by thread w (T/32 <= NT for T <= 32*NT)
-      const int NWORD = T / 32;
+      constexpr int NWORD = T / 32;
+      static_assert(NWORD <= NT, "dense bitmap words must not exceed the block");
       uint32_t wd = (threadIdx.x < NWORD) ? (uint32_t)keys[threadIdx.x] : 0u;
       int tot;
-      int o = block_excl_scan<NT>(__popc(wd), misc + 3, &tot);
+      int o = block_excl_scan<NT>(__popc(wd), misc + 8, &tot);
       while (wd) {
         const int bpos = __ffs(wd) - 1;
         wd &= wd - 1;
         const int rr = threadIdx.x * 32 + bpos;
-        out.row[ob + o] = sp.x + rr;
+        out.row[ob + o] = wk.lo + rr;
         out.val[ob + o] = SRT::out(vals[rr], A.val, B.val);
         ++o;
       }
@@ -642,58 +922,75 @@ __global__ void __launch_bounds__(NT) k_num_block(const int32_t* __restrict__ li
       int occ = 0;
       for (int s = c0; s < c1; ++s) occ += (keys[s] != kEmpty);
       int tot;
-      const int ex = block_excl_scan<NT>(occ, misc + 3, &tot);
-      compact_hash_runs<NT, SRT, V>(keys, vals, TC, threadIdx.x, ex, c0, c1, ob, A.val, B.val, out.row, out.val);
+      const int ex = block_excl_scan<NT>(occ, misc + 8, &tot);
+      compact_hash_runs<SRT, V>(keys, vals, TC, ex, c0, c1, ob, A.val, B.val, out.row, out.val);
     }
     if (threadIdx.x == 0 && misc[2]) atomicOr(out.adderr, 1);
     __syncthreads();
   }
 }
 
-// ============================================================================ 6. windowed (heavy)
+// ============================================================================ 7. windowed sweep
 // One workgroup per column, sweeping row windows [r0, r0+W) over the column's span.  Every B nonzero
-// b of the column owns a cursor into A(:,k) (cur[b], absolute index) and caches the row at the
-// cursor (nxt[b]); a window only touches segments whose cached row is inside it.
-// MODE 0 = symbolic (presence bitmap, count only), MODE 1 = numeric (dense value window + bitmap).
+// b owns a cursor into A(:,k) (cur[b], absolute index) and caches the row at the cursor (nxt[b]); a
+// window only touches segments whose cached row is inside it.
+//   MODE 0 = symbolic for spans wider than one 2^20-row bitmap: counts, and (the column is heavy)
+//            nnz per subwindow;
+//   MODE 1 = numeric fallback for whole columns whose order-preserving hash overflowed: dense value
+//            window of 8192 rows + presence bitmap, compaction in row order.
 constexpr int kWinRows = 8192;         // numeric dense window (64 KB of f64 values)
 constexpr int kSymWinRows = 1 << 20;   // symbolic bitmap window (128 KB)
 
 template <int MODE, class SRT, typename V, int NT, int W>
+constexpr size_t window_lds() {
+  return (MODE == 1 ? (size_t)W * sizeof(typename SRT::Acc) : 0) + (size_t)(W / 32) * 4 + (size_t)NT * 4 +
+         (MODE == 0 ? (size_t)(W / kWinRows + 2) * 4 : 0) + 64 * 4;
+}
+
+template <int MODE, class SRT, typename V, int NT, int W>
 __global__ void __launch_bounds__(NT) k_window(const int32_t* __restrict__ list, const int* __restrict__ count_dev,
                                                int64_t count_host, DevCsc<V> A, DevCsc<V> B,
-                                               const int2* __restrict__ span, int64_t* __restrict__ cur,
-                                               int32_t* __restrict__ nxt, int64_t* __restrict__ nnz, NumOut<V> out) {
+                                               const int2* __restrict__ span, const int64_t* __restrict__ colptr,
+                                               int64_t* __restrict__ cur, int32_t* __restrict__ nxt,
+                                               int64_t* __restrict__ nnz, HeavyOut ho, NumOut<V> out) {
   using Acc = typename SRT::Acc;
   constexpr int NWORD = W / 32;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   Acc* vals = (Acc*)smem;                                    // W (MODE 1) or 0
   uint32_t* bits = (uint32_t*)(vals + (MODE == 1 ? W : 0));  // NWORD
   int32_t* lq = (int32_t*)(bits + NWORD);                    // NT (queue of long segments)
-  int* misc = lq + NT;                                       // [0] lq n, [1] count, [2] adderr, [3..] scan
+  int32_t* scnt = lq + NT;                                   // MODE 0: subwindow counters
+  int* misc = scnt + (MODE == 0 ? (W / kWinRows + 2) : 0);   // [0] lq n, [1] count, [2] adderr, [3] h, [8..] scan
   const int64_t count = count_dev ? (int64_t)*count_dev : count_host;
   for (int64_t i = blockIdx.x; i < count; i += gridDim.x) {
     const int32_t j = list[i];
     const int2 sp = span[j];
     const int64_t bs = B.cp[j], be = B.cp[j + 1];
-    // init cursors
     for (int64_t b = bs + threadIdx.x; b < be; b += NT) {
       const int32_t k = B.ir[b];
       const int64_t a0 = A.cp[k], a1 = A.cp[k + 1];
       cur[b] = a0;
       nxt[b] = a0 < a1 ? A.ir[a0] : INT32_MAX;
     }
-    if (threadIdx.x == 0) misc[2] = 0;
+    if (threadIdx.x == 0) {
+      misc[2] = 0;
+      if (MODE == 0) {
+        const int h = atomicAdd(ho.n, 1);
+        misc[3] = h;
+        ho.cols[h] = j;
+      }
+    }
     __syncthreads();
-    int64_t outpos = (MODE == 1) ? out.colptr[j] : 0;
+    int64_t outpos = (MODE == 1) ? colptr[j] : 0;
     int64_t total = 0;
     int aerr = 0;
-    for (int64_t r0 = sp.x; r0 <= sp.y; r0 += W) {
+    const int32_t start = sp.x & ~31;
+    for (int64_t r0 = start; r0 <= sp.y; r0 += W) {
       const int32_t r1 = (int32_t)min<int64_t>(r0 + W, (int64_t)sp.y + 1);
       for (int s = threadIdx.x; s < NWORD; s += NT) bits[s] = 0u;
       if constexpr (MODE == 1)
         for (int s = threadIdx.x; s < W; s += NT) vals[s] = SRT::identity();
       __syncthreads();
-      // visit segments with work in this window
       for (int64_t base = bs; base < be; base += NT) {
         const int64_t b = base + threadIdx.x;
         int64_t q = 0, qe = 0;
@@ -706,7 +1003,6 @@ __global__ void __launch_bounds__(NT) k_window(const int32_t* __restrict__ list,
             qe = A.cp[B.ir[b] + 1];
           }
         }
-        // long-in-window test: a segment with >= 64 entries left is handed to a wavefront
         const bool islong = act && (qe - q) >= kLong && A.ir[q + kLong - 1] < r1;
         if (act && !islong) {
           const V bv = load_val(B.val, b);
@@ -759,7 +1055,6 @@ __global__ void __launch_bounds__(NT) k_window(const int32_t* __restrict__ list,
             const int nin = __popcll(m);
             sq += nin;
             if (nin < kWave) {
-              // first lane not in window holds the next row (or INT32_MAX past the end)
               const int fl = __ffsll((long long)~m) - 1;
               rn = __shfl(r, fl, kWave);
               break;
@@ -769,25 +1064,37 @@ __global__ void __launch_bounds__(NT) k_window(const int32_t* __restrict__ list,
         }
         __syncthreads();
       }
-      // compaction of this window
-      int wcnt = 0;
-      for (int s = threadIdx.x; s < NWORD; s += NT) wcnt += __popc(bits[s]);
       int tot;
       if constexpr (MODE == 0) {
-        int64_t ws = wave_sum64(wcnt);
+        // count + nnz per subwindow (windows start 32-aligned, so a word never straddles one)
+        const int32_t sf = (int32_t)(r0 >> ho.log);
+        const int nsw = (int)(((int64_t)r1 - 1) >> ho.log) - sf + 1;
+        for (int s = threadIdx.x; s < nsw; s += NT) scnt[s] = 0;
         if (threadIdx.x == 0) misc[1] = 0;
         __syncthreads();
+        int wcnt = 0;
+        for (int s = threadIdx.x; s < NWORD; s += NT) {
+          const int pc = __popc(bits[s]);
+          if (pc) {
+            wcnt += pc;
+            atomicAdd(&scnt[((r0 + 32 * s) >> ho.log) - sf], pc);
+          }
+        }
+        int64_t ws = wave_sum64(wcnt);
         if (lane_id() == 0 && ws) atomicAdd(&misc[1], (int)ws);
         __syncthreads();
         total += misc[1];
+        int32_t* dst = ho.sub + (int64_t)misc[3] * ho.nsub;
+        const int32_t slast = sp.y >> ho.log;
+        for (int s = threadIdx.x; s < nsw; s += NT)
+          if (sf + s <= slast) dst[sf + s] = scnt[s];
         __syncthreads();
       } else {
-        // thread owns words [tid*PW, tid*PW+PW), PW = NWORD/NT
         constexpr int PW = NWORD / NT;
         static_assert(NWORD % NT == 0, "window words must split evenly");
         int c = 0;
         for (int s = 0; s < PW; ++s) c += __popc(bits[threadIdx.x * PW + s]);
-        int o = block_excl_scan<NT>(c, misc + 3, &tot);
+        int o = block_excl_scan<NT>(c, misc + 8, &tot);
         for (int s = 0; s < PW; ++s) {
           uint32_t wd = bits[threadIdx.x * PW + s];
           while (wd) {

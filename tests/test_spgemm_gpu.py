@@ -217,3 +217,76 @@ def test_gpu_dcsc_input_view(gpu_ctx):
     cp, irc, v = C.to_host()
     R = fixture_product(z, "pt_f64_hash")
     assert np.array_equal(cp, R.cp) and np.array_equal(irc, R.ir) and np.array_equal(v, R.val)
+
+
+def test_gpu_unit_overflow_fallback(gpu_ctx):
+    """A heavy column (nnz > 4096 -> units) whose multi-subwindow unit has its rows packed at the top:
+    the unit's order-preserving hash overflows and is re-run as dense single-subwindow units."""
+    W = 8192
+    rows = np.r_[np.arange(10), np.arange(6 * W - 3000, 6 * W), 20 * W + np.arange(0, 4000, 2)].astype(np.int32)
+    n = 1 << 20
+    A = Csc(n, 1, [0, len(rows)], rows, np.arange(1, len(rows) + 1, dtype=np.float64))
+    B = Csc(1, 1, [0, 1], [0], np.array([2.0]))
+    _check_vs_oracle(gpu_ctx, A, B)
+    prof = gpu_ctx.last_profile()
+    assert prof["bins"][12] == 1          # one heavy column
+    assert prof["bins"][14] >= 1          # at least one unit re-run densely
+
+
+def test_gpu_heavy_units_many_columns(gpu_ctx):
+    """Many heavy columns with mixed long/short A segments, every semiring family."""
+    rng = np.random.default_rng(11)
+    n = 1 << 18
+    ncolA = 300
+    lens = np.where(rng.random(ncolA) < 0.3, rng.integers(64, 3000, ncolA), rng.integers(1, 40, ncolA))
+    cols = [np.sort(rng.choice(n, L, replace=False)).astype(np.int32) for L in lens]
+    cp = np.r_[0, np.cumsum(lens)]
+    A = Csc(n, ncolA, cp, np.concatenate(cols), rng.integers(-3, 4, cp[-1]).astype(np.int64))
+    nb = 20
+    bcp = [0]
+    bir = []
+    for j in range(nb):
+        k = np.sort(rng.choice(ncolA, int(rng.integers(5, 120)), replace=False))
+        bir.append(k.astype(np.int32))
+        bcp.append(bcp[-1] + len(k))
+    B = Csc(ncolA, nb, bcp, np.concatenate(bir), rng.integers(-3, 4, bcp[-1]).astype(np.int64))
+    for sr in ("plus_times", "min_plus", "select2nd", "select_max"):
+        _check_vs_oracle(gpu_ctx, A, B, sr, "i64")
+    assert gpu_ctx.last_profile()["bins"][12] > 0
+
+
+@pytest.mark.parametrize("sr,dt", [("plus_times", "f64"), ("plus_times", "i64"), ("min_plus", "i64"),
+                                   ("select2nd", "i64"), ("select_max", "f64")])
+@pytest.mark.parametrize("nparts", [1, 2, 4])
+def test_gpu_multiway_merge_vs_oracle(gpu_ctx, sr, dt, nparts):
+    """MultiwayMerge (MultiwayMerge.h:411-526): k column-sorted partials -> one, duplicates via SR::add in
+    list order (Select2nd: the first list holding the entry wins)."""
+    from helpers import oracle_merge
+    rng = np.random.default_rng(nparts * 7 + len(sr))
+    parts = [rand_csc(rng, 3000, 500, 0.01 + 0.01 * p, dt) for p in range(nparts)]
+    R, rc = oracle_merge(parts, sr, dt)
+    assert rc == 0
+    dparts = [upload(gpu_ctx, P) for P in parts]
+    M = cb.MultiwayMerge(SRCLS[sr](dt), dparts)
+    cp, ir, val = M.to_host()
+    C = Csc(3000, 500, cp, ir, val)
+    assert_same_product(C, R, dt, scale=np.abs(R.val) * nparts if dt == "f64" else None, what=f"merge {sr}")
+
+
+def test_gpu_merge_of_split_products_equals_product(gpu_ctx):
+    """1x1x2-style: split the inner dimension, multiply the halves on the GPU, merge on the GPU."""
+    z = load_fixture("g500_s10")
+    A, B, sr, dt = fixture_inputs(z, "pt_i64_hash")
+    As, Bs = A.to_scipy().tocsc(), B.to_scipy().tocsc()
+    h = A.ncol // 2
+    halves = []
+    for lo, hi in ((0, h), (h, A.ncol)):
+        Ah, Bh = As[:, lo:hi].tocsc(), Bs[lo:hi, :].tocsc()
+        Ah.sort_indices(); Bh.sort_indices()
+        dA = cb.SpDCCols.from_csc(gpu_ctx, Ah.shape[0], Ah.shape[1], Ah.indptr, Ah.indices, Ah.data.astype(np.int64))
+        dB = cb.SpDCCols.from_csc(gpu_ctx, Bh.shape[0], Bh.shape[1], Bh.indptr, Bh.indices, Bh.data.astype(np.int64))
+        halves.append(cb.LocalSpGEMMHash(cb.PlusTimesSRing("i64"), dA, dB))
+    M = cb.MultiwayMerge(cb.PlusTimesSRing("i64"), halves)
+    cp, ir, val = M.to_host()
+    R = fixture_product(z, "pt_i64_hash")
+    assert np.array_equal(cp, R.cp) and np.array_equal(ir, R.ir) and np.array_equal(val, R.val)
