@@ -113,7 +113,7 @@ cbg_status cbg_upload(cbg_ctx* ctx, const cbg_dcsc_view* v, cbg_csc_result* out)
   const int pb = v->ptr_bytes ? v->ptr_bytes : v->idx_bytes;
   if (v->jc || (v->idx_bytes != 8 && v->idx_bytes != 4) || (pb != 8 && pb != 4)) return CBG_EINVAL;
   HIPCHK(hipSetDevice(ctx->device));
-  std::unique_ptr<Owner> own(new Owner);
+  std::unique_ptr<Owner> own(new Owner(ctx->pool));
   hipStream_t st = ctx->stream;
   const hipMemcpyKind kind = v->on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
   HIPCHK(own->cp.reserve(8 * (v->ncol + 1)));

@@ -13,6 +13,7 @@
 #include <vector>
 #include <algorithm>
 #include <memory>
+#include <map>
 #include "cbgpu.h"
 #include "spgemm_kernels.hpp"
 
@@ -62,8 +63,52 @@ template <> struct DtOf<int64_t> { static constexpr cbg_dtype value = CBG_I64; }
 template <> struct DtOf<int32_t> { static constexpr cbg_dtype value = CBG_I32; };
 template <> struct DtOf<uint8_t> { static constexpr cbg_dtype value = CBG_BOOL; };
 
+// Caching pool for result storage.  A product's output is gigabytes at scale 20 and a fresh
+// hipMalloc/hipFree of it costs far more than the product; like PyTorch's caching allocator, freed
+// result blocks are kept per context and handed to the next result that fits (within 1.5x).
+struct Pool {
+  std::multimap<size_t, void*> free_;
+  ~Pool() { trim(); }
+  hipError_t get(size_t bytes, void** p, size_t* cap) {
+    auto it = free_.lower_bound(bytes);
+    if (it != free_.end() && it->first <= bytes + bytes / 2 + (1u << 20)) {
+      *p = it->second;
+      *cap = it->first;
+      free_.erase(it);
+      return hipSuccess;
+    }
+    hipError_t e = hipMalloc(p, bytes);
+    if (e != hipSuccess && !free_.empty()) {   // give cached blocks back and retry once
+      (void)hipGetLastError();
+      trim();
+      e = hipMalloc(p, bytes);
+    }
+    if (e == hipSuccess) *cap = bytes;
+    return e;
+  }
+  void put(void* p, size_t cap) { free_.emplace(cap, p); }
+  void trim() {
+    for (auto& kv : free_) (void)hipFree(kv.second);
+    free_.clear();
+  }
+};
+
+struct PoolBuf {
+  std::shared_ptr<Pool> pool;
+  void* p = nullptr;
+  size_t n = 0;
+  ~PoolBuf() { if (p) pool->put(p, n); }
+  hipError_t reserve(size_t bytes) {
+    if (bytes <= n) return hipSuccess;
+    if (p) { pool->put(p, n); p = nullptr; n = 0; }
+    return pool->get(bytes ? bytes : 16, &p, &n);
+  }
+  template <typename T> T* as() const { return (T*)p; }
+};
+
 struct Owner {                 // device storage behind a cbg_csc_result
-  DevBuf cp, ir, val;
+  PoolBuf cp, ir, val;
+  explicit Owner(const std::shared_ptr<Pool>& pl) { cp.pool = ir.pool = val.pool = pl; }
 };
 
 }  // namespace host
@@ -76,6 +121,7 @@ struct cbg_ctx {
   hipStream_t stream = nullptr;
   bool own_stream = false;
   hipEvent_t ev[8] = {};
+  std::shared_ptr<Pool> pool = std::make_shared<Pool>();
   cbg_profile prof{};
   // workspace (grow-only)
   DevBuf flop, span, cnt, list, hist, cursor, scan_tiles, scalars, cur, nxt, ovf_list, stageA[5], stageB[5];
@@ -199,8 +245,8 @@ inline cbg_status bin_fill(hipStream_t st, int64_t n, const int64_t* cnt, const 
 // ------------------------------------------------------------------------------- launch helpers
 template <int LOGT>
 void launch_sym_wave(hipStream_t st, const int32_t* l, int64_t n, const int64_t* Acp, const int32_t* Air,
-                     const int64_t* Bcp, const int32_t* Bir, const int2* span, int64_t* nnz) {
-  k_sym_wave<LOGT><<<(int)grid_for(n, 4, kMaxGrid * 2), 256, 0, st>>>(l, n, Acp, Air, Bcp, Bir, span, nnz);
+                     const int64_t* Bcp, const int32_t* Bir, const int2* span, int64_t* nnz, const HeavyOut& ho) {
+  k_sym_wave<LOGT><<<(int)grid_for(n, 4, kMaxGrid * 2), 256, 0, st>>>(l, n, Acp, Air, Bcp, Bir, span, nnz, ho);
 }
 template <int LOGT, int NT>
 hipError_t launch_sym_block(hipStream_t st, const int32_t* l, int64_t n, const int64_t* Acp, const int32_t* Air,
@@ -279,7 +325,7 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
   if (Av->ncol != Bv->nrow) return CBG_EDIM;
   const int64_t M = Av->nrow, N = Bv->ncol;
 
-  std::unique_ptr<Owner> own(new Owner);
+  std::unique_ptr<Owner> own(new Owner(ctx->pool));
   memset(C, 0, sizeof(*C));
   C->nrow = M; C->ncol = N;
   C->val_type = DtOf<V>::value;
@@ -352,11 +398,11 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
   {
     auto L = [&](int c) { return list + cs.off[c]; };
     auto n = [&](int c) { return (int64_t)cs.hist[c]; };
-    if (n(1)) launch_sym_wave<6>(st, L(1), n(1), A.cp, A.ir, B.cp, B.ir, span, nnz);
-    if (n(2)) launch_sym_wave<7>(st, L(2), n(2), A.cp, A.ir, B.cp, B.ir, span, nnz);
-    if (n(3)) launch_sym_wave<8>(st, L(3), n(3), A.cp, A.ir, B.cp, B.ir, span, nnz);
-    if (n(4)) launch_sym_wave<9>(st, L(4), n(4), A.cp, A.ir, B.cp, B.ir, span, nnz);
-    if (n(5)) launch_sym_wave<10>(st, L(5), n(5), A.cp, A.ir, B.cp, B.ir, span, nnz);
+    if (n(1)) launch_sym_wave<6>(st, L(1), n(1), A.cp, A.ir, B.cp, B.ir, span, nnz, ho);
+    if (n(2)) launch_sym_wave<7>(st, L(2), n(2), A.cp, A.ir, B.cp, B.ir, span, nnz, ho);
+    if (n(3)) launch_sym_wave<8>(st, L(3), n(3), A.cp, A.ir, B.cp, B.ir, span, nnz, ho);
+    if (n(4)) launch_sym_wave<9>(st, L(4), n(4), A.cp, A.ir, B.cp, B.ir, span, nnz, ho);
+    if (n(5)) launch_sym_wave<10>(st, L(5), n(5), A.cp, A.ir, B.cp, B.ir, span, nnz, ho);
     hipError_t e = hipSuccess;
     if (n(6) && e == hipSuccess) e = launch_sym_block<11, 256>(st, L(6), n(6), A.cp, A.ir, B.cp, B.ir, span, nnz, ho);
     if (n(7) && e == hipSuccess) e = launch_sym_block<12, 256>(st, L(7), n(7), A.cp, A.ir, B.cp, B.ir, span, nnz, ho);
@@ -431,6 +477,10 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
   if (H > 0 && (s = bin_fill(st, nunit_cap, ctx->ucnt.as<int64_t>(), ctx->uspan.as<int2>(), nbp, hist + 64, hn + 64,
                              ctx->ulist.as<int32_t>(), &cu)) != CBG_OK)
     return s;
+  if (cn.hist[kNumWave + kNumBlock + 1] != 0) {   // every column above kHeavy must have become units
+    fprintf(stderr, "cbgpu: %llu unbinned numeric columns\n", (unsigned long long)cn.hist[kNumWave + kNumBlock + 1]);
+    return CBG_EDEVICE;
+  }
   for (int c = 0; c < 12; ++c) pf.bins[c] = (int64_t)cn.hist[c];
   pf.bins[12] = H;
   for (int c = 1; c < 12 && H > 0; ++c) pf.bins[13] += (int64_t)cu.hist[c];

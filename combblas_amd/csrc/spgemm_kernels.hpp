@@ -412,7 +412,8 @@ template <int LOGT>
 __global__ void __launch_bounds__(256) k_sym_wave(const int32_t* __restrict__ list, int64_t count,
                                                   const int64_t* __restrict__ Acp, const int32_t* __restrict__ Air,
                                                   const int64_t* __restrict__ Bcp, const int32_t* __restrict__ Bir,
-                                                  const int2* __restrict__ span, int64_t* __restrict__ nnz) {
+                                                  const int2* __restrict__ span, int64_t* __restrict__ nnz,
+                                                  HeavyOut ho) {
   constexpr int T = 1 << LOGT;
   __shared__ int32_t s_tab[4][T];
   __shared__ int32_t s_wq[4][kWave];
@@ -447,6 +448,26 @@ __global__ void __launch_bounds__(256) k_sym_wave(const int32_t* __restrict__ li
         });
     int64_t tot = wave_sum64(cnt);
     if (l == 0) nnz[j] = tot;
+    if (tot > kHeavy) {
+      // only a bitmap table can hold more than kHeavy rows (a hash of T <= 1024 keys holds <= 512):
+      // register the column as heavy and count its rows per subwindow, like k_sym_block
+      int h = 0;
+      if (l == 0) {
+        h = atomicAdd(ho.n, 1);
+        ho.cols[h] = j;
+      }
+      h = __shfl(h, 0, kWave);
+      const int32_t sf = sp.x >> ho.log, sl = sp.y >> ho.log;
+      const int nw = ((sp.y - base) >> 5) + 1;
+      int32_t* dst = ho.sub + (int64_t)h * ho.nsub;
+      for (int32_t s = sf; s <= sl; ++s) {
+        int c = 0;
+        for (int w = l; w < nw; w += kWave)
+          if (((base + 32 * w) >> ho.log) == s) c += __popc((uint32_t)tab[w]);
+        const int64_t cs = wave_sum64(c);
+        if (l == 0) dst[s] = (int32_t)cs;
+      }
+    }
     wave_sync();
   }
 }
@@ -984,7 +1005,9 @@ __global__ void __launch_bounds__(NT) k_window(const int32_t* __restrict__ list,
     int64_t outpos = (MODE == 1) ? colptr[j] : 0;
     int64_t total = 0;
     int aerr = 0;
-    const int32_t start = sp.x & ~31;
+    // MODE 0 windows start on a subwindow boundary (W is a multiple of SUBW), so no subwindow's
+    // count straddles two windows; MODE 1 windows only need 32-row alignment for the bitmap.
+    const int32_t start = (MODE == 0) ? ((sp.x >> ho.log) << ho.log) : (sp.x & ~31);
     for (int64_t r0 = start; r0 <= sp.y; r0 += W) {
       const int32_t r1 = (int32_t)min<int64_t>(r0 + W, (int64_t)sp.y + 1);
       for (int s = threadIdx.x; s < NWORD; s += NT) bits[s] = 0u;

@@ -223,7 +223,9 @@ def test_gpu_unit_overflow_fallback(gpu_ctx):
     """A heavy column (nnz > 4096 -> units) whose multi-subwindow unit has its rows packed at the top:
     the unit's order-preserving hash overflows and is re-run as dense single-subwindow units."""
     W = 8192
-    rows = np.r_[np.arange(10), np.arange(6 * W - 3000, 6 * W), 20 * W + np.arange(0, 4000, 2)].astype(np.int32)
+    # 3000 rows packed under the top of the first unit's range [0, 20W): their order-preserving homes
+    # sit within 150 slots of T = 8192, so linear probing runs past the table tail
+    rows = np.r_[np.arange(10), np.arange(20 * W - 3000, 20 * W), 20 * W + np.arange(0, 4000, 2)].astype(np.int32)
     n = 1 << 20
     A = Csc(n, 1, [0, len(rows)], rows, np.arange(1, len(rows) + 1, dtype=np.float64))
     B = Csc(1, 1, [0, 1], [0], np.array([2.0]))
