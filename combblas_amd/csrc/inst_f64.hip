@@ -9,3 +9,16 @@ cbg_status cbg_merge_f64(cbg_ctx* ctx, const cbg_csc_result* parts, int32_t k, c
                            cbg_csc_result* C) {
   return cbg::host::merge_impl<double>(ctx, parts, k, sr, f, C);
 }
+
+#ifdef CBG_STAMPS
+extern "C" cbg_status cbg_debug_stamps(uint64_t* out, int reset) {
+  unsigned long long h[32];
+  if (hipMemcpyFromSymbol(h, HIP_SYMBOL(cbg::g_stamps), sizeof(h)) != hipSuccess) return CBG_EDEVICE;
+  for (int i = 0; i < 32; ++i) out[i] = h[i];
+  if (reset) {
+    memset(h, 0, sizeof(h));
+    if (hipMemcpyToSymbol(HIP_SYMBOL(cbg::g_stamps), h, sizeof(h)) != hipSuccess) return CBG_EDEVICE;
+  }
+  return CBG_OK;
+}
+#endif

@@ -126,6 +126,7 @@ struct cbg_ctx {
   // workspace (grow-only)
   DevBuf flop, span, cnt, list, hist, cursor, scan_tiles, scalars, cur, nxt, ovf_list, stageA[5], stageB[5];
   DevBuf split_idx, long_cols, split_tab, heavy_cols, sub, units, ucnt, uspan, ulist, fb_units, fb_list, uovf_list;
+  DevBuf nunits, segsz, segoff, useg, icnt, itemoff, items;
 };
 
 inline hipError_t launch_cfg_lds(const void* fn, size_t lds) {
@@ -252,7 +253,7 @@ template <int LOGT, int NT>
 hipError_t launch_sym_block(hipStream_t st, const int32_t* l, int64_t n, const int64_t* Acp, const int32_t* Air,
                             const int64_t* Bcp, const int32_t* Bir, const int2* span, int64_t* nnz,
                             const HeavyOut& ho) {
-  const size_t lds = (size_t)(1 << LOGT) * 4 + (size_t)NT * 17 + (size_t)(kMaxSub + 2) * 4 + 64;
+  const size_t lds = sym_block_lds<LOGT, NT>();
   hipError_t e = launch_cfg_lds((const void*)k_sym_block<LOGT, NT>, lds);
   if (e != hipSuccess) return e;
   k_sym_block<LOGT, NT><<<(int)grid_for(n, 1, kMaxGrid), NT, lds, st>>>(l, n, Acp, Air, Bcp, Bir, span, nnz, ho);
@@ -273,6 +274,17 @@ hipError_t launch_num_block(hipStream_t st, const int32_t* l, const int* n_dev, 
   hipError_t e = launch_cfg_lds((const void*)k_num_block<SRT, V, LOGT, NT, UNIT>, lds);
   if (e != hipSuccess) return e;
   k_num_block<SRT, V, LOGT, NT, UNIT><<<(int)grid, NT, lds, st>>>(l, n_dev, n, units, A, B, span, colptr, spl, o);
+  return hipGetLastError();
+}
+template <int LOGT, int NT, class SRT, typename V>
+hipError_t launch_num_heavy(hipStream_t st, int64_t nitems, const HeavyItem* items, const int32_t* hcols,
+                            const Unit* units, int32_t nsub, const DevCsc<V>& A, const DevCsc<V>& B, const int2* span,
+                            const Split& spl, const NumOut<V>& o) {
+  if (nitems <= 0) return hipSuccess;
+  const size_t lds = num_heavy_lds<SRT, V, LOGT, NT>();
+  hipError_t e = launch_cfg_lds((const void*)k_num_heavy<SRT, V, LOGT, NT>, lds);
+  if (e != hipSuccess) return e;
+  k_num_heavy<SRT, V, LOGT, NT><<<(int)nitems, NT, lds, st>>>(items, hcols, units, nsub, A, B, span, spl, o);
   return hipGetLastError();
 }
 template <int MODE, class SRT, typename V, int W>
@@ -457,39 +469,65 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
     HIPCHK(ctx->uovf_list.reserve(sizeof(int32_t) * (nunit_cap + 1)));
     HIPCHK(hipMemsetAsync(ctx->ucnt.p, 0, sizeof(int64_t) * nunit_cap, st));
     units = ctx->units.as<Unit>();
+    HIPCHK(ctx->nunits.reserve(sizeof(int32_t) * (H + 1)));
+    HIPCHK(ctx->segsz.reserve(sizeof(int64_t) * (H + 1)));
+    HIPCHK(ctx->segoff.reserve(sizeof(int64_t) * (H + 1)));
+    HIPCHK(ctx->icnt.reserve(sizeof(int64_t) * (H + 1)));
+    HIPCHK(ctx->itemoff.reserve(sizeof(int64_t) * (H + 1)));
     k_build_units<<<(H + 255) / 256, 256, 0, st>>>(H, ctx->heavy_cols.as<int32_t>(), ctx->sub.as<int32_t>(), nsub,
-                                                   slog, span, colptr, units, ctx->ucnt.as<int64_t>(),
-                                                   ctx->uspan.as<int2>(), nnz);
+                                                   slog, span, colptr, B.cp, units, ctx->ucnt.as<int64_t>(),
+                                                   ctx->uspan.as<int2>(), nnz, ctx->nunits.as<int32_t>(),
+                                                   ctx->segsz.as<int64_t>(), ctx->icnt.as<int64_t>());
+    // offsets of every heavy column's block of (unit, B nonzero) segments; total -> sc[8]
+    const int64_t ht = (H + kScanTile - 1) / kScanTile;
+    k_scan_tiles<<<(int)ht, 256, 0, st>>>(H, ctx->segsz.as<int64_t>(), ctx->scan_tiles.as<int64_t>());
+    k_scan_sums<<<1, 1024, 0, st>>>(ht, ctx->scan_tiles.as<int64_t>(), (int64_t*)(sc + 8));
+    k_scan_apply<<<(int)ht, 256, 0, st>>>(H, ctx->segsz.as<int64_t>(), ctx->scan_tiles.as<int64_t>(),
+                                          ctx->segoff.as<int64_t>());
+    // the same for the heavy items (groups of kItemUnits units); total -> sc[9]
+    k_scan_tiles<<<(int)ht, 256, 0, st>>>(H, ctx->icnt.as<int64_t>(), ctx->scan_tiles.as<int64_t>());
+    k_scan_sums<<<1, 1024, 0, st>>>(ht, ctx->scan_tiles.as<int64_t>(), (int64_t*)(sc + 9));
+    k_scan_apply<<<(int)ht, 256, 0, st>>>(H, ctx->icnt.as<int64_t>(), ctx->scan_tiles.as<int64_t>(),
+                                          ctx->itemoff.as<int64_t>());
     HIPCHK(hipGetLastError());
   }
 
   // 5. numeric binning (columns and units, one host sync) + kernels
-  Classes cn, cu;
+  Classes cn;
   BinParams nbp{kNumWave, kNumBlock, 64, 0};
   HIPCHK(hipMemsetAsync(hist, 0, sizeof(unsigned long long) * 128, st));
   bin_count(st, N, nnz, span, nbp, hist, list);
-  if (H > 0) bin_count(st, nunit_cap, ctx->ucnt.as<int64_t>(), ctx->uspan.as<int2>(), nbp, hist + 64,
-                       ctx->ulist.as<int32_t>());
-  unsigned long long hn[128];
+  unsigned long long hn[128], tots[2] = {0, 0};
   HIPCHK(hipMemcpyAsync(hn, hist, sizeof(unsigned long long) * 128, hipMemcpyDeviceToHost, st));
+  if (H > 0) HIPCHK(hipMemcpyAsync(tots, sc + 8, sizeof(tots), hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
+  const int64_t segtot = (int64_t)tots[0], nitems = (int64_t)tots[1];
+  if (H > 0) {
+    HIPCHK(ctx->useg.reserve(sizeof(UnitSeg) * (segtot + 1)));
+    HIPCHK(ctx->items.reserve(sizeof(HeavyItem) * (nitems + 1)));
+    spl.useg = ctx->useg.as<UnitSeg>();
+    k_unit_segs<<<H, 256, 0, st>>>(ctx->heavy_cols.as<int32_t>(), ctx->nunits.as<int32_t>(),
+                                   ctx->segoff.as<int64_t>(), units, nsub, A.cp, A.ir, B.cp, B.ir, spl,
+                                   ctx->useg.as<UnitSeg>());
+    k_heavy_items<<<(H + 255) / 256, 256, 0, st>>>(H, ctx->nunits.as<int32_t>(), ctx->itemoff.as<int64_t>(),
+                                                   ctx->items.as<HeavyItem>());
+    HIPCHK(hipGetLastError());
+  }
   if ((s = bin_fill(st, N, nnz, span, nbp, hist, hn, list, &cn)) != CBG_OK) return s;
-  if (H > 0 && (s = bin_fill(st, nunit_cap, ctx->ucnt.as<int64_t>(), ctx->uspan.as<int2>(), nbp, hist + 64, hn + 64,
-                             ctx->ulist.as<int32_t>(), &cu)) != CBG_OK)
-    return s;
   if (cn.hist[kNumWave + kNumBlock + 1] != 0) {   // every column above kHeavy must have become units
     fprintf(stderr, "cbgpu: %llu unbinned numeric columns\n", (unsigned long long)cn.hist[kNumWave + kNumBlock + 1]);
     return CBG_EDEVICE;
   }
   for (int c = 0; c < 12; ++c) pf.bins[c] = (int64_t)cn.hist[c];
   pf.bins[12] = H;
-  for (int c = 1; c < 12 && H > 0; ++c) pf.bins[13] += (int64_t)cu.hist[c];
+  pf.bins[13] = nitems;
   NumOut<V> oc{own->ir.as<int32_t>(), own->val.as<V>(), adderr, ovf_n, ctx->ovf_list.as<int32_t>()};
   {
     hipError_t e = launch_numeric_classes<SRT, V, false>(st, cn, list, nullptr, A, B, span, colptr, spl, oc);
     if (e == hipSuccess && H > 0) {
       NumOut<V> ou{own->ir.as<int32_t>(), own->val.as<V>(), adderr, uovf_n, ctx->uovf_list.as<int32_t>()};
-      e = launch_numeric_classes<SRT, V, true>(st, cu, ctx->ulist.as<int32_t>(), units, A, B, span, colptr, spl, ou);
+      e = launch_num_heavy<13, 1024, SRT, V>(st, nitems, ctx->items.as<HeavyItem>(), ctx->heavy_cols.as<int32_t>(),
+                                             units, nsub, A, B, span, spl, ou);
       // overflowed hash units -> single-subwindow (dense) units
       if (e == hipSuccess) {
         k_split_overflow_units<<<(int)grid_for(nunit_cap, 256, 1 << 20), 256, 0, st>>>(

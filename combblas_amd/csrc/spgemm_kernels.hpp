@@ -26,9 +26,9 @@
 // subwindow boundary inside each long A column).  Units are independent, so a column with 250k
 // outputs spreads over ~60 workgroups instead of one.
 //
-// Inside a work item the multiplies are the union of A-column segments A(:,k), k in B(:,j).  Short
-// segments are walked by one lane, long ones by a whole wavefront (coalesced); both issue kUnroll
-// independent loads before their LDS inserts so that each lane keeps several misses in flight.
+// Inside a work item the multiplies are the union of A-column segments A(:,k), k in B(:,j); they are
+// flattened and dealt to lanes evenly (for_each_multiply), so power-law segment lengths cost no
+// imbalance and every lane keeps kUnroll independent gathers in flight.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -39,12 +39,15 @@ namespace {  // internal linkage: every translation unit instantiates its own ke
 
 constexpr int kWave = 64;
 constexpr int32_t kEmpty = -1;
-constexpr int kLong = 64;          // segment length handed to a whole wavefront
-constexpr int kUnroll = 4;         // independent loads in flight per lane
+constexpr int kLong = 64;          // k_window: segment length handed to a whole wavefront
+constexpr int kUnroll = 4;         // independent gathers in flight per lane (numeric)
+constexpr int kUnrollSym = 8;      // same, symbolic (4-byte items)
+constexpr int kUnrollHeavy = 8;    // same, k_num_heavy (few multiplies per lane per chunk: all in flight)
 constexpr int64_t kHeavy = 4096;   // nnz(C(:,j)) above which a column is split into units
 constexpr int64_t kUnitCap = 4096; // max outputs of a multi-subwindow unit (T = 8192, load <= 0.5)
-constexpr int kSplitMin = 64;      // A columns at least this long get split-table rows
-constexpr int kMaxSub = 2048;      // max subwindows per column (SUBW chosen so nrow/SUBW <= kMaxSub)
+constexpr int kSplitMin = 16;      // A columns at least this long get split-table rows
+constexpr int kMaxSub = 2048;
+constexpr int kItemUnits = 8;      // units of one heavy column per workgroup item (k_num_heavy)      // max subwindows per column (SUBW chosen so nrow/SUBW <= kMaxSub)
 
 template <typename V>
 struct DevCsc {
@@ -55,11 +58,13 @@ struct DevCsc {
 };
 
 // split table: for long A columns, tab[idx[k]*(nsub+1) + s] = (first entry with row >= s*SUBW) - cp[k]
+struct UnitSeg;
 struct Split {
   const int32_t* idx;   // per A column: row of tab, or -1
   const int32_t* tab;
   int32_t nsub;         // subwindows in the row space
   int32_t log;          // log2(SUBW)
+  const UnitSeg* useg;  // precomputed unit segments (k_unit_segs)
 };
 
 struct Unit {
@@ -67,6 +72,11 @@ struct Unit {
   int32_t s0, s1;       // subwindows [s0, s1)
   int32_t cnt;          // outputs
   int64_t outoff;       // position of the first output in C
+  int64_t segbase;      // this unit's A segments in the precomputed table (UnitSeg), or -1
+};
+
+struct UnitSeg {        // A segment [a0, a1) of one (unit, B nonzero) pair
+  int64_t a0, a1;
 };
 
 // per-item description shared by all numeric/symbolic kernels
@@ -75,6 +85,7 @@ struct Work {
   int32_t lo, hi;       // row range [lo, hi]
   int32_t s0, s1;       // unit subwindows, s0 < 0 for a whole column
   int64_t ob;           // output offset (numeric)
+  int64_t segbase;      // unit: precomputed segments (index of B(:,j)'s first nonzero), or -1
 };
 
 template <typename V>
@@ -87,6 +98,26 @@ __device__ __forceinline__ void wave_sync() {
 }
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & (kWave - 1); }
+
+// Diagnostic build only (-DCBG_STAMPS, tools/diag): per-phase cycle sums of thread 0 of every
+// workgroup, read back with cbg_debug_stamps.  No stamp executes in the product library.
+#ifdef CBG_STAMPS
+__device__ unsigned long long g_stamps[32];
+#define STAMP_DECL unsigned long long st_prev_ = 0;
+#define STAMP(i)                                                                        \
+  do {                                                                                  \
+    if (threadIdx.x == 0) {                                                             \
+      const unsigned long long t_ = __builtin_amdgcn_s_memtime();                       \
+      if (st_prev_) atomicAdd(&g_stamps[i], t_ - st_prev_);                             \
+      st_prev_ = t_;                                                                    \
+    }                                                                                   \
+  } while (0)
+#define STAMP_COUNT(i, v) do { if (threadIdx.x == 0) atomicAdd(&g_stamps[i], (unsigned long long)(v)); } while (0)
+#else
+#define STAMP_DECL
+#define STAMP(i) do {} while (0)
+#define STAMP_COUNT(i, v) do {} while (0)
+#endif
 
 // ---------------------------------------------------------------- wave / block scans (int32)
 __device__ __forceinline__ int wave_incl_scan(int v) {
@@ -133,18 +164,19 @@ __device__ __forceinline__ int64_t lower_bound_rows(const int32_t* __restrict__ 
   return lo;
 }
 
-// A segment of unit (s0, s1) inside column k
-__device__ __forceinline__ void unit_bounds(const int64_t* __restrict__ Acp, const int32_t* __restrict__ Air,
-                                            const Split& sp, int32_t k, int32_t s0, int32_t s1, int64_t& a0,
-                                            int64_t& a1) {
+// A segment of unit (s0, s1) inside column k: exact for split-table columns; a short column
+// (< kSplitMin entries) is taken whole and its rows outside the unit are dropped at insert time
+// (cheaper than two dependent binary searches per unit and B nonzero).
+__device__ __forceinline__ void unit_bounds(const int64_t* __restrict__ Acp, const Split& sp, int32_t k,
+                                            int32_t s0, int32_t s1, int64_t& a0, int64_t& a1) {
   const int64_t c0 = Acp[k], c1 = Acp[k + 1];
   if (c1 - c0 >= kSplitMin) {
     const int32_t* t = sp.tab + (int64_t)sp.idx[k] * (sp.nsub + 1);
     a0 = c0 + t[s0];
     a1 = c0 + t[s1];
   } else {
-    a0 = lower_bound_rows(Air, c0, c1, (int64_t)s0 << sp.log);
-    a1 = lower_bound_rows(Air, a0, c1, (int64_t)s1 << sp.log);
+    a0 = c0;
+    a1 = c1;
   }
 }
 
@@ -221,7 +253,7 @@ __device__ __forceinline__ int class_of(int64_t need, const BinParams& bp) {
 __device__ __forceinline__ int64_t need_of(int64_t cnt, int2 sp, int sym) {
   if (cnt <= 0 || sp.y < sp.x) return 0;
   const int64_t span = (int64_t)sp.y - sp.x + 1;
-  if (sym) return min(2 * cnt, (span + 31) / 32 + 1);
+  if (sym) return min(2 * cnt, (int64_t)((sp.y - (sp.x & ~31)) >> 5) + 1);   // exact bitmap words
   return min(2 * cnt, span);
 }
 
@@ -258,91 +290,122 @@ __global__ void __launch_bounds__(256) k_bin(int64_t n, const int64_t* __restric
 }
 
 // ============================================================================ segment expansion
-// Visit every multiply (q in A segment of b, b in B(:,j)[bs, be)) with NT lanes (a wavefront when
-// WAVE, else the block).  seg(b, a0, a1, bv) gives the A segment and B value of nonzero b;
+// Visit every multiply of a work item: q in the A segment of b, for b in B(:,j)[bs, be).  The B
+// nonzeros are taken NT at a time (a wavefront when WAVE, else the block); each lane computes its
+// segment (seg(b, a0, a1, bv)), a scan over the segment lengths gives every multiply a flat index
+// m, and then the NT lanes take consecutive m's: lane t handles m = m0 + u*NT + t and finds its
+// segment by a binary search over the LDS prefix offsets.  Every lane gets the same share of the
+// multiplies whatever the (power-law) segment lengths, consecutive lanes read consecutive A
+// entries of one segment (coalesced), and each lane keeps U independent gathers in flight.
 // ld(q) loads what an insert needs; ins(item, bv, q, b) inserts it.
 template <typename V>
-struct LongQ {          // LDS queue of long segments (block mode)
-  int64_t* a0;
-  int32_t* len;
-  int32_t* b;           // relative to bs
-  V* bv;
-  int* n;
+struct SegBuf {         // LDS, NT entries each (+ scan scratch for block mode)
+  int64_t* qb;          // a0 - off: the A index of flat multiply m in segment s is qb[s] + m
+  int64_t* off;         // exclusive prefix of segment lengths
+  V* bv;                // B value of the segment's nonzero
+  int64_t* scratch;     // block mode: NT/64 + 1 entries
 };
 
-template <int NT, bool WAVE, typename V, class SegF, class LdF, class InsF>
-__device__ __forceinline__ void for_each_multiply(int64_t bs, int64_t be, int32_t* wq, LongQ<V> lq, SegF seg,
-                                                  LdF ld, InsF ins) {
+__device__ __forceinline__ int64_t wave_incl_scan64(int64_t v) {
+  const int l = lane_id();
+#pragma unroll
+  for (int d = 1; d < kWave; d <<= 1) {
+    const int64_t t = __shfl_up(v, d, kWave);
+    if (l >= d) v += t;
+  }
+  return v;
+}
+
+// exclusive scan over the block (int64); the caller synchronises before `scratch` is reused
+template <int NT>
+__device__ __forceinline__ int64_t block_excl_scan64(int64_t v, int64_t* scratch, int64_t* total) {
+  constexpr int NW = NT / kWave;
+  const int w = threadIdx.x / kWave, l = lane_id();
+  const int64_t inc = wave_incl_scan64(v);
+  if (l == kWave - 1) scratch[w] = inc;
+  __syncthreads();
+  if (threadIdx.x < kWave) {
+    const int64_t p = l < NW ? scratch[l] : 0;
+    const int64_t pi = wave_incl_scan64(p);
+    if (l < NW) scratch[l] = pi - p;
+    if (l == NW - 1) scratch[NW] = pi;
+  }
+  __syncthreads();
+  *total = scratch[NW];
+  return scratch[w] + inc - v;
+}
+
+// last s in [0, P) with off[s] <= m (off non-decreasing, off[0] = 0 <= m): the non-empty segment
+// holding flat multiply m.  P is a power of two covering the staged segments (P <= NT).
+template <int NT>
+__device__ __forceinline__ int seg_search(const int64_t* off, int64_t m, int P) {
+  int s = 0;
+  for (int step = P >> 1; step > 0; step >>= 1)
+    if (off[s + step] <= m) s += step;
+  return s;
+}
+
+// Stage one chunk of NT segments (this lane's a0, a1, bv) into LDS; returns the chunk's multiply
+// count.  The LDS arrays are valid on return (synchronised).
+template <int NT, bool WAVE, typename V>
+__device__ __forceinline__ int64_t stage_segments(const SegBuf<V>& sb, int64_t a0, int64_t a1, V bv) {
+  const int tid = WAVE ? lane_id() : (int)threadIdx.x;
+  const int64_t len = a1 - a0;
+  int64_t ex, F;
+  if constexpr (WAVE) {
+    const int64_t inc = wave_incl_scan64(len);
+    F = __shfl(inc, kWave - 1, kWave);
+    ex = inc - len;
+  } else {
+    ex = block_excl_scan64<NT>(len, sb.scratch, &F);
+  }
+  sb.qb[tid] = a0 - ex;
+  sb.off[tid] = ex;
+  sb.bv[tid] = bv;
+  if constexpr (WAVE) wave_sync(); else __syncthreads();
+  return F;
+}
+
+// Deal the F staged multiplies to the NT lanes (U independent gathers in flight per lane).
+// `base` is the B position of staged segment 0.  The caller synchronises before re-staging.
+template <int NT, int U, typename V, class LdF, class InsF>
+__device__ __forceinline__ void expand_staged(const SegBuf<V>& sb, int tid, int64_t F, int64_t base, int nseg,
+                                              LdF ld, InsF ins) {
   using Item = decltype(ld(int64_t(0)));
+  int P = 1;
+  while (P < nseg) P <<= 1;
+  for (int64_t m0 = 0; m0 < F; m0 += (int64_t)NT * U) {
+    Item it[U];
+    int ss[U];
+    int64_t qq[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t m = m0 + (int64_t)u * NT + tid;
+      if (m < F) {
+        ss[u] = seg_search<NT>(sb.off, m, P);
+        qq[u] = sb.qb[ss[u]] + m;
+        it[u] = ld(qq[u]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t m = m0 + (int64_t)u * NT + tid;
+      if (m < F) ins(it[u], sb.bv[ss[u]], qq[u], base + ss[u]);
+    }
+  }
+}
+
+template <int NT, bool WAVE, int U, typename V, class SegF, class LdF, class InsF>
+__device__ __forceinline__ void for_each_multiply(int64_t bs, int64_t be, SegBuf<V> sb, SegF seg, LdF ld, InsF ins) {
   const int tid = WAVE ? lane_id() : (int)threadIdx.x;
   for (int64_t base = bs; base < be; base += NT) {
     const int64_t b = base + tid;
     int64_t a0 = 0, a1 = 0;
     V bv = V(0);
     if (b < be) seg(b, a0, a1, bv);
-    const bool islong = (a1 - a0) >= kLong;
-    if (!islong) {
-      for (int64_t q = a0; q < a1; q += kUnroll) {
-        Item it[kUnroll];
-#pragma unroll
-        for (int u = 0; u < kUnroll; ++u)
-          if (q + u < a1) it[u] = ld(q + u);
-#pragma unroll
-        for (int u = 0; u < kUnroll; ++u)
-          if (q + u < a1) ins(it[u], bv, q + u, b);
-      }
-    }
-    if constexpr (WAVE) {
-      const unsigned long long m = __ballot(islong);
-      const int pos = __popcll(m & ((1ull << lane_id()) - 1));
-      if (islong) wq[pos] = tid;
-      wave_sync();
-      const int nl = __popcll(m);
-      for (int i = 0; i < nl; ++i) {
-        const int src = wq[i];
-        const int64_t sb = base + src;
-        const int64_t s0 = __shfl(a0, src, kWave), s1 = __shfl(a1, src, kWave);
-        const V sbv = __shfl(bv, src, kWave);
-        for (int64_t q = s0 + lane_id(); q < s1; q += kWave * kUnroll) {
-          Item it[kUnroll];
-#pragma unroll
-          for (int u = 0; u < kUnroll; ++u)
-            if (q + u * kWave < s1) it[u] = ld(q + u * kWave);
-#pragma unroll
-          for (int u = 0; u < kUnroll; ++u)
-            if (q + u * kWave < s1) ins(it[u], sbv, q + u * kWave, sb);
-        }
-      }
-      wave_sync();
-    } else {
-      if (threadIdx.x == 0) *lq.n = 0;
-      __syncthreads();
-      if (islong) {
-        const int e = atomicAdd(lq.n, 1);
-        lq.a0[e] = a0;
-        lq.len[e] = (int32_t)(a1 - a0);
-        lq.b[e] = tid;
-        lq.bv[e] = bv;
-      }
-      __syncthreads();
-      const int nl = *lq.n;
-      constexpr int NW = NT / kWave;
-      for (int e = threadIdx.x / kWave; e < nl; e += NW) {
-        const int64_t sb = base + lq.b[e];
-        const int64_t s0 = lq.a0[e], s1 = s0 + lq.len[e];
-        const V sbv = lq.bv[e];
-        for (int64_t q = s0 + lane_id(); q < s1; q += kWave * kUnroll) {
-          Item it[kUnroll];
-#pragma unroll
-          for (int u = 0; u < kUnroll; ++u)
-            if (q + u * kWave < s1) it[u] = ld(q + u * kWave);
-#pragma unroll
-          for (int u = 0; u < kUnroll; ++u)
-            if (q + u * kWave < s1) ins(it[u], sbv, q + u * kWave, sb);
-        }
-      }
-      __syncthreads();
-    }
+    const int64_t F = stage_segments<NT, WAVE, V>(sb, a0, a1, bv);
+    expand_staged<NT, U, V>(sb, tid, F, base, (int)min<int64_t>(NT, be - base), ld, ins);
+    if constexpr (WAVE) wave_sync(); else __syncthreads();
   }
 }
 
@@ -408,6 +471,19 @@ struct HeavyOut {       // columns with nnz > kHeavy: list + nnz per subwindow
   int32_t nsub, log;
 };
 
+// symbolic insert of row r into a presence bitmap (base = 32-aligned first row) or a keys-only hash;
+// returns 1 if r is new
+template <int LOGT>
+__device__ __forceinline__ int sym_insert(int32_t* tab, bool bitmap, int32_t base, int32_t r) {
+  if (bitmap) {
+    const int32_t o = r - base;
+    const uint32_t bit = 1u << (o & 31);
+    if (tab[o >> 5] & bit) return 0;
+    return (atomicOr((uint32_t*)&tab[o >> 5], bit) & bit) ? 0 : 1;
+  }
+  return hash_insert_sym(tab, r, LOGT);
+}
+
 template <int LOGT>
 __global__ void __launch_bounds__(256) k_sym_wave(const int32_t* __restrict__ list, int64_t count,
                                                   const int64_t* __restrict__ Acp, const int32_t* __restrict__ Air,
@@ -416,9 +492,11 @@ __global__ void __launch_bounds__(256) k_sym_wave(const int32_t* __restrict__ li
                                                   HeavyOut ho) {
   constexpr int T = 1 << LOGT;
   __shared__ int32_t s_tab[4][T];
-  __shared__ int32_t s_wq[4][kWave];
+  __shared__ int64_t s_qb[4][kWave], s_off[4][kWave];
+  __shared__ uint8_t s_bv[4][kWave];
   const int w = threadIdx.x / kWave, l = lane_id();
   int32_t* tab = s_tab[w];
+  const SegBuf<uint8_t> sb{s_qb[w], s_off[w], s_bv[w], nullptr};
   const int64_t nwaves = (int64_t)gridDim.x * 4;
   for (int64_t i = blockIdx.x * 4 + w; i < count; i += nwaves) {
     const int32_t j = list[i];
@@ -428,24 +506,15 @@ __global__ void __launch_bounds__(256) k_sym_wave(const int32_t* __restrict__ li
     for (int s = l; s < T; s += kWave) tab[s] = bitmap ? 0 : kEmpty;
     wave_sync();
     int cnt = 0;
-    for_each_multiply<kWave, true, uint8_t>(
-        Bcp[j], Bcp[j + 1], s_wq[w], LongQ<uint8_t>{},
-        [&](int64_t b, int64_t& a0, int64_t& a1, uint8_t& bv) {
+    for_each_multiply<kWave, true, kUnrollSym, uint8_t>(
+        Bcp[j], Bcp[j + 1], sb,
+        [&](int64_t b, int64_t& a0, int64_t& a1, uint8_t&) {
           const int32_t k = Bir[b];
           a0 = Acp[k];
           a1 = Acp[k + 1];
-          bv = 0;
         },
         [&](int64_t q) { return Air[q]; },
-        [&](int32_t r, uint8_t, int64_t, int64_t) {
-          if (bitmap) {
-            const int32_t o = r - base;
-            const uint32_t bit = 1u << (o & 31);
-            if (!(tab[o >> 5] & bit)) cnt += (atomicOr((uint32_t*)&tab[o >> 5], bit) & bit) ? 0 : 1;
-          } else {
-            cnt += hash_insert_sym(tab, r, LOGT);
-          }
-        });
+        [&](int32_t r, uint8_t, int64_t, int64_t) { cnt += sym_insert<LOGT>(tab, bitmap, base, r); });
     int64_t tot = wave_sum64(cnt);
     if (l == 0) nnz[j] = tot;
     if (tot > kHeavy) {
@@ -462,8 +531,8 @@ __global__ void __launch_bounds__(256) k_sym_wave(const int32_t* __restrict__ li
       int32_t* dst = ho.sub + (int64_t)h * ho.nsub;
       for (int32_t s = sf; s <= sl; ++s) {
         int c = 0;
-        for (int w = l; w < nw; w += kWave)
-          if (((base + 32 * w) >> ho.log) == s) c += __popc((uint32_t)tab[w]);
+        for (int w2 = l; w2 < nw; w2 += kWave)
+          if (((base + 32 * w2) >> ho.log) == s) c += __popc((uint32_t)tab[w2]);
         const int64_t cs = wave_sum64(c);
         if (l == 0) dst[s] = (int32_t)cs;
       }
@@ -474,6 +543,11 @@ __global__ void __launch_bounds__(256) k_sym_wave(const int32_t* __restrict__ li
 
 // block kernel: one column per workgroup; heavy columns also report nnz per subwindow
 template <int LOGT, int NT>
+constexpr size_t sym_block_lds() {
+  return (size_t)(1 << LOGT) * 4 + (size_t)NT * 17 + (size_t)(NT / kWave + 1) * 8 + (size_t)(kMaxSub + 2) * 4 + 64;
+}
+
+template <int LOGT, int NT>
 __global__ void __launch_bounds__(NT) k_sym_block(const int32_t* __restrict__ list, int64_t count,
                                                   const int64_t* __restrict__ Acp, const int32_t* __restrict__ Air,
                                                   const int64_t* __restrict__ Bcp, const int32_t* __restrict__ Bir,
@@ -481,14 +555,14 @@ __global__ void __launch_bounds__(NT) k_sym_block(const int32_t* __restrict__ li
                                                   HeavyOut ho) {
   constexpr int T = 1 << LOGT;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  int32_t* tab = (int32_t*)smem;                  // T
-  int64_t* q_a0 = (int64_t*)(tab + T);            // NT
-  int32_t* q_len = (int32_t*)(q_a0 + NT);         // NT
-  int32_t* q_b = q_len + NT;                      // NT
-  int32_t* scnt = q_b + NT;                       // kMaxSub + 2
-  uint8_t* q_bv = (uint8_t*)(scnt + kMaxSub + 2); // NT
-  int* misc = (int*)(q_bv + NT);                  // [0] queue n, [1] total, [2] heavy id
-  LongQ<uint8_t> lq{q_a0, q_len, q_b, q_bv, &misc[0]};
+  int64_t* qb = (int64_t*)smem;                   // NT
+  int64_t* off = qb + NT;                         // NT
+  int64_t* scr = off + NT;                        // NT/64 + 1
+  int32_t* tab = (int32_t*)(scr + NT / kWave + 1);// T
+  int32_t* scnt = tab + T;                        // kMaxSub + 2
+  int* misc = scnt + kMaxSub + 2;                 // [1] total, [2] heavy id
+  uint8_t* bvs = (uint8_t*)(misc + 8);            // NT
+  const SegBuf<uint8_t> sb{qb, off, bvs, scr};
   for (int64_t i = blockIdx.x; i < count; i += gridDim.x) {
     const int32_t j = list[i];
     const int2 sp = span[j];
@@ -498,24 +572,15 @@ __global__ void __launch_bounds__(NT) k_sym_block(const int32_t* __restrict__ li
     if (threadIdx.x == 0) misc[1] = 0;
     __syncthreads();
     int cnt = 0;
-    for_each_multiply<NT, false, uint8_t>(
-        Bcp[j], Bcp[j + 1], nullptr, lq,
-        [&](int64_t b, int64_t& a0, int64_t& a1, uint8_t& bv) {
+    for_each_multiply<NT, false, kUnrollSym, uint8_t>(
+        Bcp[j], Bcp[j + 1], sb,
+        [&](int64_t b, int64_t& a0, int64_t& a1, uint8_t&) {
           const int32_t k = Bir[b];
           a0 = Acp[k];
           a1 = Acp[k + 1];
-          bv = 0;
         },
         [&](int64_t q) { return Air[q]; },
-        [&](int32_t r, uint8_t, int64_t, int64_t) {
-          if (bitmap) {
-            const int32_t o = r - base;
-            const uint32_t bit = 1u << (o & 31);
-            if (!(tab[o >> 5] & bit)) cnt += (atomicOr((uint32_t*)&tab[o >> 5], bit) & bit) ? 0 : 1;
-          } else {
-            cnt += hash_insert_sym(tab, r, LOGT);
-          }
-        });
+        [&](int32_t r, uint8_t, int64_t, int64_t) { cnt += sym_insert<LOGT>(tab, bitmap, base, r); });
     int64_t wc = wave_sum64(cnt);
     if (lane_id() == 0 && wc) atomicAdd(&misc[1], (int)wc);
     __syncthreads();
@@ -662,8 +727,9 @@ __global__ void __launch_bounds__(256) k_split_fill(int nlong, const int32_t* __
 // units of a heavy column: consecutive subwindows while the running count stays <= kUnitCap
 __global__ void k_build_units(int H, const int32_t* __restrict__ cols, const int32_t* __restrict__ sub, int32_t nsub,
                               int32_t log, const int2* __restrict__ span, const int64_t* __restrict__ colptr,
-                              Unit* __restrict__ units, int64_t* __restrict__ ucnt, int2* __restrict__ uspan,
-                              int64_t* __restrict__ nnz) {
+                              const int64_t* __restrict__ Bcp, Unit* __restrict__ units, int64_t* __restrict__ ucnt,
+                              int2* __restrict__ uspan, int64_t* __restrict__ nnz, int32_t* __restrict__ nunits,
+                              int64_t* __restrict__ segsz, int64_t* __restrict__ icnt) {
   const int h = blockIdx.x * blockDim.x + threadIdx.x;
   if (h >= H) return;
   const int32_t j = cols[h];
@@ -675,7 +741,7 @@ __global__ void k_build_units(int H, const int32_t* __restrict__ cols, const int
   int u = 0, st = sf;
   int64_t acc = 0;
   auto emit = [&](int32_t s0, int32_t s1, int64_t n) {
-    units[slot + u] = Unit{j, s0, s1, (int32_t)n, out};
+    units[slot + u] = Unit{j, s0, s1, (int32_t)n, out, -1};
     ucnt[slot + u] = n;
     const int64_t lo = max((int64_t)sp.x, (int64_t)s0 << log);
     const int64_t hi = min((int64_t)sp.y, ((int64_t)s1 << log) - 1);
@@ -694,6 +760,47 @@ __global__ void k_build_units(int H, const int32_t* __restrict__ cols, const int
   }
   if (acc > 0) emit(st, sl + 1, acc);
   nnz[j] = 0;   // the whole column is now covered by units
+  nunits[h] = u;
+  segsz[h] = (int64_t)u * (Bcp[j + 1] - Bcp[j]);
+  icnt[h] = (u + kItemUnits - 1) / kItemUnits;
+}
+
+// Segment table of every unit: for each heavy column, each B nonzero b = (k, B(k,j)) is visited once
+// and its A column's boundaries for all of the column's units are written (one split-table row read,
+// mostly from cache, instead of a dependent lookup chain per (unit, b) inside the numeric kernel).
+// Short A columns are given whole (rows outside a unit are dropped at insert time) unless their row
+// range misses the unit entirely.
+__global__ void __launch_bounds__(256) k_unit_segs(const int32_t* __restrict__ cols, const int32_t* __restrict__ nunits,
+                                                   const int64_t* __restrict__ segoff, Unit* __restrict__ units,
+                                                   int32_t nsub, const int64_t* __restrict__ Acp,
+                                                   const int32_t* __restrict__ Air, const int64_t* __restrict__ Bcp,
+                                                   const int32_t* __restrict__ Bir, Split sp, UnitSeg* __restrict__ seg) {
+  const int h = blockIdx.x;
+  const int32_t j = cols[h];
+  const int nu = nunits[h];
+  const int64_t bs = Bcp[j], nb = Bcp[j + 1] - bs;
+  const int64_t base = segoff[h];
+  Unit* U = units + (int64_t)h * nsub;
+  for (int u = threadIdx.x; u < nu; u += blockDim.x) U[u].segbase = base + (int64_t)u * nb;
+  for (int64_t i = threadIdx.x; i < nb; i += blockDim.x) {
+    const int32_t k = Bir[bs + i];
+    const int64_t c0 = Acp[k], c1 = Acp[k + 1];
+    UnitSeg* out = seg + base + i;
+    if (c1 - c0 >= kSplitMin) {
+      const int32_t* t = sp.tab + (int64_t)sp.idx[k] * (sp.nsub + 1);
+      for (int u = 0; u < nu; ++u) {
+        const Unit un = U[u];
+        out[(int64_t)u * nb] = UnitSeg{c0 + t[un.s0], c0 + t[un.s1]};
+      }
+    } else {
+      const int32_t rf = c1 > c0 ? Air[c0] : 0, rl = c1 > c0 ? Air[c1 - 1] : -1;
+      for (int u = 0; u < nu; ++u) {
+        const Unit un = U[u];
+        const bool hit = c1 > c0 && rl >= ((int64_t)un.s0 << sp.log) && rf < ((int64_t)un.s1 << sp.log);
+        out[(int64_t)u * nb] = hit ? UnitSeg{c0, c1} : UnitSeg{c0, c0};
+      }
+    }
+  }
 }
 // overflowed (hash) units -> single-subwindow units, which run in dense mode
 __global__ void k_split_overflow_units(const int* __restrict__ n_ovf, const int32_t* __restrict__ ovf,
@@ -710,7 +817,7 @@ __global__ void k_split_overflow_units(const int* __restrict__ n_ovf, const int3
     const int32_t n = sub[h * nsub + s];
     if (n > 0) {
       const int e = atomicAdd(n_out, 1);
-      out_units[e] = Unit{u.j, s, s + 1, n, off};
+      out_units[e] = Unit{u.j, s, s + 1, n, off, -1};
       out_list[e] = e;
       off += n;
     }
@@ -742,6 +849,7 @@ __device__ __forceinline__ Work get_work(const int32_t* __restrict__ list, int64
     w.lo = (int32_t)max((int64_t)sp.x, (int64_t)u.s0 << log);
     w.hi = (int32_t)min((int64_t)sp.y, ((int64_t)u.s1 << log) - 1);
     w.ob = u.outoff;
+    w.segbase = u.segbase;
   } else {
     const int32_t j = list[i];
     const int2 sp = span[j];
@@ -750,6 +858,7 @@ __device__ __forceinline__ Work get_work(const int32_t* __restrict__ list, int64
     w.lo = sp.x;
     w.hi = sp.y;
     w.ob = colptr ? colptr[j] : 0;
+    w.segbase = -1;
   }
   return w;
 }
@@ -785,8 +894,153 @@ __device__ __forceinline__ void compact_hash_runs(const int32_t* keys, const typ
   }
 }
 
+// Block compaction of an order-preserving hash table (TC = Te + NT slots, CH = TC/NT <= CHMAX per
+// thread) into C(:, ...) at `ob`: run-rank positions are computed from the table into registers,
+// the table is then reused as a staging buffer in output order, and the staged block is written
+// with consecutive lanes on consecutive addresses (coalesced) instead of one scattered store per
+// entry.  Contains barriers; the caller synchronises before the table is re-initialised.
+// Block compaction of an order-preserving hash table into C(:, ...) at `ob`, sorted by row, with no
+// per-run scans (a run-walking compaction is SIMD-divergent: a wave pays for the longest run among
+// its lanes).  home(r) is monotone in r, so the keys with a smaller home all precede r: with
+// cnt[h] = #keys whose home is h, r's output position is excl_scan(cnt)[home(r)] plus its rank among
+// the (rare, tiny) group of keys sharing its home.
+//   1. cnt[h] in LDS as packed 16-bit halves (hc: Te/2 words, caller-provided scratch);
+//   2. exclusive scan of the Te counts in place;
+//   3. each key takes base[h] + an atomic cursor, kept in registers with its accumulator;
+//   4. the table is reused as the staging buffer: (row, acc) written at their positions, then every
+//      home group of >= 2 keys is insertion-sorted by the thread owning that home;
+//   5. the staged block is written out coalesced.
+// TC = table slots (Te + tail), CH = ceil(TC/NT) <= CHMAX slots per thread (contiguous chunks).
+// Contains barriers; the caller synchronises before the table is re-initialised.
+template <class SRT, typename V, int NT, int CHMAX>
+__device__ __forceinline__ void compact_hash_homes(int32_t* keys, typename SRT::Acc* vals, int TC, int Te,
+                                                   int32_t lo, uint32_t mult, uint32_t* hc, int* scan,
+                                                   int64_t ob, const V* aval, const V* bval, int32_t* orow,
+                                                   V* oval) {
+  using Acc = typename SRT::Acc;
+  const int CH = (TC + NT - 1) / NT;
+  const int c0 = threadIdx.x * CH;
+  const int NW = Te >> 1;                        // packed count words
+  for (int w = threadIdx.x; w < NW; w += NT) hc[w] = 0u;
+  __syncthreads();
+  int32_t rk[CHMAX];
+  uint32_t hm[CHMAX];
+#pragma unroll
+  for (int i = 0; i < CHMAX; ++i) {
+    const int sl = c0 + i;
+    rk[i] = (i < CH && sl < TC) ? keys[sl] : kEmpty;
+    hm[i] = 0;
+    if (rk[i] != kEmpty) {
+      hm[i] = mono_home(rk[i], lo, mult);
+      atomicAdd(&hc[hm[i] >> 1], 1u << (16 * (hm[i] & 1)));
+    }
+  }
+  __syncthreads();
+  // exclusive scan over the Te 16-bit counts: thread t owns count words [w0, w1) (homes 2*w0 ...)
+  const int WP = (NW + NT - 1) / NT;
+  const int w0 = min(NW, (int)threadIdx.x * WP), w1 = min(NW, w0 + WP);
+  int local = 0;
+  for (int w = w0; w < w1; ++w) {
+    const uint32_t x = hc[w];
+    local += (int)(x & 0xffffu) + (int)(x >> 16);
+  }
+  int tot;
+  int run = block_excl_scan<NT>(local, scan, &tot);
+  for (int w = w0; w < w1; ++w) {
+    const uint32_t x = hc[w];
+    const uint32_t c_lo = x & 0xffffu, c_hi = x >> 16;
+    hc[w] = (uint32_t)run | ((uint32_t)(run + (int)c_lo) << 16);
+    run += (int)(c_lo + c_hi);
+  }
+  __syncthreads();
+  int ro[CHMAX];
+  Acc rv[CHMAX];
+#pragma unroll
+  for (int i = 0; i < CHMAX; ++i) {
+    ro[i] = -1;
+    if (rk[i] != kEmpty) {
+      const uint32_t sh = 16 * (hm[i] & 1);
+      ro[i] = (int)((atomicAdd(&hc[hm[i] >> 1], 1u << sh) >> sh) & 0xffffu);
+      rv[i] = vals[c0 + i];
+    }
+  }
+  __syncthreads();   // every table read is done: reuse keys/vals as the staging buffer
+#pragma unroll
+  for (int i = 0; i < CHMAX; ++i)
+    if (ro[i] >= 0) {
+      keys[ro[i]] = rk[i];
+      vals[ro[i]] = rv[i];
+    }
+  __syncthreads();
+  // home h's group is [end(h-1), end(h)), end = the advanced cursor; sort groups of >= 2 keys
+  for (int h = 2 * w0; h < 2 * w1; ++h) {
+    const uint32_t w = hc[h >> 1];
+    const int e = (int)((w >> (16 * (h & 1))) & 0xffffu);
+    int st;
+    if (h == 0) st = 0;
+    else { const uint32_t wp = hc[(h - 1) >> 1]; st = (int)((wp >> (16 * ((h - 1) & 1))) & 0xffffu); }
+    for (int i = st + 1; i < e; ++i) {
+      const int32_t k = keys[i];
+      const Acc v = vals[i];
+      int q = i - 1;
+      while (q >= st && keys[q] > k) {
+        keys[q + 1] = keys[q];
+        vals[q + 1] = vals[q];
+        --q;
+      }
+      keys[q + 1] = k;
+      vals[q + 1] = v;
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < tot; i += NT) {
+    orow[ob + i] = keys[i];
+    oval[ob + i] = SRT::out(vals[i], aval, bval);
+  }
+}
+
 // ---- wave numeric: one item per wavefront, table T slots (+kTail) per wave
 constexpr int kTail = 64;
+
+// one numeric insert (dense: bitmap + value slot; hash: order-preserving open addressing).  Unit
+// items drop rows outside their range (whole short A columns, see unit_bounds).
+template <class SRT, typename V, bool UNIT>
+__device__ __forceinline__ void num_insert(Table<typename SRT::Acc>& t, bool dense, const Work& wk, uint32_t mult,
+                                           const NumItem<V>& it, V bv, int64_t q, int64_t b, int& ovf, int& aerr) {
+  using Acc = typename SRT::Acc;
+  if constexpr (UNIT)
+    if (it.r < wk.lo || it.r > wk.hi) return;
+  const Acc x = SRT::mul(it.a, bv, q, b);
+  if (dense) {
+    const int32_t o = it.r - wk.lo;
+    const uint32_t bit = 1u << (o & 31);
+    const uint32_t old = atomicOr((uint32_t*)&t.keys[o >> 5], bit);
+    if (SRT::kAddIsError && (old & bit)) aerr = 1;
+    SRT::acc(&t.vals[o], x);
+  } else {
+    if (!hash_insert_num<SRT>(t, it.r, mono_home(it.r, wk.lo, mult), x, &aerr)) ovf = 1;
+  }
+}
+
+template <typename V, bool UNIT>
+__device__ __forceinline__ void num_seg(const DevCsc<V>& A, const DevCsc<V>& B, const Split& spl,
+                                        const UnitSeg* __restrict__ useg, const Work& wk, int64_t b, int64_t& a0,
+                                        int64_t& a1, V& bv) {
+  if constexpr (UNIT) {
+    if (wk.segbase >= 0) {
+      const UnitSeg sg = useg[wk.segbase + (b - B.cp[wk.j])];
+      a0 = sg.a0;
+      a1 = sg.a1;
+    } else {
+      unit_bounds(A.cp, spl, B.ir[b], wk.s0, wk.s1, a0, a1);
+    }
+  } else {
+    const int32_t k = B.ir[b];
+    a0 = A.cp[k];
+    a1 = A.cp[k + 1];
+  }
+  bv = load_val(B.val, b);
+}
 
 template <class SRT, typename V, int LOGT, bool UNIT>
 __global__ void __launch_bounds__(256) k_num_wave(const int32_t* __restrict__ list, int64_t count,
@@ -798,9 +1052,11 @@ __global__ void __launch_bounds__(256) k_num_wave(const int32_t* __restrict__ li
   constexpr int TC = T + kTail;
   __shared__ int32_t s_keys[4][TC];
   __shared__ Acc s_vals[4][TC];
-  __shared__ int32_t s_wq[4][kWave];
+  __shared__ int64_t s_qb[4][kWave], s_off[4][kWave];
+  __shared__ V s_bv[4][kWave];
   const int w = threadIdx.x / kWave, l = lane_id();
   Table<Acc> t{s_keys[w], s_vals[w], T, TC};
+  const SegBuf<V> sb{s_qb[w], s_off[w], s_bv[w], nullptr};
   const int64_t nwaves = (int64_t)gridDim.x * 4;
   for (int64_t i = blockIdx.x * 4 + w; i < count; i += nwaves) {
     const Work wk = get_work<UNIT>(list, i, units, span, colptr, spl.log);
@@ -810,26 +1066,12 @@ __global__ void __launch_bounds__(256) k_num_wave(const int32_t* __restrict__ li
     for (int s = l; s < TC; s += kWave) { t.keys[s] = dense ? 0 : kEmpty; t.vals[s] = SRT::identity(); }
     wave_sync();
     int ovf = 0, aerr = 0;
-    for_each_multiply<kWave, true, V>(
-        B.cp[wk.j], B.cp[wk.j + 1], s_wq[w], LongQ<V>{},
-        [&](int64_t b, int64_t& a0, int64_t& a1, V& bv) {
-          const int32_t k = B.ir[b];
-          if constexpr (UNIT) unit_bounds(A.cp, A.ir, spl, k, wk.s0, wk.s1, a0, a1);
-          else { a0 = A.cp[k]; a1 = A.cp[k + 1]; }
-          bv = load_val(B.val, b);
-        },
+    for_each_multiply<kWave, true, kUnroll, V>(
+        B.cp[wk.j], B.cp[wk.j + 1], sb,
+        [&](int64_t b, int64_t& a0, int64_t& a1, V& bv) { num_seg<V, UNIT>(A, B, spl, spl.useg, wk, b, a0, a1, bv); },
         [&](int64_t q) { return NumItem<V>{A.ir[q], load_val(A.val, q)}; },
         [&](const NumItem<V>& it, V bv, int64_t q, int64_t b) {
-          const Acc x = SRT::mul(it.a, bv, q, b);
-          if (dense) {
-            const int32_t o = it.r - wk.lo;
-            const uint32_t bit = 1u << (o & 31);
-            const uint32_t old = atomicOr((uint32_t*)&t.keys[o >> 5], bit);
-            if (SRT::kAddIsError && (old & bit)) aerr = 1;
-            SRT::acc(&t.vals[o], x);
-          } else {
-            if (!hash_insert_num<SRT>(t, it.r, mono_home(it.r, wk.lo, mult), x, &aerr)) ovf = 1;
-          }
+          num_insert<SRT, V, UNIT>(t, dense, wk, mult, it, bv, q, b, ovf, aerr);
         });
     wave_sync();
     const bool wov = __any(ovf);
@@ -865,7 +1107,8 @@ __global__ void __launch_bounds__(256) k_num_wave(const int32_t* __restrict__ li
 // ---- block numeric: one item per workgroup
 template <class SRT, typename V, int LOGT, int NT>
 constexpr size_t num_block_lds() {
-  return (size_t)((1 << LOGT) + NT) * (sizeof(typename SRT::Acc) + 4) + (size_t)NT * (16 + sizeof(V)) + 64 * 4;
+  return (size_t)((1 << LOGT) + NT) * (sizeof(typename SRT::Acc) + 4) + (size_t)NT * (16 + sizeof(V)) +
+         (size_t)(NT / kWave + 1) * 8 + 64 * 4;
 }
 
 template <class SRT, typename V, int LOGT, int NT, bool UNIT>
@@ -878,14 +1121,14 @@ __global__ void __launch_bounds__(NT) k_num_block(const int32_t* __restrict__ li
   constexpr int TC = T + NT;      // tail = one slot per thread keeps chunks uniform
   extern __shared__ __attribute__((aligned(16))) char smem[];
   Acc* vals = (Acc*)smem;                        // TC
-  int64_t* q_a0 = (int64_t*)(vals + TC);         // NT
-  V* q_bv = (V*)(q_a0 + NT);                     // NT
-  int32_t* keys = (int32_t*)(q_bv + NT);         // TC
-  int32_t* q_len = keys + TC;                    // NT
-  int32_t* q_b = q_len + NT;                     // NT
-  int* misc = q_b + NT;                          // [0] queue n, [1] overflow, [2] adderr, [8..] scan
-  LongQ<V> lq{q_a0, q_len, q_b, q_bv, &misc[0]};
+  int64_t* qb = (int64_t*)(vals + TC);           // NT   (Acc is 4 or 8 bytes and TC is even)
+  int64_t* off = qb + NT;                        // NT
+  int64_t* scr = off + NT;                       // NT/64 + 1
+  V* bvs = (V*)(scr + NT / kWave + 1);           // NT
+  int32_t* keys = (int32_t*)(bvs + NT);          // TC
+  int* misc = keys + TC;                         // [1] overflow, [2] adderr, [8..] int scan
   Table<Acc> t{keys, vals, T, TC};
+  const SegBuf<V> sb{qb, off, bvs, scr};
   const int64_t count = count_dev ? (int64_t)*count_dev : count_host;
   for (int64_t i = blockIdx.x; i < count; i += gridDim.x) {
     const Work wk = get_work<UNIT>(list, i, units, span, colptr, spl.log);
@@ -896,26 +1139,12 @@ __global__ void __launch_bounds__(NT) k_num_block(const int32_t* __restrict__ li
     if (threadIdx.x == 0) { misc[1] = 0; misc[2] = 0; }
     __syncthreads();
     int ovf = 0, aerr = 0;
-    for_each_multiply<NT, false, V>(
-        B.cp[wk.j], B.cp[wk.j + 1], nullptr, lq,
-        [&](int64_t b, int64_t& a0, int64_t& a1, V& bv) {
-          const int32_t k = B.ir[b];
-          if constexpr (UNIT) unit_bounds(A.cp, A.ir, spl, k, wk.s0, wk.s1, a0, a1);
-          else { a0 = A.cp[k]; a1 = A.cp[k + 1]; }
-          bv = load_val(B.val, b);
-        },
+    for_each_multiply<NT, false, kUnroll, V>(
+        B.cp[wk.j], B.cp[wk.j + 1], sb,
+        [&](int64_t b, int64_t& a0, int64_t& a1, V& bv) { num_seg<V, UNIT>(A, B, spl, spl.useg, wk, b, a0, a1, bv); },
         [&](int64_t q) { return NumItem<V>{A.ir[q], load_val(A.val, q)}; },
         [&](const NumItem<V>& it, V bv, int64_t q, int64_t b) {
-          const Acc x = SRT::mul(it.a, bv, q, b);
-          if (dense) {
-            const int32_t o = it.r - wk.lo;
-            const uint32_t bit = 1u << (o & 31);
-            const uint32_t old = atomicOr((uint32_t*)&keys[o >> 5], bit);
-            if (SRT::kAddIsError && (old & bit)) aerr = 1;
-            SRT::acc(&vals[o], x);
-          } else {
-            if (!hash_insert_num<SRT>(t, it.r, mono_home(it.r, wk.lo, mult), x, &aerr)) ovf = 1;
-          }
+          num_insert<SRT, V, UNIT>(t, dense, wk, mult, it, bv, q, b, ovf, aerr);
         });
     if (ovf) misc[1] = 1;
     if (aerr) misc[2] = 1;
@@ -949,6 +1178,149 @@ __global__ void __launch_bounds__(NT) k_num_block(const int32_t* __restrict__ li
     if (threadIdx.x == 0 && misc[2]) atomicOr(out.adderr, 1);
     __syncthreads();
   }
+}
+
+// ---- heavy numeric: one workgroup per item = up to kItemUnits consecutive units of one heavy column.
+// The item's unit descriptors are loaded once, and each unit's segments come from the precomputed
+// table (k_unit_segs), fetched one chunk ahead so that the fetch overlaps the current expansion.
+// Hash tables are sized per unit (power of two >= 2*cnt, >= NT) inside the T-slot allocation.
+struct HeavyItem {
+  int32_t h, u0, u1, pad;   // units [u0, u1) of heavy column h
+};
+
+template <class SRT, typename V, int LOGT, int NT>
+constexpr size_t num_heavy_lds() {
+  return num_block_lds<SRT, V, LOGT, NT>() + kItemUnits * sizeof(Unit);
+}
+
+template <class SRT, typename V, int LOGT, int NT>
+__global__ void __launch_bounds__(NT) k_num_heavy(const HeavyItem* __restrict__ items,
+                                                  const int32_t* __restrict__ hcols, const Unit* __restrict__ units,
+                                                  int32_t nsub, DevCsc<V> A, DevCsc<V> B,
+                                                  const int2* __restrict__ span, Split spl, NumOut<V> out) {
+  using Acc = typename SRT::Acc;
+  constexpr int T = 1 << LOGT;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  Acc* vals = (Acc*)smem;                        // T + NT
+  int64_t* qb = (int64_t*)(vals + T + NT);       // NT
+  int64_t* off = qb + NT;                        // NT
+  int64_t* scr = off + NT;                       // NT/64 + 1
+  V* bvs = (V*)(scr + NT / kWave + 1);           // NT
+  int32_t* keys = (int32_t*)(bvs + NT);          // T + NT
+  int* misc = keys + T + NT;                     // [1] overflow, [2] adderr, [8..] int scan (64 ints)
+  Unit* s_units = (Unit*)(misc + 64);            // kItemUnits
+  const SegBuf<V> sb{qb, off, bvs, scr};
+  STAMP_DECL
+  STAMP(0);
+  const HeavyItem item = items[blockIdx.x];
+  const int32_t j = hcols[item.h];
+  const int2 sp = span[j];
+  const int64_t bs = B.cp[j], nb = B.cp[j + 1] - bs;
+  const int nu = item.u1 - item.u0;
+  if ((int)threadIdx.x < nu) s_units[threadIdx.x] = units[(int64_t)item.h * nsub + item.u0 + threadIdx.x];
+  __syncthreads();
+  auto fetch = [&](int u, int64_t c, int64_t& a0, int64_t& a1, V& bv) {
+    const int64_t i = c + threadIdx.x;
+    a0 = a1 = 0;
+    bv = V(0);
+    if (u < nu && i < nb) {
+      const UnitSeg g = spl.useg[s_units[u].segbase + i];
+      a0 = g.a0;
+      a1 = g.a1;
+      bv = load_val(B.val, bs + i);
+    }
+  };
+  int64_t pa0, pa1;
+  V pbv;
+  fetch(0, 0, pa0, pa1, pbv);
+  STAMP(1);
+  for (int u = 0; u < nu; ++u) {
+    const Unit un = s_units[u];
+    Work wk;
+    wk.j = j;
+    wk.s0 = un.s0;
+    wk.s1 = un.s1;
+    wk.lo = (int32_t)max((int64_t)sp.x, (int64_t)un.s0 << spl.log);
+    wk.hi = (int32_t)min((int64_t)sp.y, ((int64_t)un.s1 << spl.log) - 1);
+    wk.ob = un.outoff;
+    wk.segbase = un.segbase;
+    const int64_t spn = (int64_t)wk.hi - wk.lo + 1;
+    const bool dense = spn <= T;
+    int Te = NT;
+    while (Te < T && Te < 2 * un.cnt) Te <<= 1;
+    const int TC = Te + NT;
+    const uint32_t mult = dense ? 0u : (uint32_t)(((uint64_t)Te << 32) / (uint64_t)spn);
+    Table<Acc> t{keys, vals, Te, TC};
+    if (dense) {
+      for (int s = threadIdx.x; s < T / 32; s += NT) keys[s] = 0;
+      for (int s = threadIdx.x; s < spn; s += NT) vals[s] = SRT::identity();
+    } else {
+      for (int s = threadIdx.x; s < TC; s += NT) { keys[s] = kEmpty; vals[s] = SRT::identity(); }
+    }
+    if (threadIdx.x == 0) { misc[1] = 0; misc[2] = 0; }
+    __syncthreads();
+    STAMP(2);
+    STAMP_COUNT(10, 1);
+    int ovf = 0, aerr = 0;
+    for (int64_t c = 0; c < nb; c += NT) {
+      const int64_t a0 = pa0, a1 = pa1;
+      const V bv = pbv;
+      if (c + NT < nb) fetch(u, c + NT, pa0, pa1, pbv);
+      else fetch(u + 1, 0, pa0, pa1, pbv);
+      const int64_t F = stage_segments<NT, false, V>(sb, a0, a1, bv);
+      STAMP(3);
+      STAMP_COUNT(11, 1);
+      STAMP_COUNT(12, F);
+      expand_staged<NT, kUnrollHeavy, V>(
+          sb, threadIdx.x, F, bs + c, (int)min<int64_t>(NT, nb - c), [&](int64_t q) { return NumItem<V>{A.ir[q], load_val(A.val, q)}; },
+          [&](const NumItem<V>& it, V bv2, int64_t q, int64_t b) {
+            num_insert<SRT, V, true>(t, dense, wk, mult, it, bv2, q, b, ovf, aerr);
+          });
+      __syncthreads();
+      STAMP(4);
+    }
+    if (ovf) misc[1] = 1;
+    if (aerr) misc[2] = 1;
+    __syncthreads();
+    STAMP(6);
+    const int64_t ob = wk.ob;
+    if (misc[1]) {
+      if (threadIdx.x == 0) out.ovf_list[atomicAdd(out.ovf_n, 1)] = (int32_t)((int64_t)item.h * nsub + item.u0 + u);
+    } else if (dense) {
+      constexpr int NWORD = T / 32;
+      static_assert(NWORD <= NT, "dense bitmap words must not exceed the block");
+      uint32_t wd = (threadIdx.x < NWORD) ? (uint32_t)keys[threadIdx.x] : 0u;
+      int tot;
+      int o = block_excl_scan<NT>(__popc(wd), misc + 8, &tot);
+      while (wd) {
+        const int bpos = __ffs(wd) - 1;
+        wd &= wd - 1;
+        const int rr = threadIdx.x * 32 + bpos;
+        out.row[ob + o] = wk.lo + rr;
+        out.val[ob + o] = SRT::out(vals[rr], A.val, B.val);
+        ++o;
+      }
+    } else {
+      STAMP(7);
+      compact_hash_homes<SRT, V, NT, T / NT + 1>(keys, vals, TC, Te, wk.lo, mult, (uint32_t*)qb, misc + 8, ob,
+                                                A.val, B.val, out.row, out.val);
+      STAMP(8);
+      STAMP_COUNT(13, 1);
+    }
+    if (threadIdx.x == 0 && misc[2]) atomicOr(out.adderr, 1);
+    __syncthreads();
+    STAMP(5);
+  }
+}
+
+// items of every heavy column: ceil(nunits / kItemUnits) consecutive unit groups
+__global__ void k_heavy_items(int H, const int32_t* __restrict__ nunits, const int64_t* __restrict__ itemoff,
+                              HeavyItem* __restrict__ items) {
+  const int h = blockIdx.x * blockDim.x + threadIdx.x;
+  if (h >= H) return;
+  const int nu = nunits[h];
+  int64_t o = itemoff[h];
+  for (int u = 0; u < nu; u += kItemUnits) items[o++] = HeavyItem{h, u, min(nu, u + kItemUnits), 0};
 }
 
 // ============================================================================ 7. windowed sweep
