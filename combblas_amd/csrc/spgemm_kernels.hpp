@@ -40,9 +40,9 @@ namespace {  // internal linkage: every translation unit instantiates its own ke
 constexpr int kWave = 64;
 constexpr int32_t kEmpty = -1;
 constexpr int kLong = 64;          // k_window: segment length handed to a whole wavefront
-constexpr int kUnroll = 4;         // independent gathers in flight per lane (numeric)
-constexpr int kUnrollSym = 8;      // same, symbolic (4-byte items)
-constexpr int kUnrollHeavy = 8;    // same, k_num_heavy (few multiplies per lane per chunk: all in flight)
+constexpr int kUnroll = 2;         // groups of kGroup multiplies in flight per lane (numeric)
+constexpr int kUnrollSym = 4;      // same, symbolic (4-byte items)
+constexpr int kUnrollHeavy = 2;    // same, k_num_heavy
 constexpr int64_t kHeavy = 4096;   // nnz(C(:,j)) above which a column is split into units
 constexpr int64_t kUnitCap = 4096; // max outputs of a multi-subwindow unit (T = 8192, load <= 0.5)
 constexpr int kSplitMin = 16;      // A columns at least this long get split-table rows
@@ -300,10 +300,11 @@ __global__ void __launch_bounds__(256) k_bin(int64_t n, const int64_t* __restric
 // ld(q) loads what an insert needs; ins(item, bv, q, b) inserts it.
 template <typename V>
 struct SegBuf {         // LDS, NT entries each (+ scan scratch for block mode)
-  int64_t* qb;          // a0 - off: the A index of flat multiply m in segment s is qb[s] + m
-  int64_t* off;         // exclusive prefix of segment lengths
+  int64_t* qb;          // segment start (A index)
+  int64_t* off;         // exclusive prefix of segment group counts
   V* bv;                // B value of the segment's nonzero
   int64_t* scratch;     // block mode: NT/64 + 1 entries
+  int32_t* len;         // segment length (multiplies)
 };
 
 __device__ __forceinline__ int64_t wave_incl_scan64(int64_t v) {
@@ -345,28 +346,35 @@ __device__ __forceinline__ int seg_search(const int64_t* off, int64_t m, int P) 
   return s;
 }
 
-// Stage one chunk of NT segments (this lane's a0, a1, bv) into LDS; returns the chunk's multiply
-// count.  The LDS arrays are valid on return (synchronised).
+// Stage one chunk of NT segments (this lane's a0, a1, bv) into LDS; returns the chunk's number of
+// GROUPS: a segment of len multiplies is cut into ceil(len/kGroup) groups of kGroup consecutive A
+// entries, and the groups (not the multiplies) are what lanes are dealt.  The LDS arrays are valid
+// on return (synchronised).
+constexpr int kGroup = 4;
 template <int NT, bool WAVE, typename V>
 __device__ __forceinline__ int64_t stage_segments(const SegBuf<V>& sb, int64_t a0, int64_t a1, V bv) {
   const int tid = WAVE ? lane_id() : (int)threadIdx.x;
   const int64_t len = a1 - a0;
+  const int64_t ng = (len + kGroup - 1) / kGroup;
   int64_t ex, F;
   if constexpr (WAVE) {
-    const int64_t inc = wave_incl_scan64(len);
+    const int64_t inc = wave_incl_scan64(ng);
     F = __shfl(inc, kWave - 1, kWave);
-    ex = inc - len;
+    ex = inc - ng;
   } else {
-    ex = block_excl_scan64<NT>(len, sb.scratch, &F);
+    ex = block_excl_scan64<NT>(ng, sb.scratch, &F);
   }
-  sb.qb[tid] = a0 - ex;
+  sb.qb[tid] = a0;
   sb.off[tid] = ex;
+  sb.len[tid] = (int32_t)len;
   sb.bv[tid] = bv;
   if constexpr (WAVE) wave_sync(); else __syncthreads();
   return F;
 }
 
-// Deal the F staged multiplies to the NT lanes (U independent gathers in flight per lane).
+// Deal the F staged groups to the NT lanes: lane t takes groups g = g0 + u*NT + t and finds the
+// group's segment by a binary search over the LDS prefix offsets (one search per kGroup multiplies),
+// then issues the group's kGroup gathers back to back (U*kGroup independent gathers per lane).
 // `base` is the B position of staged segment 0.  The caller synchronises before re-staging.
 template <int NT, int U, typename V, class LdF, class InsF>
 __device__ __forceinline__ void expand_staged(const SegBuf<V>& sb, int tid, int64_t F, int64_t base, int nseg,
@@ -374,23 +382,34 @@ __device__ __forceinline__ void expand_staged(const SegBuf<V>& sb, int tid, int6
   using Item = decltype(ld(int64_t(0)));
   int P = 1;
   while (P < nseg) P <<= 1;
-  for (int64_t m0 = 0; m0 < F; m0 += (int64_t)NT * U) {
-    Item it[U];
+  for (int64_t g0 = 0; g0 < F; g0 += (int64_t)NT * U) {
+    Item it[U][kGroup];
     int ss[U];
     int64_t qq[U];
+    int nv[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int64_t m = m0 + (int64_t)u * NT + tid;
-      if (m < F) {
-        ss[u] = seg_search<NT>(sb.off, m, P);
-        qq[u] = sb.qb[ss[u]] + m;
-        it[u] = ld(qq[u]);
+      const int64_t g = g0 + (int64_t)u * NT + tid;
+      nv[u] = 0;
+      if (g < F) {
+        const int sg = seg_search<NT>(sb.off, g, P);
+        const int64_t k0 = (g - sb.off[sg]) * kGroup;
+        ss[u] = sg;
+        qq[u] = sb.qb[sg] + k0;
+        nv[u] = (int)min<int64_t>(kGroup, sb.len[sg] - k0);
+#pragma unroll
+        for (int i = 0; i < kGroup; ++i)
+          if (i < nv[u]) it[u][i] = ld(qq[u] + i);
       }
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int64_t m = m0 + (int64_t)u * NT + tid;
-      if (m < F) ins(it[u], sb.bv[ss[u]], qq[u], base + ss[u]);
+      if (nv[u] > 0) {
+        const V bv = sb.bv[ss[u]];
+#pragma unroll
+        for (int i = 0; i < kGroup; ++i)
+          if (i < nv[u]) ins(it[u][i], bv, qq[u] + i, base + ss[u]);
+      }
     }
   }
 }
@@ -494,9 +513,10 @@ __global__ void __launch_bounds__(256) k_sym_wave(const int32_t* __restrict__ li
   __shared__ int32_t s_tab[4][T];
   __shared__ int64_t s_qb[4][kWave], s_off[4][kWave];
   __shared__ uint8_t s_bv[4][kWave];
+  __shared__ int32_t s_len[4][kWave];
   const int w = threadIdx.x / kWave, l = lane_id();
   int32_t* tab = s_tab[w];
-  const SegBuf<uint8_t> sb{s_qb[w], s_off[w], s_bv[w], nullptr};
+  const SegBuf<uint8_t> sb{s_qb[w], s_off[w], s_bv[w], nullptr, s_len[w]};
   const int64_t nwaves = (int64_t)gridDim.x * 4;
   for (int64_t i = blockIdx.x * 4 + w; i < count; i += nwaves) {
     const int32_t j = list[i];
@@ -544,7 +564,7 @@ __global__ void __launch_bounds__(256) k_sym_wave(const int32_t* __restrict__ li
 // block kernel: one column per workgroup; heavy columns also report nnz per subwindow
 template <int LOGT, int NT>
 constexpr size_t sym_block_lds() {
-  return (size_t)(1 << LOGT) * 4 + (size_t)NT * 17 + (size_t)(NT / kWave + 1) * 8 + (size_t)(kMaxSub + 2) * 4 + 64;
+  return (size_t)(1 << LOGT) * 4 + (size_t)NT * 21 + (size_t)(NT / kWave + 1) * 8 + (size_t)(kMaxSub + 2) * 4 + 64;
 }
 
 template <int LOGT, int NT>
@@ -561,8 +581,9 @@ __global__ void __launch_bounds__(NT) k_sym_block(const int32_t* __restrict__ li
   int32_t* tab = (int32_t*)(scr + NT / kWave + 1);// T
   int32_t* scnt = tab + T;                        // kMaxSub + 2
   int* misc = scnt + kMaxSub + 2;                 // [1] total, [2] heavy id
-  uint8_t* bvs = (uint8_t*)(misc + 8);            // NT
-  const SegBuf<uint8_t> sb{qb, off, bvs, scr};
+  int32_t* lens = misc + 8;                       // NT
+  uint8_t* bvs = (uint8_t*)(lens + NT);           // NT
+  const SegBuf<uint8_t> sb{qb, off, bvs, scr, lens};
   for (int64_t i = blockIdx.x; i < count; i += gridDim.x) {
     const int32_t j = list[i];
     const int2 sp = span[j];
@@ -1018,7 +1039,11 @@ __device__ __forceinline__ void num_insert(Table<typename SRT::Acc>& t, bool den
     if (SRT::kAddIsError && (old & bit)) aerr = 1;
     SRT::acc(&t.vals[o], x);
   } else {
+#ifdef CBG_FAKE_INSERT
+    t.keys[mono_home(it.r, wk.lo, mult)] = it.r;   // diagnostic timing only: no probing, no atomics
+#else
     if (!hash_insert_num<SRT>(t, it.r, mono_home(it.r, wk.lo, mult), x, &aerr)) ovf = 1;
+#endif
   }
 }
 
@@ -1054,9 +1079,10 @@ __global__ void __launch_bounds__(256) k_num_wave(const int32_t* __restrict__ li
   __shared__ Acc s_vals[4][TC];
   __shared__ int64_t s_qb[4][kWave], s_off[4][kWave];
   __shared__ V s_bv[4][kWave];
+  __shared__ int32_t s_len[4][kWave];
   const int w = threadIdx.x / kWave, l = lane_id();
   Table<Acc> t{s_keys[w], s_vals[w], T, TC};
-  const SegBuf<V> sb{s_qb[w], s_off[w], s_bv[w], nullptr};
+  const SegBuf<V> sb{s_qb[w], s_off[w], s_bv[w], nullptr, s_len[w]};
   const int64_t nwaves = (int64_t)gridDim.x * 4;
   for (int64_t i = blockIdx.x * 4 + w; i < count; i += nwaves) {
     const Work wk = get_work<UNIT>(list, i, units, span, colptr, spl.log);
@@ -1107,7 +1133,7 @@ __global__ void __launch_bounds__(256) k_num_wave(const int32_t* __restrict__ li
 // ---- block numeric: one item per workgroup
 template <class SRT, typename V, int LOGT, int NT>
 constexpr size_t num_block_lds() {
-  return (size_t)((1 << LOGT) + NT) * (sizeof(typename SRT::Acc) + 4) + (size_t)NT * (16 + sizeof(V)) +
+  return (size_t)((1 << LOGT) + NT) * (sizeof(typename SRT::Acc) + 4) + (size_t)NT * (20 + sizeof(V)) +
          (size_t)(NT / kWave + 1) * 8 + 64 * 4;
 }
 
@@ -1124,11 +1150,12 @@ __global__ void __launch_bounds__(NT) k_num_block(const int32_t* __restrict__ li
   int64_t* qb = (int64_t*)(vals + TC);           // NT   (Acc is 4 or 8 bytes and TC is even)
   int64_t* off = qb + NT;                        // NT
   int64_t* scr = off + NT;                       // NT/64 + 1
-  V* bvs = (V*)(scr + NT / kWave + 1);           // NT
+  int32_t* lens = (int32_t*)(scr + NT / kWave + 1); // NT
+  V* bvs = (V*)(lens + NT);                      // NT
   int32_t* keys = (int32_t*)(bvs + NT);          // TC
   int* misc = keys + TC;                         // [1] overflow, [2] adderr, [8..] int scan
   Table<Acc> t{keys, vals, T, TC};
-  const SegBuf<V> sb{qb, off, bvs, scr};
+  const SegBuf<V> sb{qb, off, bvs, scr, lens};
   const int64_t count = count_dev ? (int64_t)*count_dev : count_host;
   for (int64_t i = blockIdx.x; i < count; i += gridDim.x) {
     const Work wk = get_work<UNIT>(list, i, units, span, colptr, spl.log);
@@ -1205,11 +1232,12 @@ __global__ void __launch_bounds__(NT) k_num_heavy(const HeavyItem* __restrict__ 
   int64_t* qb = (int64_t*)(vals + T + NT);       // NT
   int64_t* off = qb + NT;                        // NT
   int64_t* scr = off + NT;                       // NT/64 + 1
-  V* bvs = (V*)(scr + NT / kWave + 1);           // NT
+  int32_t* lens = (int32_t*)(scr + NT / kWave + 1); // NT
+  V* bvs = (V*)(lens + NT);                      // NT
   int32_t* keys = (int32_t*)(bvs + NT);          // T + NT
   int* misc = keys + T + NT;                     // [1] overflow, [2] adderr, [8..] int scan (64 ints)
   Unit* s_units = (Unit*)(misc + 64);            // kItemUnits
-  const SegBuf<V> sb{qb, off, bvs, scr};
+  const SegBuf<V> sb{qb, off, bvs, scr, lens};
   STAMP_DECL
   STAMP(0);
   const HeavyItem item = items[blockIdx.x];
