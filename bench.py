@@ -1,21 +1,27 @@
 #!/usr/bin/env python3
-"""Benchmark: SpGEMM multiplies/s on R-MAT A*A (PlusTimes<double>), MI355X-native local hash SpGEMM.
+"""Benchmark: SpGEMM multiplies/s on R-MAT A*A (PlusTimes<double>) on MI355X.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--scale S] [--no-cpu]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
-One "step" = one full local SpGEMM C = A*B through the C ABI (column stats, binning, symbolic,
-scan, allocation of C, numeric with row-sorted output), inputs already resident in HBM.
+Workload (BASELINE.json configs): Graph500 Kronecker / R-MAT, edge factor 16, A*A over PlusTimes<double>,
+inputs generated on the host with a fixed seed and resident in HBM before the timed region.
+  N = 1: configs[1], scale 20, the local hash SpGEMM (cbg_spgemm_local) on one GPU.
+  N > 1: the distributed product on the mandated layout (combblas_amd/dist.py):
+         2 -> 1x1x2, 4 -> 2x2 SUMMA, 8 -> 2x2x2 (configs[2] at scale 22), RCCL over xGMI.
+         Default scale 20 + {2: 1, 4: 1, 8: 2}[N]: per-GPU work stays within ~1.5x of N = 1 ("weak").
+One step = one complete product (column statistics, binning, symbolic, scan, allocation of C, numeric
+with row-sorted output; for N > 1 also the stage broadcasts, partial merges and the fiber exchange).
+K steps are timed between a barrier + device synchronisation on both sides, max over ranks; value =
+all ranks' multiplies / that time.
 
-N = 1: the whole product on one GPU (BASELINE config 2: R-MAT scale-20, edge factor 16).
-N > 1 (torchrun, one rank per GPU): A is generated identically on every rank (deterministic seed),
-B's columns are split into N contiguous ranges of equal multiplies, and each rank computes its
-C(:, range) -- independent output columns, no data-path collective ("replicas of A").  Total work is
-fixed (strong scaling).  Timing: barrier + device sync around exactly K steps, max over ranks.
-
-Prints ONE JSON line on rank 0 (schema in the task contract) with `roofline` for the numeric phase and
-`cpu_baseline` = the oracle CPU restatement timed on a bounded sample of the same product.
+Rank 0 prints ONE JSON line.  N = 1 adds `roofline` for the dominant kernel (k_num_heavy: the
+heavy-column units, timed with HIP events on the library stream; algorithmic bytes per SURVEY §8d)
+and `cpu_baseline` (the oracle CPU restatement on a bounded sample of the same product).
 """
 import argparse
+import ctypes
+import glob
 import json
 import os
 import sys
@@ -26,8 +32,10 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 
+METRIC = "SpGEMM multiplies/sec, R-MAT s22 A·A at 1/2/4/8 MI355X + achieved HBM GB/s"
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 S_I, S_V, S_P = 4, 8, 8        # row-index, value, column-pointer bytes
+K_HEAVY = 4096                 # nnz(C(:,j)) above which a column is split into units (spgemm_kernels.hpp)
 
 
 def balg_bytes(mults, nnzc, nnzb, ncolb):
@@ -36,25 +44,34 @@ def balg_bytes(mults, nnzc, nnzb, ncolb):
             + 4 * (ncolb + 1) * S_P)
 
 
-def numeric_bytes(mults, nnzc, nnzb, ncolb):
-    """Algorithmic bytes of the numeric phase only (the dominant kernels): gather A (row,val) per
-    multiply, read B (row,val) + A colptr pair per B nonzero, write C (row,val), colptr."""
-    return mults * (S_I + S_V) + nnzb * (S_I + S_V + 2 * S_P) + nnzc * (S_I + S_V) + 2 * (ncolb + 1) * S_P
+def heavy_bytes(flop_col, nnz_c_col, nnz_b_col, heavy):
+    """SURVEY §8(d) numeric-phase algorithmic bytes of the heavy columns (what k_num_heavy processes):
+    gather A (row, val) per multiply, read B (row, val) + the A colptr pair per B nonzero, write C."""
+    return (int(flop_col[heavy].sum()) * (S_I + S_V) + int(nnz_b_col[heavy].sum()) * (S_I + S_V + 2 * S_P)
+            + int(nnz_c_col[heavy].sum()) * (S_I + S_V))
 
 
-def flop_split(cp, ir, nparts):
-    """Column ranges of equal multiplies (estimateFLOP per column, mtSpGEMM.h:1117-1135)."""
+def load_traffic(scale, edgefactor):
+    """HBM bytes per k_num_heavy launch from the newest committed rocprofv3 PMC summary for this
+    workload (profiles/*_pmc_heavy.json, written by tools/pmc_heavy.py), or (None, None)."""
+    best = None
+    for f in sorted(glob.glob(os.path.join(HERE, "profiles", "*_pmc_heavy.json"))):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if d.get("scale") == scale and d.get("edgefactor") == edgefactor:
+            best = (f, d)
+    if best is None:
+        return None, None
+    return best[1]["bytes_per_launch"], os.path.relpath(best[0], HERE)
+
+
+def col_flops(cp, ir):
+    """estimateFLOP per column of A*A (mtSpGEMM.h:1117-1135)."""
     nnz_col = np.diff(cp)
-    per_b = nnz_col[ir]                      # nnz(A(:,k)) for every B nonzero (B = A)
-    csum = np.concatenate([[0], np.cumsum(per_b)])
-    flop_col = csum[cp[1:]] - csum[cp[:-1]]
-    cum = np.cumsum(flop_col)
-    tot = cum[-1]
-    bounds = [0]
-    for r in range(1, nparts):
-        bounds.append(int(np.searchsorted(cum, tot * r / nparts)))
-    bounds.append(len(flop_col))
-    return bounds, flop_col
+    csum = np.concatenate([[0], np.cumsum(nnz_col[ir])])
+    return csum[cp[1:]] - csum[cp[:-1]]
 
 
 def cpu_baseline(cp, ir, val, n, flop_col, target_mults):
@@ -74,8 +91,154 @@ def cpu_baseline(cp, ir, val, n, flop_col, target_mults):
     dt = time.perf_counter() - t0
     assert rc == 0
     return {"value": mults / dt, "unit": "multiplies/s", "cores": threads, "kind": "port",
-            "sample": f"oracle/oracle.c (CPU restatement of LocalSpGEMMHash, OpenMP) on every {stride}-th "
-                      f"column of B ({len(cols)} columns, {mults} multiplies, {dt:.2f} s)"}
+            "sample": f"oracle/oracle.c (CPU restatement of LocalSpGEMMHash, OpenMP, {threads} threads) on "
+                      f"every {stride}-th column of B ({len(cols)} columns, {mults} multiplies, {dt:.2f} s)"}
+
+
+def workload(scale, edgefactor, parallelism):
+    return {"workload": f"R-MAT (Graph500 Kronecker a,b,c,d=.57,.19,.19,.05, scrambled ids, duplicates summed) "
+                        f"scale-{scale} edge factor {edgefactor} A*A PlusTimes<double>",
+            "scale": scale, "edgefactor": edgefactor, "parallelism": parallelism}
+
+
+# ------------------------------------------------------------------------------------------ N = 1
+def bench_local(args):
+    import combblas_amd as cb
+    from combblas_amd import _abi
+
+    n, cp, ir, val = cb.generate_rmat_host(args.scale, args.edgefactor, seed=args.seed)
+    flop_col = col_flops(cp, ir)
+    ctx = cb.Context(0)
+    A = cb.SpDCCols.from_csc(ctx, n, n, cp, ir, val)
+    va = A._view()
+    lib = ctx._lib
+    keep = {}
+
+    def step(keep_colptr=False):
+        res = _abi.CscResult()
+        m = ctypes.c_int64()
+        _abi.check(lib.cbg_spgemm_local(ctx._ptr, ctypes.byref(va), ctypes.byref(va), _abi.SR_PLUS_TIMES,
+                                        _abi.F64, _abi.SORTED_COLS, ctypes.byref(res), ctypes.byref(m)),
+                   "cbg_spgemm_local")
+        prof = ctx.last_profile()
+        if keep_colptr:   # structure of C, outside the timed region: which columns were heavy
+            ccp = np.zeros(int(res.ncol) + 1, np.int64)
+            _abi.check(lib.cbg_result_to_host(ctx._ptr, ctypes.byref(res), ccp.ctypes.data, None, None))
+            keep["cp"] = ccp
+        nnzc = int(res.nnz)
+        lib.cbg_result_free(ctx._ptr, ctypes.byref(res))
+        return int(m.value), nnzc, prof
+
+    for w in range(max(args.warmup, 1)):
+        step(keep_colptr=(w == 0))
+    ctx.synchronize()
+    t0 = time.perf_counter()
+    mults = nnzc = 0
+    profs = []
+    for _ in range(args.steps):
+        m, z, prof = step()
+        mults += m
+        nnzc += z
+        profs.append(prof)
+    ctx.synchronize()
+    elapsed = time.perf_counter() - t0
+
+    nnz_c_col = np.diff(keep["cp"])
+    heavy = nnz_c_col > K_HEAVY
+    mult_step, nnzc_step = mults / args.steps, nnzc / args.steps
+    nnzb = int(cp[-1])
+    hb = heavy_bytes(flop_col, nnz_c_col, np.diff(cp), heavy)
+    heavy_ms = float(np.mean([p["heavy_ms"] for p in profs]))
+    achieved = hb / (heavy_ms / 1e3) / 1e9
+    traffic, tsrc = load_traffic(args.scale, args.edgefactor)
+    cfg = workload(args.scale, args.edgefactor, "single GPU, local hash SpGEMM (BASELINE configs[1])")
+    cfg.update({"nnz_A": nnzb, "multiplies": int(mult_step), "nnz_C": int(nnzc_step)})
+    out = {
+        "metric": METRIC, "value": mults / elapsed, "unit": "multiplies/s", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": 1000.0 * elapsed / args.steps, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic", "config": cfg,
+        "effective_GBps": balg_bytes(mult_step, nnzc_step, nnzb, n) / (elapsed / args.steps) / 1e9,
+        "phases_ms": {k: round(float(np.mean([p[k] for p in profs])), 3)
+                      for k in ("flops_ms", "bin_ms", "symbolic_ms", "scan_ms", "numeric_ms", "heavy_ms",
+                                "total_ms")},
+        "roofline": {"bound": "hbm", "kernel": "k_num_heavy", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "traffic_source": tsrc, "algorithmic_bytes_per_launch": hb, "avg_launch_ms": heavy_ms,
+                     "heavy_columns": int(heavy.sum()), "heavy_multiplies": int(flop_col[heavy].sum()),
+                     "heavy_nnz_C": int(nnz_c_col[heavy].sum())},
+    }
+    if not args.no_cpu:
+        out["cpu_baseline"] = cpu_baseline(cp, ir, val, n, flop_col, args.cpu_mults)
+    print(json.dumps(out), flush=True)
+
+
+# ------------------------------------------------------------------------------------------ N > 1
+def bench_dist(args, world, rank, local_rank):
+    import torch
+    import torch.distributed as dist
+    import combblas_amd as cb
+    from combblas_amd import dist as cbd
+
+    # production: RCCL, one GPU per rank.  CBG_DIST_BACKEND=gloo rehearses the same schedule with ranks
+    # sharing the visible GPUs (blocks staged through the host), e.g. on a one-GPU box.
+    backend = os.environ.get("CBG_DIST_BACKEND", "nccl")
+    dev = local_rank % torch.cuda.device_count()
+    torch.cuda.set_device(dev)
+    if backend == "nccl":
+        dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+    else:
+        dist.init_process_group(backend)
+    L, q, _ = cbd.grid_for(world)
+    grid = cbd.CommGrid3D(L, q, q)
+    n, cp, ir, val = cb.generate_rmat_host(args.scale, args.edgefactor, seed=args.seed)
+    ctx = cb.Context(dev)
+    be = cbd.GpuBackend(ctx)
+    A = cbd.SpParMat3D.from_global_csc(grid, n, n, cp, ir, val, True, be)
+    B = cbd.SpParMat3D.from_global_csc(grid, n, n, cp, ir, val, False, be)
+    nnzb = int(cp[-1])
+    del cp, ir, val
+    SR = cb.PlusTimesSRing("f64")
+
+    def step():
+        st = {}
+        C = cbd.Mult_AnXBn_SUMMA3D(SR, A, B, st)
+        nz = C.block.nnz
+        del C
+        return st.get("multiplies", 0), nz
+
+    for _ in range(max(args.warmup, 1)):
+        step()
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    mults = nnzc = 0
+    for _ in range(args.steps):
+        m, z = step()
+        mults += m
+        nnzc += z
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], dtype=torch.float64, device=be.comm_device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    s = torch.tensor([mults, nnzc], dtype=torch.float64, device=be.comm_device)
+    dist.all_reduce(s)
+    elapsed, mults, nnzc = float(t.item()), float(s[0].item()), float(s[1].item())
+    if rank == 0:
+        cfg = workload(args.scale, args.edgefactor,
+                       f"{L}x{q}x{q} ({'3D split SUMMA' if L > 1 else '2D SUMMA'}), "
+                       f"{'RCCL' if backend == 'nccl' else backend}")
+        cfg.update({"nnz_A": nnzb, "multiplies": int(mults / args.steps), "nnz_C": int(nnzc / args.steps)})
+        out = {"metric": METRIC, "value": mults / elapsed, "unit": "multiplies/s", "n_gpus": world,
+               "steps": args.steps, "warmup": args.warmup, "ms_per_step": 1000.0 * elapsed / args.steps,
+               "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+               "data": "synthetic", "config": cfg,
+               "effective_GBps": balg_bytes(mults / args.steps, nnzc / args.steps, nnzb, n)
+               / (elapsed / args.steps) / 1e9}
+        print(json.dumps(out), flush=True)
+    dist.destroy_process_group()
 
 
 def main():
@@ -83,118 +246,21 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--scale", type=int, default=20)
+    ap.add_argument("--scale", type=int, default=0, help="R-MAT scale (default 20 + {1:0,2:1,4:1,8:2}[N])")
     ap.add_argument("--edgefactor", type=int, default=16)
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-mults", type=float, default=1.5e9, help="multiplies in the CPU baseline sample")
     args = ap.parse_args()
-
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch
-        import torch.distributed as dist
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl" if torch.cuda.is_available() else "gloo")
-
-    import combblas_amd as cb
-    from combblas_amd import _abi
-
-    n, cp, ir, val = cb.generate_rmat_host(args.scale, args.edgefactor, seed=args.seed)
-    bounds, flop_col = flop_split(cp, ir, world)
-    c0, c1 = bounds[rank], bounds[rank + 1]
-
-    ctx = cb.Context(local_rank if world > 1 else 0)
-    A = cb.SpDCCols.from_csc(ctx, n, n, cp, ir, val)
-    va = A._view()
-    vb = A._view()
-    # B = A(:, c0:c1): same device arrays, colptr offset (absolute positions stay valid)
-    vb.ncol = c1 - c0
-    vb.nzc = c1 - c0
-    vb.cp = (va.cp or 0) + 8 * c0
-    vb.nnz = int(cp[c1] - cp[c0])
-
-    import ctypes
-    lib = ctx._lib
-
-    def step():
-        res = _abi.CscResult()
-        m = ctypes.c_int64()
-        _abi.check(lib.cbg_spgemm_local(ctx._ptr, ctypes.byref(va), ctypes.byref(vb), _abi.SR_PLUS_TIMES,
-                                        _abi.F64, _abi.SORTED_COLS, ctypes.byref(res), ctypes.byref(m)),
-                   "cbg_spgemm_local")
-        prof = ctx.last_profile()
-        nnzc = int(res.nnz)
-        lib.cbg_result_free(ctx._ptr, ctypes.byref(res))
-        return int(m.value), nnzc, prof
-
-    def barrier():
-        ctx.synchronize()
-        if dist is not None:
-            dist.barrier()
-
-    for _ in range(args.warmup):
-        step()
-    barrier()
-    t0 = time.perf_counter()
-    mults = nnzc = 0
-    num_ms = []
-    tot_ms = []
-    for _ in range(args.steps):
-        m, z, prof = step()
-        mults += m
-        nnzc += z
-        num_ms.append(prof["numeric_ms"])
-        tot_ms.append(prof["total_ms"])
-    barrier()
-    elapsed = time.perf_counter() - t0
-
-    local = np.array([elapsed, mults, nnzc, np.mean(num_ms)], np.float64)
-    if dist is not None:
-        import torch
-        t = torch.tensor(local, dtype=torch.float64, device="cuda")
-        tmax = t.clone()
-        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-        tsum = t.clone()
-        dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
-        elapsed, mults, nnzc = float(tmax[0]), float(tsum[1]), float(tsum[2])
-        num_mean_ms = float(tmax[3])
+    if not args.scale:
+        args.scale = 20 + {1: 0, 2: 1, 4: 1, 8: 2}.get(world, 0)
+    if world == 1:
+        bench_local(args)
     else:
-        num_mean_ms = float(np.mean(num_ms))
-
-    if rank == 0:
-        ms_per_step = 1000.0 * elapsed / args.steps
-        mult_step = mults / args.steps
-        nnzc_step = nnzc / args.steps
-        value = mults / elapsed
-        nnzb = int(cp[-1])
-        b_alg = balg_bytes(mult_step, nnzc_step, nnzb, n)
-        nb = numeric_bytes(mult_step / world, nnzc_step / world, nnzb / world, n / world)
-        achieved = nb / (num_mean_ms / 1e3) / 1e9
-        out = {
-            "metric": "SpGEMM multiplies/sec, R-MAT s22 A·A at 1/2/4/8 MI355X + achieved HBM GB/s",
-            "value": value, "unit": "multiplies/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True,
-            "scaling": "strong", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
-            "config": {"workload": f"R-MAT (Graph500 Kronecker, clip-and-flip, scrambled) scale-{args.scale} "
-                                   f"edge factor {args.edgefactor} A*A PlusTimes<double>, local hash SpGEMM "
-                                   f"(BASELINE config 2)",
-                       "scale": args.scale, "edgefactor": args.edgefactor, "nnz_A": nnzb,
-                       "multiplies": int(mult_step), "nnz_C": int(nnzc_step),
-                       "parallelism": "single" if world == 1 else f"1D column split x{world}, A replicated"},
-            "effective_GBps": b_alg / (elapsed / args.steps) / 1e9,
-            "roofline": {"bound": "hbm", "kernel": "numeric phase (k_num_wave/k_num_block/k_window)",
-                         "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None},
-        }
-        if world == 1 and not args.no_cpu:
-            out["cpu_baseline"] = cpu_baseline(cp, ir, val, n, flop_col, args.cpu_mults)
-        print(json.dumps(out), flush=True)
-    if dist is not None:
-        dist.destroy_process_group()
+        bench_dist(args, world, rank, local_rank)
 
 
 if __name__ == "__main__":

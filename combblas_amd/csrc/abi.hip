@@ -94,9 +94,9 @@ cbg_status cbg_estimate(cbg_ctx* ctx, const cbg_dcsc_view* A, const cbg_dcsc_vie
 cbg_status cbg_result_to_host(cbg_ctx* ctx, const cbg_csc_result* C, int64_t* colptr, int32_t* row, void* val) {
   if (!ctx || !C) return CBG_EINVAL;
   HIPCHK(hipSetDevice(ctx->device));
-  if (colptr) HIPCHK(hipMemcpyAsync(colptr, C->colptr, sizeof(int64_t) * (C->ncol + 1), hipMemcpyDeviceToHost, ctx->stream));
-  if (row && C->nnz) HIPCHK(hipMemcpyAsync(row, C->row, sizeof(int32_t) * C->nnz, hipMemcpyDeviceToHost, ctx->stream));
-  if (val && C->nnz) HIPCHK(hipMemcpyAsync(val, C->val, dt_size(C->val_type) * C->nnz, hipMemcpyDeviceToHost, ctx->stream));
+  if (colptr) HIPCHK(hipMemcpyAsync(colptr, C->colptr, sizeof(int64_t) * (C->ncol + 1), hipMemcpyDefault, ctx->stream));
+  if (row && C->nnz) HIPCHK(hipMemcpyAsync(row, C->row, sizeof(int32_t) * C->nnz, hipMemcpyDefault, ctx->stream));
+  if (val && C->nnz) HIPCHK(hipMemcpyAsync(val, C->val, dt_size(C->val_type) * C->nnz, hipMemcpyDefault, ctx->stream));
   HIPCHK(hipStreamSynchronize(ctx->stream));
   return CBG_OK;
 }

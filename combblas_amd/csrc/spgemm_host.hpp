@@ -526,8 +526,10 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
     hipError_t e = launch_numeric_classes<SRT, V, false>(st, cn, list, nullptr, A, B, span, colptr, spl, oc);
     if (e == hipSuccess && H > 0) {
       NumOut<V> ou{own->ir.as<int32_t>(), own->val.as<V>(), adderr, uovf_n, ctx->uovf_list.as<int32_t>()};
+      HIPCHK(hipEventRecord(ctx->ev[6], st));
       e = launch_num_heavy<13, 1024, SRT, V>(st, nitems, ctx->items.as<HeavyItem>(), ctx->heavy_cols.as<int32_t>(),
                                              units, nsub, A, B, span, spl, ou);
+      HIPCHK(hipEventRecord(ctx->ev[7], st));
       // overflowed hash units -> single-subwindow (dense) units
       if (e == hipSuccess) {
         k_split_overflow_units<<<(int)grid_for(nunit_cap, 256, 1 << 20), 256, 0, st>>>(
@@ -559,6 +561,7 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
   (void)hipEventElapsedTime(&t, ctx->ev[3], ctx->ev[4]); pf.scan_ms = t;
   (void)hipEventElapsedTime(&t, ctx->ev[4], ctx->ev[5]); pf.numeric_ms = t;
   (void)hipEventElapsedTime(&t, ctx->ev[0], ctx->ev[5]); pf.total_ms = t;
+  if (H > 0) { (void)hipEventElapsedTime(&t, ctx->ev[6], ctx->ev[7]); pf.heavy_ms = t; }
   pf.bins[14] = herr[4];   // overflowed units (re-run dense per subwindow)
   pf.bins[15] = herr[3];   // overflowed columns (windowed fallback)
   C->nnz = nnzc;

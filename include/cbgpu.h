@@ -103,6 +103,7 @@ typedef struct cbg_ctx cbg_ctx;
 typedef struct {
   double flops_ms, bin_ms, symbolic_ms, scan_ms, numeric_ms, total_ms;
   int64_t multiplies, nnz_out, bins[16];
+  double heavy_ms;      /* k_num_heavy alone (heavy-column units), HIP events on the context stream */
 } cbg_profile;
 
 int32_t     cbg_abi_version(void);
@@ -129,7 +130,8 @@ cbg_status cbg_estimate(cbg_ctx* ctx, const cbg_dcsc_view* A, const cbg_dcsc_vie
 cbg_status cbg_merge(cbg_ctx* ctx, const cbg_csc_result* parts, int32_t nparts, cbg_semiring sr,
                      cbg_dtype val_type, uint32_t flags, cbg_csc_result* C);
 
-/* Copy a result to caller-owned host arrays (colptr ncol+1, row nnz, val nnz). */
+/* Copy a result to caller-owned arrays (colptr ncol+1, row nnz, val nnz), host or device memory
+ * (unified addressing; a device destination stays a device-to-device copy). */
 cbg_status cbg_result_to_host(cbg_ctx* ctx, const cbg_csc_result* C, int64_t* colptr, int32_t* row,
                               void* val);
 void       cbg_result_free(cbg_ctx* ctx, cbg_csc_result* C);

@@ -1,0 +1,134 @@
+"""TEST INFRASTRUCTURE for the distributed drivers (combblas_amd/dist.py).
+
+`ScipyBackend` is a CPU stand-in for the local multiply/merge so that the SUMMA / 3D schedules, the
+block distribution and the fiber exchange can be checked with gloo on CPU processes; it is never used
+by the product.  `run_dist_case` is the per-rank body shared by the CPU (gloo + scipy) and GPU
+(gloo + libcbgpu, ranks sharing cuda:0) tests: every rank builds the same global inputs, distributes
+them, multiplies, and checks its own output piece against the global product.
+"""
+import os
+import sys
+
+import numpy as np
+import scipy.sparse as sp
+import torch
+import torch.distributed as dist
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(HERE))
+sys.path.insert(0, HERE)
+
+from combblas_amd import dist as cbd  # noqa: E402
+from combblas_amd.dist import Block  # noqa: E402
+
+
+class ScipyBackend:
+    """PlusTimes only (the schedules are semiring-agnostic; semirings are covered by the GPU tests)."""
+
+    def __init__(self, val_dtype=torch.float64):
+        self.device = torch.device("cpu")
+        self.comm_device = torch.device("cpu")
+        self.val_dtype = val_dtype
+
+    @staticmethod
+    def _csc(b):
+        return sp.csc_matrix((b.val.numpy(), b.ir.numpy(), b.cp.numpy()), shape=(b.nrow, b.ncol))
+
+    @staticmethod
+    def _block(M, dtype):
+        M = sp.csc_matrix(M)
+        M.sum_duplicates()
+        M.sort_indices()
+        return Block(M.shape[0], M.shape[1], torch.as_tensor(M.indptr.astype(np.int64)),
+                     torch.as_tensor(M.indices.astype(np.int32)), torch.as_tensor(M.data.astype(dtype)))
+
+    def multiply(self, A, B, sr, stats=None):
+        P = self._csc(A) @ self._csc(B)
+        if stats is not None:
+            m = int(np.diff(A.cp.numpy())[B.ir.numpy()].sum()) if B.nnz else 0
+            stats["multiplies"] = stats.get("multiplies", 0) + m
+        return self._block(P, A.val.numpy().dtype)
+
+    def merge(self, parts, sr):
+        S = self._csc(parts[0])
+        for p in parts[1:]:
+            S = S + self._csc(p)
+        return self._block(S, parts[0].val.numpy().dtype)
+
+
+def random_csc(n, m, density, seed, dtype=np.float64, integer=True):
+    rng = np.random.default_rng(seed)
+    M = sp.random(n, m, density=density, format="csc", random_state=rng,
+                  data_rvs=(lambda k: rng.integers(1, 5, k).astype(dtype)) if integer else None)
+    M.sort_indices()
+    return M
+
+
+def run_dist_case(rank, world, port, backend_kind, cases, errq):
+    """Per-rank body: init gloo, build the mandated grid for `world`, run every case."""
+    try:
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        L, q, _ = cbd.grid_for(world)
+        grid = cbd.CommGrid3D(L, q, q)
+        if backend_kind == "scipy":
+            be = ScipyBackend()
+        else:
+            import combblas_amd as cb
+            ctx = cb.Context(0)
+            be = cbd.GpuBackend(ctx)
+        for (n, k, m, dA, dB, seed) in cases:
+            A = random_csc(n, k, dA, seed)
+            B = random_csc(k, m, dB, seed + 1)
+            Ad = cbd.SpParMat3D.from_global_csc(grid, n, k, A.indptr, A.indices, A.data, True, be)
+            Bd = cbd.SpParMat3D.from_global_csc(grid, k, m, B.indptr, B.indices, B.data, False, be)
+            stats = {}
+            C = cbd.Mult_AnXBn_SUMMA3D(cb_sr(backend_kind), Ad, Bd, stats)
+            R = (A @ B).tocsc()
+            R.sort_indices()
+            (r0, r1), (c0, c1) = C.local_range()
+            Rl = R[r0:r1, c0:c1].tocsc()
+            Rl.sort_indices()
+            blk = C.block
+            cp, ir, val = blk.cp.cpu().numpy(), blk.ir.cpu().numpy(), blk.val.cpu().numpy()
+            assert (blk.nrow, blk.ncol) == (r1 - r0, c1 - c0), (blk.nrow, blk.ncol, r0, r1, c0, c1)
+            assert np.array_equal(cp, Rl.indptr), f"rank {rank}: colptr differs"
+            assert np.array_equal(ir, Rl.indices), f"rank {rank}: rows differ"
+            assert np.array_equal(val, Rl.data), f"rank {rank}: values differ"   # integer-valued: exact
+            # the layer multiplies add up to the product's multiplies
+            t = torch.tensor([stats.get("multiplies", 0)], dtype=torch.int64)
+            dist.all_reduce(t)
+            want = int(np.diff(A.indptr)[B.indices].sum())
+            assert int(t.item()) == want, (int(t.item()), want)
+            assert C.getnnz() == R.nnz
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:  # report to the parent, which fails the test
+        import traceback
+        errq.put(f"rank {rank}: {e!r}\n{traceback.format_exc()}")
+        raise
+
+
+def cb_sr(kind):
+    import combblas_amd as cb
+    return cb.PlusTimesSRing("f64")
+
+
+def spawn_case(world, backend_kind, cases, port):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    errq = ctx.SimpleQueue()
+    procs = [ctx.Process(target=run_dist_case, args=(r, world, port, backend_kind, cases, errq)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=300)
+    errs = []
+    while not errq.empty():
+        errs.append(errq.get())
+    codes = [p.exitcode for p in procs]
+    for p in procs:
+        if p.is_alive():
+            p.kill()
+    assert not errs and all(c == 0 for c in codes), "\n".join(errs) + f"\nexit codes {codes}"

@@ -1,0 +1,17 @@
+"""Distributed drivers on CPU: gloo process groups with a scipy local multiply (TEST INFRASTRUCTURE).
+
+Checks the mandated layouts end to end: 1x1x2 (2 ranks: fiber exchange, no broadcast),
+2x2 SUMMA (4 ranks: row/column broadcasts, 2 stages, merge), 2x2x2 (8 ranks: both), on square and
+rectangular products with empty blocks; every rank checks its output piece exactly against the global
+product and the multiplies add up to estimateFLOP of the whole product.
+"""
+import pytest
+
+from dist_support import spawn_case
+
+CASES = [(60, 50, 40, 0.08, 0.1, 3), (33, 17, 29, 0.2, 0.15, 5), (7, 5, 9, 0.3, 0.3, 9), (5, 64, 6, 0.01, 0.01, 11)]
+
+
+@pytest.mark.parametrize("world,port", [(2, 29611), (4, 29612), (8, 29613)])
+def test_summa_layouts_gloo_cpu(world, port):
+    spawn_case(world, "scipy", CASES, port)

@@ -1,0 +1,15 @@
+"""Distributed drivers with the real local kernel: gloo process groups whose ranks all share cuda:0,
+each running libcbgpu for its local multiplies and merges (the production path uses RCCL, one GPU per
+rank; the schedules are identical).  Checks every rank's output piece exactly."""
+import pytest
+
+from dist_support import spawn_case
+
+pytestmark = pytest.mark.gpu
+
+CASES = [(300, 280, 260, 0.03, 0.03, 21), (33, 17, 29, 0.2, 0.15, 5), (5, 64, 6, 0.01, 0.01, 11)]
+
+
+@pytest.mark.parametrize("world,port", [(2, 29621), (4, 29622), (8, 29623)])
+def test_summa_layouts_gloo_gpu(world, port):
+    spawn_case(world, "gpu", CASES, port)
