@@ -1,0 +1,199 @@
+/*
+ * combblas_gpu.h -- C++ drop-in for the reference's local SpGEMM plugin point, over the C ABI
+ * (include/cbgpu.h, libcbgpu.so).  Include it after CombBLAS/CombBLAS.h; it adds
+ *
+ *   combblas::gpu::LocalSpGEMMHash<SR, NTO>(A, B, clearA, clearB, sort)   mtSpGEMM.h:465-470
+ *   combblas::gpu::LocalHybridSpGEMM<SR, NTO>(A, B, clearA, clearB, aux)  mtSpGEMM.h:212-217
+ *   combblas::gpu::LocalSpGEMM<SR, NTO>(A, B, clearA, clearB)             mtSpGEMM.h:73-78
+ *   combblas::gpu::MultiwayMerge<SR>(lists, mdim, ndim, delarrs)          MultiwayMerge.h:411-412
+ *   combblas::gpu::EstimateLocalFLOP<SR>(A, B)                             mtSpGEMM.h:667-694
+ *
+ * with the reference's signatures and conventions: A, B are SpDCCols<IT, NT> (their DCSC arrays are
+ * handed to the device as they are, GetArrays order cp, jc, ir, numx); the product comes back as a
+ * column-sorted SpTuples<IT, NTO>* owned by the caller; clearA / clearB delete the inputs after the
+ * call (mtSpGEMM.h:644-647); an empty operand gives an empty SpTuples (mtSpGEMM.h:478-481).
+ * A semiring without a device functor (anything but the six policies of Semirings.h mapped below)
+ * runs the reference's own CPU template.  Device/ABI errors throw std::runtime_error; a dimension
+ * mismatch throws too (the MPI drivers abort with DIMMISMATCH 3002 there).
+ *
+ * Not part of libcbgpu: a maintainer adds this header on the reference side.
+ */
+#ifndef COMBBLAS_GPU_H
+#define COMBBLAS_GPU_H
+
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+#include <tuple>
+#include <type_traits>
+#include <vector>
+
+#include "cbgpu.h"
+
+namespace combblas {
+namespace gpu {
+
+// ---------------------------------------------------------------- semiring / dtype mapping
+template <class SR> struct DeviceSemiring { static constexpr bool ok = false; };
+template <class T1, class T2> struct DeviceSemiring<PlusTimesSRing<T1, T2>> {
+  static constexpr bool ok = true; static constexpr cbg_semiring code = CBG_SR_PLUS_TIMES; };
+template <class T1, class T2> struct DeviceSemiring<MinPlusSRing<T1, T2>> {
+  static constexpr bool ok = true; static constexpr cbg_semiring code = CBG_SR_MIN_PLUS; };
+template <class T1, class T2, class O> struct DeviceSemiring<Select2ndSRing<T1, T2, O>> {
+  static constexpr bool ok = true; static constexpr cbg_semiring code = CBG_SR_SELECT2ND; };
+template <class T1, class T2> struct DeviceSemiring<SelectMaxSRing<T1, T2>> {
+  static constexpr bool ok = true;
+  static constexpr cbg_semiring code = std::is_same<T1, bool>::value ? CBG_SR_SELECT_MAX_BOOL : CBG_SR_SELECT_MAX; };
+template <class O> struct DeviceSemiring<BoolCopy1stSRing<O>> {
+  static constexpr bool ok = true; static constexpr cbg_semiring code = CBG_SR_BOOL_COPY1ST; };
+template <class O> struct DeviceSemiring<BoolCopy2ndSRing<O>> {
+  static constexpr bool ok = true; static constexpr cbg_semiring code = CBG_SR_BOOL_COPY2ND; };
+
+template <class T> struct DeviceType { static constexpr bool ok = false; };
+template <> struct DeviceType<double> { static constexpr bool ok = true; static constexpr cbg_dtype code = CBG_F64; };
+template <> struct DeviceType<float> { static constexpr bool ok = true; static constexpr cbg_dtype code = CBG_F32; };
+template <> struct DeviceType<int64_t> { static constexpr bool ok = true; static constexpr cbg_dtype code = CBG_I64; };
+template <> struct DeviceType<int32_t> { static constexpr bool ok = true; static constexpr cbg_dtype code = CBG_I32; };
+template <> struct DeviceType<bool> { static constexpr bool ok = true; static constexpr cbg_dtype code = CBG_BOOL; };
+
+inline void check(cbg_status s, const char* where) {
+  if (s != CBG_OK) throw std::runtime_error(std::string(where) + ": " + cbg_strerror(s));
+}
+
+// one context per process/host thread, on the device the caller selected (default 0)
+inline cbg_ctx* context(int device = -1) {
+  static thread_local cbg_ctx* ctx = nullptr;
+  static thread_local int dev = 0;
+  if (device >= 0 && ctx && device != dev) { cbg_destroy(ctx); ctx = nullptr; }
+  if (!ctx) {
+    dev = device >= 0 ? device : 0;
+    check(cbg_init(dev, &ctx), "cbg_init");
+  }
+  return ctx;
+}
+
+// borrowed view of an SpDCCols (the DCSC arrays as GetArrays hands them out, SpDCCols.cpp:817-839)
+template <class IT, class NT>
+cbg_dcsc_view view_of(const SpDCCols<IT, NT>& M) {
+  static_assert(sizeof(IT) == 4 || sizeof(IT) == 8, "IT must be a 32- or 64-bit integer");
+  cbg_dcsc_view v{};
+  v.nrow = M.getnrow(); v.ncol = M.getncol(); v.nnz = M.getnnz(); v.nzc = M.getnzc();
+  Arr<IT, NT> arr = M.GetArrays();
+  v.cp = arr.indarrs[0].addr; v.jc = arr.indarrs[1].addr; v.ir = arr.indarrs[2].addr;
+  if (v.jc == nullptr) v.nzc = 0;              // empty matrix: no DCSC arrays at all
+  v.idx_bytes = (int32_t)sizeof(IT); v.ptr_bytes = (int32_t)sizeof(IT);
+  v.val = arr.numarrs[0].addr; v.val_type = DeviceType<NT>::code; v.on_device = 0;
+  return v;
+}
+
+// device CSC result -> column-sorted SpTuples (new[] tuples, isOpNew = false)
+template <class IT, class NTO>
+SpTuples<IT, NTO>* to_tuples(cbg_ctx* ctx, cbg_csc_result& C) {
+  std::vector<int64_t> cp(C.ncol + 1);
+  std::vector<int32_t> row(C.nnz > 0 ? C.nnz : 1);
+  std::vector<NTO> val(C.nnz > 0 ? C.nnz : 1);
+  const int64_t nrow = C.nrow, ncol = C.ncol;
+  cbg_status s = cbg_result_to_host(ctx, &C, cp.data(), row.data(), C.val ? (void*)val.data() : nullptr);
+  cbg_result_free(ctx, &C);   // clears C
+  check(s, "cbg_result_to_host");
+  const int64_t nnz = cp[ncol];
+  std::tuple<IT, IT, NTO>* t = new std::tuple<IT, IT, NTO>[nnz > 0 ? nnz : 1];
+  for (int64_t j = 0; j < ncol; ++j)
+    for (int64_t p = cp[j]; p < cp[j + 1]; ++p) t[p] = std::make_tuple((IT)row[p], (IT)j, val[p]);
+  return new SpTuples<IT, NTO>(nnz, (IT)nrow, (IT)ncol, t, /*sorted=*/true, /*isOpNew=*/false);
+}
+
+// ------------------------------------------------------------------------- entry points
+template <class SR, class NTO, class IT, class NT1, class NT2>
+SpTuples<IT, NTO>* LocalSpGEMMHash(const SpDCCols<IT, NT1>& A, const SpDCCols<IT, NT2>& B, bool clearA,
+                                   bool clearB, bool sort = true) {
+  // the device computes in NTO: operands must carry NTO values, or be bool patterns
+  constexpr bool dev = DeviceSemiring<SR>::ok && DeviceType<NTO>::ok &&
+                       (std::is_same<NT1, NTO>::value || std::is_same<NT1, bool>::value) &&
+                       (std::is_same<NT2, NTO>::value || std::is_same<NT2, bool>::value);
+  if constexpr (!dev) {
+    return combblas::LocalSpGEMMHash<SR, NTO>(A, B, clearA, clearB, sort);   // no device functor
+  } else {
+    if (A.getncol() != B.getnrow()) throw std::runtime_error("LocalSpGEMMHash: DIMMISMATCH (3002)");
+    cbg_ctx* ctx = context();
+    cbg_dcsc_view va = view_of(A), vb = view_of(B);
+    cbg_csc_result C{};
+    int64_t mults = 0;
+    check(cbg_spgemm_local(ctx, &va, &vb, DeviceSemiring<SR>::code, DeviceType<NTO>::code,
+                           sort ? CBG_SORTED_COLS : 0u, &C, &mults), "cbg_spgemm_local");
+    SpTuples<IT, NTO>* out = to_tuples<IT, NTO>(ctx, C);
+    if (clearA) delete const_cast<SpDCCols<IT, NT1>*>(&A);
+    if (clearB) delete const_cast<SpDCCols<IT, NT2>*>(&B);
+    return out;
+  }
+}
+
+template <class SR, class NTO, class IT, class NT1, class NT2>
+SpTuples<IT, NTO>* LocalHybridSpGEMM(const SpDCCols<IT, NT1>& A, const SpDCCols<IT, NT2>& B, bool clearA,
+                                     bool clearB, IT* aux = nullptr) {
+  (void)aux;   // heap/hash switch is a CPU heuristic; the device product is always sorted
+  return LocalSpGEMMHash<SR, NTO>(A, B, clearA, clearB, true);
+}
+
+template <class SR, class NTO, class IT, class NT1, class NT2>
+SpTuples<IT, NTO>* LocalSpGEMM(const SpDCCols<IT, NT1>& A, const SpDCCols<IT, NT2>& B, bool clearA, bool clearB) {
+  return LocalSpGEMMHash<SR, NTO>(A, B, clearA, clearB, true);
+}
+
+template <class SR, class IT, class NT1, class NT2>
+int64_t EstimateLocalFLOP(const SpDCCols<IT, NT1>& A, const SpDCCols<IT, NT2>& B) {
+  cbg_dcsc_view va = view_of(A), vb = view_of(B);
+  int64_t mults = 0, nnzc = 0;
+  check(cbg_estimate(context(), &va, &vb, &mults, &nnzc), "cbg_estimate");
+  return mults;
+}
+
+// MultiwayMerge: column-sorted partial products of one shape -> one SpTuples (duplicates: SR::add)
+template <class SR, class IT, class NT>
+SpTuples<IT, NT>* MultiwayMerge(std::vector<SpTuples<IT, NT>*>& lists, IT mdim = 0, IT ndim = 0,
+                                bool delarrs = false) {
+  if constexpr (!(DeviceSemiring<SR>::ok && DeviceType<NT>::ok)) {
+    return combblas::MultiwayMerge<SR>(lists, mdim, ndim, delarrs);
+  } else {
+    if (lists.empty()) return new SpTuples<IT, NT>(0, mdim, ndim);
+    cbg_ctx* ctx = context();
+    std::vector<cbg_csc_result> parts(lists.size());
+    std::vector<cbg_dcsc_view> views(lists.size());
+    std::vector<std::vector<int64_t>> cps(lists.size());
+    std::vector<std::vector<int32_t>> rows(lists.size());
+    std::vector<std::vector<NT>> vals(lists.size());
+    for (size_t l = 0; l < lists.size(); ++l) {   // SpTuples -> host CSC -> device (cbg_upload)
+      SpTuples<IT, NT>& T = *lists[l];
+      const IT m = T.getnrow(), n = T.getncol();
+      if ((mdim && m != mdim) || (ndim && n != ndim)) throw std::runtime_error("MultiwayMerge: dimension mismatch");
+      T.SortColBased();
+      cps[l].assign(n + 1, 0);
+      rows[l].resize(T.getnnz() > 0 ? T.getnnz() : 1);
+      vals[l].resize(T.getnnz() > 0 ? T.getnnz() : 1);
+      for (int64_t k = 0; k < T.getnnz(); ++k) {
+        ++cps[l][T.colindex(k) + 1];
+        rows[l][k] = (int32_t)T.rowindex(k);
+        vals[l][k] = T.numvalue(k);
+      }
+      for (IT j = 0; j < n; ++j) cps[l][j + 1] += cps[l][j];
+      cbg_dcsc_view v{};
+      v.nrow = m; v.ncol = n; v.nnz = T.getnnz(); v.nzc = n;
+      v.cp = cps[l].data(); v.ir = rows[l].data(); v.idx_bytes = 4; v.ptr_bytes = 8;
+      v.val = vals[l].data(); v.val_type = DeviceType<NT>::code; v.on_device = 0;
+      check(cbg_upload(ctx, &v, &parts[l]), "cbg_upload");
+    }
+    cbg_csc_result C{};
+    cbg_status s = cbg_merge(ctx, parts.data(), (int32_t)parts.size(), DeviceSemiring<SR>::code,
+                             DeviceType<NT>::code, CBG_SORTED_COLS, &C);
+    for (auto& p : parts) cbg_result_free(ctx, &p);
+    check(s, "cbg_merge");
+    if (delarrs)
+      for (auto* T : lists) delete T;
+    return to_tuples<IT, NT>(ctx, C);
+  }
+}
+
+}  // namespace gpu
+}  // namespace combblas
+
+#endif  // COMBBLAS_GPU_H

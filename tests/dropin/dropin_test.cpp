@@ -1,0 +1,112 @@
+// tests/dropin/dropin_test.cpp -- TEST INFRASTRUCTURE: the C++ drop-in (include/combblas_gpu.h)
+// against the reference's own types and kernels, in one process.
+//
+// Builds SpDCCols<int64_t, T> operands through the reference's SpTuples -> SpDCCols path, runs
+// combblas::gpu::LocalSpGEMMHash (libcbgpu) and the reference's combblas::LocalSpGEMMHash (CPU), and
+// compares the column-sorted products entry by entry (the reference output is re-sorted with
+// SortColBased: its integerSort mis-sorts power-of-two rows).  Also MultiwayMerge and a
+// semiring without a device functor (must take the reference CPU path).
+//   usage: dropin_test [--expect-no-gpu]
+// Exit 0 = all equal (or, with --expect-no-gpu, the device path threw a device error).
+#include <mpi.h>
+#include <cstdio>
+#include <cstdlib>
+#include <random>
+#include <tuple>
+#include <vector>
+#include "CombBLAS/CombBLAS.h"
+#include "combblas_gpu.h"
+using namespace combblas;
+
+typedef int64_t I;
+
+template <class T>
+SpDCCols<I, T>* random_dccols(I m, I n, double density, unsigned seed) {
+  std::mt19937_64 g(seed);
+  std::uniform_real_distribution<double> u(0.0, 1.0);
+  std::vector<std::tuple<I, I, T>> tv;
+  for (I j = 0; j < n; ++j)
+    for (I i = 0; i < m; ++i)
+      if (u(g) < density) tv.emplace_back(i, j, (T)(1 + (g() % 9)));
+  std::tuple<I, I, T>* t = new std::tuple<I, I, T>[tv.size()];
+  for (size_t k = 0; k < tv.size(); ++k) t[k] = tv[k];
+  SpTuples<I, T> tup((int64_t)tv.size(), m, n, t, true);
+  return new SpDCCols<I, T>(tup, false);
+}
+
+template <class T>
+bool same(SpTuples<I, T>* a, SpTuples<I, T>* b, const char* what) {
+  a->SortColBased();
+  b->SortColBased();
+  if (a->getnnz() != b->getnnz()) { printf("%s: nnz %lld vs %lld\n", what, (long long)a->getnnz(), (long long)b->getnnz()); return false; }
+  for (I k = 0; k < a->getnnz(); ++k)
+    if (a->rowindex(k) != b->rowindex(k) || a->colindex(k) != b->colindex(k) || a->numvalue(k) != b->numvalue(k)) {
+      printf("%s: entry %lld differs\n", what, (long long)k);
+      return false;
+    }
+  printf("%s: %lld entries equal\n", what, (long long)a->getnnz());
+  return true;
+}
+
+template <class T1, class T2>
+struct MaxTimesSR {   // no device functor: must run the reference CPU template
+  typedef typename promote_trait<T1, T2>::T_promote T_promote;
+  static T_promote id() { return 0; }
+  static bool returnedSAID() { return false; }
+  static MPI_Op mpi_op() { return MPI_MAX; }
+  static T_promote add(const T_promote& a, const T_promote& b) { return a > b ? a : b; }
+  static T_promote multiply(const T1& a, const T2& b) { return (T_promote)a * (T_promote)b; }
+};
+
+int main(int argc, char** argv) {
+  MPI_Init(&argc, &argv);
+  const bool expect_no_gpu = argc > 1 && std::string(argv[1]) == "--expect-no-gpu";
+  int rc = 0;
+  {
+    auto* A = random_dccols<double>(300, 250, 0.05, 1);
+    auto* B = random_dccols<double>(250, 200, 0.05, 2);
+    typedef PlusTimesSRing<double, double> PT;
+    SpTuples<I, double>* ref = LocalSpGEMMHash<PT, double>(*A, *B, false, false, true);
+    SpTuples<I, double>* dev = nullptr;
+    try {
+      dev = gpu::LocalSpGEMMHash<PT, double>(*A, *B, false, false, true);
+    } catch (std::exception& e) {
+      printf("device path: %s\n", e.what());
+      MPI_Finalize();
+      return expect_no_gpu ? 0 : 2;
+    }
+    if (expect_no_gpu) { printf("expected no GPU but the device path ran\n"); rc = 3; }
+    if (!same(dev, ref, "PlusTimes<double>")) rc = 1;
+
+    auto* Ai = random_dccols<int64_t>(120, 90, 0.1, 3);
+    auto* Bi = random_dccols<int64_t>(90, 110, 0.1, 4);
+    typedef MinPlusSRing<int64_t, int64_t> MP;
+    SpTuples<I, int64_t>* ri = LocalSpGEMMHash<MP, int64_t>(*Ai, *Bi, false, false, true);
+    SpTuples<I, int64_t>* di = gpu::LocalSpGEMMHash<MP, int64_t>(*Ai, *Bi, false, false, true);
+    if (!same(di, ri, "MinPlus<int64>")) rc = 1;
+
+    typedef MaxTimesSR<int64_t, int64_t> MT;   // CPU fallback inside the drop-in
+    SpTuples<I, int64_t>* rc1 = LocalSpGEMMHash<MT, int64_t>(*Ai, *Bi, false, false, true);
+    SpTuples<I, int64_t>* dc1 = gpu::LocalSpGEMMHash<MT, int64_t>(*Ai, *Bi, false, false, true);
+    if (!same(dc1, rc1, "custom semiring (CPU template)")) rc = 1;
+
+    // MultiwayMerge of two products of the same shape
+    std::vector<SpTuples<I, double>*> l1 = {new SpTuples<I, double>(*ref), new SpTuples<I, double>(*dev)};
+    std::vector<SpTuples<I, double>*> l2 = {new SpTuples<I, double>(*ref), new SpTuples<I, double>(*dev)};
+    SpTuples<I, double>* mr = MultiwayMerge<PT>(l1, (I)300, (I)200, true);
+    SpTuples<I, double>* md = gpu::MultiwayMerge<PT>(l2, (I)300, (I)200, true);
+    if (!same(md, mr, "MultiwayMerge")) rc = 1;
+
+    const int64_t f = gpu::EstimateLocalFLOP<PT>(*A, *B);
+    int64_t fr = 0;
+    { Arr<I, double> a = B->GetArrays(); (void)a; }
+    fr = EstimateLocalFLOP<PT>(*A, *B, false, false);
+    printf("EstimateLocalFLOP device %lld reference %lld\n", (long long)f, (long long)fr);
+    if (f != fr) rc = 1;
+    delete ref; delete dev; delete ri; delete di; delete rc1; delete dc1; delete mr; delete md;
+    delete A; delete B; delete Ai; delete Bi;
+  }
+  MPI_Finalize();
+  printf(rc == 0 ? "DROPIN OK\n" : "DROPIN FAILED\n");
+  return rc;
+}

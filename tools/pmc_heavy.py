@@ -1,0 +1,68 @@
+#!/usr/bin/env python3
+"""HBM traffic of k_num_heavy from rocprofv3 PMC passes -> profiles/<tag>_pmc_heavy.json.
+
+Run on the GPU box (each counter group is its own rocprofv3 run, MI355X_MICROARCH.md §rocprofv3):
+    python tools/pmc_heavy.py run <tag> [scale]      # two PMC passes over bench.py + summary
+FETCH_SIZE / WRITE_SIZE are in KiB per dispatch (TCC EA requests).  The guide's gfx950 correction
+(FETCH_SIZE reads 1/2 of a 16-B-per-lane coalesced stream) is calibrated for wide streaming loads
+only; k_num_heavy's loads are 4/8-B gathers plus 16-B segment reads, so the JSON carries the raw
+counter sum as `bytes_per_launch` and the doubled-fetch figure as an upper bound beside it.
+"""
+import csv
+import glob
+import json
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+
+
+def per_dispatch(path, kernel_substr):
+    vals = {}
+    for f in glob.glob(os.path.join(path, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            if kernel_substr in r["Kernel_Name"]:
+                key = (r["Dispatch_Id"], r["Counter_Name"])
+                vals[key] = vals.get(key, 0.0) + float(r["Counter_Value"])
+    out = {}
+    for (d, c), v in vals.items():
+        out.setdefault(c, []).append(v)
+    return out
+
+
+def run(tag, scale):
+    out = os.path.join(REPO, "gpurun_out", tag)
+    os.makedirs(out, exist_ok=True)
+    env = dict(os.environ, TMPDIR="/tmp")
+    for i, ctr in enumerate(("FETCH_SIZE", "WRITE_SIZE")):
+        cmd = ["timeout", "-s", "KILL", "240", "rocprofv3", "--pmc", ctr, "--output-format", "csv",
+               "-d", os.path.join(out, f"pmc{i}"), "-o", "run", "--", sys.executable, os.path.join(REPO, "bench.py"),
+               "--steps", "1", "--warmup", "1", "--no-cpu", "--scale", str(scale)]
+        r = subprocess.run(cmd, env=env, cwd=REPO, stdout=open(os.path.join(out, f"pmc{i}.log"), "w"),
+                           stderr=subprocess.STDOUT)
+        print(f"pass {ctr}: rc={r.returncode}", flush=True)
+        if r.returncode != 0:
+            sys.exit(r.returncode)
+    f = per_dispatch(os.path.join(out, "pmc0"), "k_num_heavy").get("FETCH_SIZE", [])
+    w = per_dispatch(os.path.join(out, "pmc1"), "k_num_heavy").get("WRITE_SIZE", [])
+    if not f or not w:
+        sys.exit("no k_num_heavy dispatches in the PMC output")
+    fetch = sum(f) / len(f) * 1024.0
+    write = sum(w) / len(w) * 1024.0
+    res = {"kernel": "k_num_heavy", "scale": scale, "edgefactor": 16, "launches": [len(f), len(w)],
+           "fetch_bytes_per_launch": fetch, "write_bytes_per_launch": write,
+           "bytes_per_launch": fetch + write, "bytes_per_launch_fetch_doubled": 2 * fetch + write,
+           "note": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (KiB x 1024), averaged over dispatches; "
+                   "gfx950 halves FETCH_SIZE for 16-B/lane streams, gathers are uncalibrated"}
+    dst = os.path.join(out, f"{tag}_pmc_heavy.json")   # copied into profiles/ by hand
+    json.dump(res, open(dst, "w"), indent=1)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    if len(sys.argv) >= 3 and sys.argv[1] == "run":
+        run(sys.argv[2], int(sys.argv[3]) if len(sys.argv) > 3 else 20)
+    else:
+        print(__doc__)
