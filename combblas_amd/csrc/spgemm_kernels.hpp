@@ -143,10 +143,11 @@ __device__ __forceinline__ int block_excl_scan(int v, int* scratch, int* total) 
   int inc = wave_incl_scan(v);
   if (l == kWave - 1) scratch[w] = inc;
   __syncthreads();
-  if (threadIdx.x == 0) {
-    int run = 0;
-    for (int i = 0; i < NW; ++i) { int t = scratch[i]; scratch[i] = run; run += t; }
-    scratch[NW] = run;
+  if (threadIdx.x < kWave) {
+    const int p = l < NW ? scratch[l] : 0;
+    const int pi = wave_incl_scan(p);
+    if (l < NW) scratch[l] = pi - p;
+    if (l == NW - 1) scratch[NW] = pi;
   }
   __syncthreads();
   int ex = scratch[w] + inc - v;
@@ -448,8 +449,8 @@ __device__ __forceinline__ bool hash_insert_num(Table<typename SRT::Acc>& t, int
                                                 typename SRT::Acc x, int* adderr) {
   int32_t s = (int32_t)home;
   while (s < t.Tcap) {
-    int32_t cur = t.keys[s];
-    if (cur == kEmpty) cur = atomicCAS(&t.keys[s], kEmpty, r);
+    // one LDS op per probe step: claims an empty slot, or returns the key already there
+    const int32_t cur = atomicCAS(&t.keys[s], kEmpty, r);
     if (cur == kEmpty || cur == r) {
       if (SRT::kAddIsError && cur == r) *adderr = 1;
       SRT::acc(&t.vals[s], x);
@@ -932,6 +933,7 @@ __device__ __forceinline__ void compact_hash_runs(const int32_t* keys, const typ
 //      home group of >= 2 keys is insertion-sorted by the thread owning that home;
 //   5. the staged block is written out coalesced.
 // TC = table slots (Te + tail), CH = ceil(TC/NT) <= CHMAX slots per thread (contiguous chunks).
+// hc (Te/2 words) must be zero on entry (the caller clears it with the table).
 // Contains barriers; the caller synchronises before the table is re-initialised.
 template <class SRT, typename V, int NT, int CHMAX>
 __device__ __forceinline__ void compact_hash_homes(int32_t* keys, typename SRT::Acc* vals, int TC, int Te,
@@ -942,22 +944,29 @@ __device__ __forceinline__ void compact_hash_homes(int32_t* keys, typename SRT::
   const int CH = (TC + NT - 1) / NT;
   const int c0 = threadIdx.x * CH;
   const int NW = Te >> 1;                        // packed count words
-  for (int w = threadIdx.x; w < NW; w += NT) hc[w] = 0u;
-  __syncthreads();
+  STAMP_DECL
+  STAMP(14);
+  // 1. count keys per home; the returned count is the key's index inside its home group
   int32_t rk[CHMAX];
+  Acc rv[CHMAX];
   uint32_t hm[CHMAX];
+  int ix[CHMAX];
 #pragma unroll
   for (int i = 0; i < CHMAX; ++i) {
     const int sl = c0 + i;
     rk[i] = (i < CH && sl < TC) ? keys[sl] : kEmpty;
     hm[i] = 0;
+    ix[i] = 0;
     if (rk[i] != kEmpty) {
       hm[i] = mono_home(rk[i], lo, mult);
-      atomicAdd(&hc[hm[i] >> 1], 1u << (16 * (hm[i] & 1)));
+      rv[i] = vals[sl];
+      const uint32_t sh = 16 * (hm[i] & 1);
+      ix[i] = (int)((atomicAdd(&hc[hm[i] >> 1], 1u << sh) >> sh) & 0xffffu);
     }
   }
   __syncthreads();
-  // exclusive scan over the Te 16-bit counts: thread t owns count words [w0, w1) (homes 2*w0 ...)
+  STAMP(15);
+  // 2. exclusive scan over the Te 16-bit counts in place: hc half h = base(h)
   const int WP = (NW + NT - 1) / NT;
   const int w0 = min(NW, (int)threadIdx.x * WP), w1 = min(NW, w0 + WP);
   int local = 0;
@@ -974,18 +983,25 @@ __device__ __forceinline__ void compact_hash_homes(int32_t* keys, typename SRT::
     run += (int)(c_lo + c_hi);
   }
   __syncthreads();
-  int ro[CHMAX];
-  Acc rv[CHMAX];
+  STAMP(16);
+  // 3. positions; the index-0 key of a home group also learns the group size
+  int ro[CHMAX], gs[CHMAX];
 #pragma unroll
   for (int i = 0; i < CHMAX; ++i) {
     ro[i] = -1;
+    gs[i] = 0;
     if (rk[i] != kEmpty) {
-      const uint32_t sh = 16 * (hm[i] & 1);
-      ro[i] = (int)((atomicAdd(&hc[hm[i] >> 1], 1u << sh) >> sh) & 0xffffu);
-      rv[i] = vals[c0 + i];
+      const uint32_t h = hm[i];
+      const int base = (int)((hc[h >> 1] >> (16 * (h & 1))) & 0xffffu);
+      ro[i] = base + ix[i];
+      if (ix[i] == 0) {
+        const int nxt = (h + 1 < (uint32_t)Te) ? (int)((hc[(h + 1) >> 1] >> (16 * ((h + 1) & 1))) & 0xffffu) : tot;
+        gs[i] = nxt - base;
+      }
     }
   }
   __syncthreads();   // every table read is done: reuse keys/vals as the staging buffer
+  STAMP(17);
 #pragma unroll
   for (int i = 0; i < CHMAX; ++i)
     if (ro[i] >= 0) {
@@ -993,31 +1009,34 @@ __device__ __forceinline__ void compact_hash_homes(int32_t* keys, typename SRT::
       vals[ro[i]] = rv[i];
     }
   __syncthreads();
-  // home h's group is [end(h-1), end(h)), end = the advanced cursor; sort groups of >= 2 keys
-  for (int h = 2 * w0; h < 2 * w1; ++h) {
-    const uint32_t w = hc[h >> 1];
-    const int e = (int)((w >> (16 * (h & 1))) & 0xffffu);
-    int st;
-    if (h == 0) st = 0;
-    else { const uint32_t wp = hc[(h - 1) >> 1]; st = (int)((wp >> (16 * ((h - 1) & 1))) & 0xffffu); }
-    for (int i = st + 1; i < e; ++i) {
-      const int32_t k = keys[i];
-      const Acc v = vals[i];
-      int q = i - 1;
-      while (q >= st && keys[q] > k) {
-        keys[q + 1] = keys[q];
-        vals[q + 1] = vals[q];
-        --q;
+  STAMP(18);
+  // 4. keys sharing a home (1-3 at load <= 0.5) were staged in arbitrary order: the group's first
+  //    key sorts the group
+#pragma unroll
+  for (int i = 0; i < CHMAX; ++i) {
+    if (gs[i] >= 2) {
+      const int st = ro[i], e = ro[i] + gs[i];
+      for (int p = st + 1; p < e; ++p) {
+        const int32_t k = keys[p];
+        const Acc v = vals[p];
+        int q = p - 1;
+        while (q >= st && keys[q] > k) {
+          keys[q + 1] = keys[q];
+          vals[q + 1] = vals[q];
+          --q;
+        }
+        keys[q + 1] = k;
+        vals[q + 1] = v;
       }
-      keys[q + 1] = k;
-      vals[q + 1] = v;
     }
   }
   __syncthreads();
+  STAMP(19);
   for (int i = threadIdx.x; i < tot; i += NT) {
     orow[ob + i] = keys[i];
     oval[ob + i] = SRT::out(vals[i], aval, bval);
   }
+  STAMP(20);
 }
 
 // ---- wave numeric: one item per wavefront, table T slots (+kTail) per wave
@@ -1217,7 +1236,7 @@ struct HeavyItem {
 
 template <class SRT, typename V, int LOGT, int NT>
 constexpr size_t num_heavy_lds() {
-  return num_block_lds<SRT, V, LOGT, NT>() + kItemUnits * sizeof(Unit);
+  return num_block_lds<SRT, V, LOGT, NT>() + kItemUnits * sizeof(Unit) + (size_t)(1 << LOGT) * 2;
 }
 
 template <class SRT, typename V, int LOGT, int NT>
@@ -1237,6 +1256,7 @@ __global__ void __launch_bounds__(NT) k_num_heavy(const HeavyItem* __restrict__ 
   int32_t* keys = (int32_t*)(bvs + NT);          // T + NT
   int* misc = keys + T + NT;                     // [1] overflow, [2] adderr, [8..] int scan (64 ints)
   Unit* s_units = (Unit*)(misc + 64);            // kItemUnits
+  uint32_t* hc = (uint32_t*)(s_units + kItemUnits); // T/2 packed home counters (compaction)
   const SegBuf<V> sb{qb, off, bvs, scr, lens};
   STAMP_DECL
   STAMP(0);
@@ -1284,6 +1304,7 @@ __global__ void __launch_bounds__(NT) k_num_heavy(const HeavyItem* __restrict__ 
       for (int s = threadIdx.x; s < spn; s += NT) vals[s] = SRT::identity();
     } else {
       for (int s = threadIdx.x; s < TC; s += NT) { keys[s] = kEmpty; vals[s] = SRT::identity(); }
+      for (int s = threadIdx.x; s < (Te >> 1); s += NT) hc[s] = 0u;
     }
     if (threadIdx.x == 0) { misc[1] = 0; misc[2] = 0; }
     __syncthreads();
@@ -1330,7 +1351,7 @@ __global__ void __launch_bounds__(NT) k_num_heavy(const HeavyItem* __restrict__ 
       }
     } else {
       STAMP(7);
-      compact_hash_homes<SRT, V, NT, T / NT + 1>(keys, vals, TC, Te, wk.lo, mult, (uint32_t*)qb, misc + 8, ob,
+      compact_hash_homes<SRT, V, NT, T / NT + 1>(keys, vals, TC, Te, wk.lo, mult, hc, misc + 8, ob,
                                                 A.val, B.val, out.row, out.val);
       STAMP(8);
       STAMP_COUNT(13, 1);

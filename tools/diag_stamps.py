@@ -26,7 +26,8 @@ names = {0: "item setup", 1: "(unused)", 2: "table init", 3: "stage (fetch+scan)
 tot = sum(s[i] for i in range(9))
 for i in range(9):
     print(f"phase {i} {names[i]:40s} {s[i]:16d} cycles  {100.0*s[i]/max(tot,1):5.1f}%")
-for i, nm in ((15, "  sort_runs (thread 0)"), (16, "  sync after sort"), (17, "  count+scan+staging+sync"), (18, "  coalesced copy (thread 0)")):
+for i, nm in ((15, "  home count atomics+sync"), (16, "  scan+rewrite+sync"), (17, "  positions+sync"),
+              (18, "  staging writes+sync"), (19, "  group sort+sync"), (20, "  coalesced copy (thread 0)")):
     print(f"phase {i} {nm:40s} {s[i]:16d} cycles")
 print("runs", s[19], "keys in runs", s[20], "max run", s[21], "sum L^2", s[22])
 print("units", s[10], "chunks", s[11], "multiplies", s[12], "hash units", s[13])
