@@ -40,9 +40,11 @@ namespace {  // internal linkage: every translation unit instantiates its own ke
 constexpr int kWave = 64;
 constexpr int32_t kEmpty = -1;
 constexpr int kLong = 64;          // k_window: segment length handed to a whole wavefront
-constexpr int kUnroll = 2;         // groups of kGroup multiplies in flight per lane (numeric)
-constexpr int kUnrollSym = 4;      // same, symbolic (4-byte items)
+constexpr int kUnroll = 2;         // groups of G multiplies in flight per lane (numeric)
+constexpr int kUnrollSym = 2;      // same, symbolic (4-byte items)
 constexpr int kUnrollHeavy = 2;    // same, k_num_heavy
+constexpr int kGroupSym = 4;       // consecutive A entries per lane group (one segment search each), symbolic
+constexpr int kGroupNum = 2;       // same, numeric
 constexpr int64_t kHeavy = 4096;   // nnz(C(:,j)) above which a column is split into units
 constexpr int64_t kUnitCap = 4096; // max outputs of a multi-subwindow unit (T = 8192, load <= 0.5)
 constexpr int kSplitMin = 16;      // A columns at least this long get split-table rows
@@ -348,15 +350,14 @@ __device__ __forceinline__ int seg_search(const int64_t* off, int64_t m, int P) 
 }
 
 // Stage one chunk of NT segments (this lane's a0, a1, bv) into LDS; returns the chunk's number of
-// GROUPS: a segment of len multiplies is cut into ceil(len/kGroup) groups of kGroup consecutive A
+// GROUPS: a segment of len multiplies is cut into ceil(len/G) groups of G consecutive A
 // entries, and the groups (not the multiplies) are what lanes are dealt.  The LDS arrays are valid
 // on return (synchronised).
-constexpr int kGroup = 4;
-template <int NT, bool WAVE, typename V>
+template <int NT, bool WAVE, int G, typename V>
 __device__ __forceinline__ int64_t stage_segments(const SegBuf<V>& sb, int64_t a0, int64_t a1, V bv) {
   const int tid = WAVE ? lane_id() : (int)threadIdx.x;
   const int64_t len = a1 - a0;
-  const int64_t ng = (len + kGroup - 1) / kGroup;
+  const int64_t ng = (len + G - 1) / G;
   int64_t ex, F;
   if constexpr (WAVE) {
     const int64_t inc = wave_incl_scan64(ng);
@@ -374,17 +375,17 @@ __device__ __forceinline__ int64_t stage_segments(const SegBuf<V>& sb, int64_t a
 }
 
 // Deal the F staged groups to the NT lanes: lane t takes groups g = g0 + u*NT + t and finds the
-// group's segment by a binary search over the LDS prefix offsets (one search per kGroup multiplies),
-// then issues the group's kGroup gathers back to back (U*kGroup independent gathers per lane).
+// group's segment by a binary search over the LDS prefix offsets (one search per G multiplies),
+// then issues the group's G gathers back to back (U*G independent gathers per lane).
 // `base` is the B position of staged segment 0.  The caller synchronises before re-staging.
-template <int NT, int U, typename V, class LdF, class InsF>
+template <int NT, int U, int G, typename V, class LdF, class InsF>
 __device__ __forceinline__ void expand_staged(const SegBuf<V>& sb, int tid, int64_t F, int64_t base, int nseg,
                                               LdF ld, InsF ins) {
   using Item = decltype(ld(int64_t(0)));
   int P = 1;
   while (P < nseg) P <<= 1;
   for (int64_t g0 = 0; g0 < F; g0 += (int64_t)NT * U) {
-    Item it[U][kGroup];
+    Item it[U][G];
     int ss[U];
     int64_t qq[U];
     int nv[U];
@@ -394,12 +395,12 @@ __device__ __forceinline__ void expand_staged(const SegBuf<V>& sb, int tid, int6
       nv[u] = 0;
       if (g < F) {
         const int sg = seg_search<NT>(sb.off, g, P);
-        const int64_t k0 = (g - sb.off[sg]) * kGroup;
+        const int64_t k0 = (g - sb.off[sg]) * G;
         ss[u] = sg;
         qq[u] = sb.qb[sg] + k0;
-        nv[u] = (int)min<int64_t>(kGroup, sb.len[sg] - k0);
+        nv[u] = (int)min<int64_t>(G, sb.len[sg] - k0);
 #pragma unroll
-        for (int i = 0; i < kGroup; ++i)
+        for (int i = 0; i < G; ++i)
           if (i < nv[u]) it[u][i] = ld(qq[u] + i);
       }
     }
@@ -408,14 +409,14 @@ __device__ __forceinline__ void expand_staged(const SegBuf<V>& sb, int tid, int6
       if (nv[u] > 0) {
         const V bv = sb.bv[ss[u]];
 #pragma unroll
-        for (int i = 0; i < kGroup; ++i)
+        for (int i = 0; i < G; ++i)
           if (i < nv[u]) ins(it[u][i], bv, qq[u] + i, base + ss[u]);
       }
     }
   }
 }
 
-template <int NT, bool WAVE, int U, typename V, class SegF, class LdF, class InsF>
+template <int NT, bool WAVE, int U, int G, typename V, class SegF, class LdF, class InsF>
 __device__ __forceinline__ void for_each_multiply(int64_t bs, int64_t be, SegBuf<V> sb, SegF seg, LdF ld, InsF ins) {
   const int tid = WAVE ? lane_id() : (int)threadIdx.x;
   for (int64_t base = bs; base < be; base += NT) {
@@ -423,8 +424,8 @@ __device__ __forceinline__ void for_each_multiply(int64_t bs, int64_t be, SegBuf
     int64_t a0 = 0, a1 = 0;
     V bv = V(0);
     if (b < be) seg(b, a0, a1, bv);
-    const int64_t F = stage_segments<NT, WAVE, V>(sb, a0, a1, bv);
-    expand_staged<NT, U, V>(sb, tid, F, base, (int)min<int64_t>(NT, be - base), ld, ins);
+    const int64_t F = stage_segments<NT, WAVE, G, V>(sb, a0, a1, bv);
+    expand_staged<NT, U, G, V>(sb, tid, F, base, (int)min<int64_t>(NT, be - base), ld, ins);
     if constexpr (WAVE) wave_sync(); else __syncthreads();
   }
 }
@@ -527,7 +528,7 @@ __global__ void __launch_bounds__(256) k_sym_wave(const int32_t* __restrict__ li
     for (int s = l; s < T; s += kWave) tab[s] = bitmap ? 0 : kEmpty;
     wave_sync();
     int cnt = 0;
-    for_each_multiply<kWave, true, kUnrollSym, uint8_t>(
+    for_each_multiply<kWave, true, kUnrollSym, kGroupSym, uint8_t>(
         Bcp[j], Bcp[j + 1], sb,
         [&](int64_t b, int64_t& a0, int64_t& a1, uint8_t&) {
           const int32_t k = Bir[b];
@@ -594,7 +595,7 @@ __global__ void __launch_bounds__(NT) k_sym_block(const int32_t* __restrict__ li
     if (threadIdx.x == 0) misc[1] = 0;
     __syncthreads();
     int cnt = 0;
-    for_each_multiply<NT, false, kUnrollSym, uint8_t>(
+    for_each_multiply<NT, false, kUnrollSym, kGroupSym, uint8_t>(
         Bcp[j], Bcp[j + 1], sb,
         [&](int64_t b, int64_t& a0, int64_t& a1, uint8_t&) {
           const int32_t k = Bir[b];
@@ -1111,7 +1112,7 @@ __global__ void __launch_bounds__(256) k_num_wave(const int32_t* __restrict__ li
     for (int s = l; s < TC; s += kWave) { t.keys[s] = dense ? 0 : kEmpty; t.vals[s] = SRT::identity(); }
     wave_sync();
     int ovf = 0, aerr = 0;
-    for_each_multiply<kWave, true, kUnroll, V>(
+    for_each_multiply<kWave, true, kUnroll, kGroupNum, V>(
         B.cp[wk.j], B.cp[wk.j + 1], sb,
         [&](int64_t b, int64_t& a0, int64_t& a1, V& bv) { num_seg<V, UNIT>(A, B, spl, spl.useg, wk, b, a0, a1, bv); },
         [&](int64_t q) { return NumItem<V>{A.ir[q], load_val(A.val, q)}; },
@@ -1185,7 +1186,7 @@ __global__ void __launch_bounds__(NT) k_num_block(const int32_t* __restrict__ li
     if (threadIdx.x == 0) { misc[1] = 0; misc[2] = 0; }
     __syncthreads();
     int ovf = 0, aerr = 0;
-    for_each_multiply<NT, false, kUnroll, V>(
+    for_each_multiply<NT, false, kUnroll, kGroupNum, V>(
         B.cp[wk.j], B.cp[wk.j + 1], sb,
         [&](int64_t b, int64_t& a0, int64_t& a1, V& bv) { num_seg<V, UNIT>(A, B, spl, spl.useg, wk, b, a0, a1, bv); },
         [&](int64_t q) { return NumItem<V>{A.ir[q], load_val(A.val, q)}; },
@@ -1316,11 +1317,11 @@ __global__ void __launch_bounds__(NT) k_num_heavy(const HeavyItem* __restrict__ 
       const V bv = pbv;
       if (c + NT < nb) fetch(u, c + NT, pa0, pa1, pbv);
       else fetch(u + 1, 0, pa0, pa1, pbv);
-      const int64_t F = stage_segments<NT, false, V>(sb, a0, a1, bv);
+      const int64_t F = stage_segments<NT, false, kGroupNum, V>(sb, a0, a1, bv);
       STAMP(3);
       STAMP_COUNT(11, 1);
       STAMP_COUNT(12, F);
-      expand_staged<NT, kUnrollHeavy, V>(
+      expand_staged<NT, kUnrollHeavy, kGroupNum, V>(
           sb, threadIdx.x, F, bs + c, (int)min<int64_t>(NT, nb - c), [&](int64_t q) { return NumItem<V>{A.ir[q], load_val(A.val, q)}; },
           [&](const NumItem<V>& it, V bv2, int64_t q, int64_t b) {
             num_insert<SRT, V, true>(t, dense, wk, mult, it, bv2, q, b, ovf, aerr);
