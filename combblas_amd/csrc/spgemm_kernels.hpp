@@ -45,6 +45,7 @@ constexpr int kUnrollSym = 2;      // same, symbolic (4-byte items)
 constexpr int kUnrollHeavy = 2;    // same, k_num_heavy
 constexpr int kGroupSym = 4;       // consecutive A entries per lane group (one segment search each), symbolic
 constexpr int kGroupNum = 2;       // same, numeric
+constexpr int kGroupHeavy = 2;     // same, k_num_heavy
 constexpr int64_t kHeavy = 4096;   // nnz(C(:,j)) above which a column is split into units
 constexpr int64_t kUnitCap = 4096; // max outputs of a multi-subwindow unit (T = 8192, load <= 0.5)
 constexpr int kSplitMin = 16;      // A columns at least this long get split-table rows
@@ -985,20 +986,14 @@ __device__ __forceinline__ void compact_hash_homes(int32_t* keys, typename SRT::
   }
   __syncthreads();
   STAMP(16);
-  // 3. positions; the index-0 key of a home group also learns the group size
-  int ro[CHMAX], gs[CHMAX];
+  // 3. positions: group base + index inside the group
+  int ro[CHMAX];
 #pragma unroll
   for (int i = 0; i < CHMAX; ++i) {
     ro[i] = -1;
-    gs[i] = 0;
     if (rk[i] != kEmpty) {
       const uint32_t h = hm[i];
-      const int base = (int)((hc[h >> 1] >> (16 * (h & 1))) & 0xffffu);
-      ro[i] = base + ix[i];
-      if (ix[i] == 0) {
-        const int nxt = (h + 1 < (uint32_t)Te) ? (int)((hc[(h + 1) >> 1] >> (16 * ((h + 1) & 1))) & 0xffffu) : tot;
-        gs[i] = nxt - base;
-      }
+      ro[i] = (int)((hc[h >> 1] >> (16 * (h & 1))) & 0xffffu) + ix[i];
     }
   }
   __syncthreads();   // every table read is done: reuse keys/vals as the staging buffer
@@ -1011,26 +1006,36 @@ __device__ __forceinline__ void compact_hash_homes(int32_t* keys, typename SRT::
     }
   __syncthreads();
   STAMP(18);
-  // 4. keys sharing a home (1-3 at load <= 0.5) were staged in arbitrary order: the group's first
-  //    key sorts the group
+  // 4. keys sharing a home (1-3 at load <= 0.5) were staged contiguously but in arbitrary order:
+  //    every output position computes its key's rank inside its group with independent reads of the
+  //    group (no dependent chains), then all keys move after one barrier
+  constexpr int PMAX = CHMAX;                    // tot <= Te/2 <= CHMAX * NT
+  int pp[PMAX];
+  int32_t pk[PMAX];
+  Acc pv[PMAX];
 #pragma unroll
-  for (int i = 0; i < CHMAX; ++i) {
-    if (gs[i] >= 2) {
-      const int st = ro[i], e = ro[i] + gs[i];
-      for (int p = st + 1; p < e; ++p) {
-        const int32_t k = keys[p];
-        const Acc v = vals[p];
-        int q = p - 1;
-        while (q >= st && keys[q] > k) {
-          keys[q + 1] = keys[q];
-          vals[q + 1] = vals[q];
-          --q;
-        }
-        keys[q + 1] = k;
-        vals[q + 1] = v;
-      }
+  for (int i = 0; i < PMAX; ++i) {
+    const int p = (int)threadIdx.x + i * NT;
+    pp[i] = -1;
+    if (p < tot) {
+      const int32_t k = keys[p];
+      const uint32_t h = mono_home(k, lo, mult);
+      const int st = (int)((hc[h >> 1] >> (16 * (h & 1))) & 0xffffu);
+      const int en = (h + 1 < (uint32_t)Te) ? (int)((hc[(h + 1) >> 1] >> (16 * ((h + 1) & 1))) & 0xffffu) : tot;
+      int r = 0;
+      for (int q = st; q < en; ++q) r += (keys[q] < k);
+      pp[i] = st + r;
+      pk[i] = k;
+      pv[i] = vals[p];
     }
   }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < PMAX; ++i)
+    if (pp[i] >= 0) {
+      keys[pp[i]] = pk[i];
+      vals[pp[i]] = pv[i];
+    }
   __syncthreads();
   STAMP(19);
   for (int i = threadIdx.x; i < tot; i += NT) {
@@ -1317,11 +1322,11 @@ __global__ void __launch_bounds__(NT) k_num_heavy(const HeavyItem* __restrict__ 
       const V bv = pbv;
       if (c + NT < nb) fetch(u, c + NT, pa0, pa1, pbv);
       else fetch(u + 1, 0, pa0, pa1, pbv);
-      const int64_t F = stage_segments<NT, false, kGroupNum, V>(sb, a0, a1, bv);
+      const int64_t F = stage_segments<NT, false, kGroupHeavy, V>(sb, a0, a1, bv);
       STAMP(3);
       STAMP_COUNT(11, 1);
       STAMP_COUNT(12, F);
-      expand_staged<NT, kUnrollHeavy, kGroupNum, V>(
+      expand_staged<NT, kUnrollHeavy, kGroupHeavy, V>(
           sb, threadIdx.x, F, bs + c, (int)min<int64_t>(NT, nb - c), [&](int64_t q) { return NumItem<V>{A.ir[q], load_val(A.val, q)}; },
           [&](const NumItem<V>& it, V bv2, int64_t q, int64_t b) {
             num_insert<SRT, V, true>(t, dense, wk, mult, it, bv2, q, b, ovf, aerr);
