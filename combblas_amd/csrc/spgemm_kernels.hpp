@@ -1219,13 +1219,13 @@ __global__ void __launch_bounds__(NT) k_num_block(const int32_t* __restrict__ li
         ++o;
       }
     } else {
-      constexpr int CH = TC / NT;
-      const int c0 = threadIdx.x * CH, c1 = c0 + CH;
-      int occ = 0;
-      for (int s = c0; s < c1; ++s) occ += (keys[s] != kEmpty);
-      int tot;
-      const int ex = block_excl_scan<NT>(occ, misc + 8, &tot);
-      compact_hash_runs<SRT, V>(keys, vals, TC, ex, c0, c1, ob, A.val, B.val, out.row, out.val);
+      // home counters in the (now idle) segment staging arrays: T/2 words <= 2*NT int64 slots
+      static_assert((1 << LOGT) * 2 <= NT * 16, "home counters must fit the segment arrays");
+      uint32_t* hc = (uint32_t*)qb;
+      for (int w2 = threadIdx.x; w2 < T / 2; w2 += NT) hc[w2] = 0u;
+      __syncthreads();
+      compact_hash_homes<SRT, V, NT, TC / NT>(keys, vals, TC, T, wk.lo, mult, hc, misc + 8, ob, A.val, B.val,
+                                              out.row, out.val);
     }
     if (threadIdx.x == 0 && misc[2]) atomicOr(out.adderr, 1);
     __syncthreads();
