@@ -126,7 +126,7 @@ struct cbg_ctx {
   // workspace (grow-only)
   DevBuf flop, span, cnt, list, hist, cursor, scan_tiles, scalars, cur, nxt, ovf_list, stageA[5], stageB[5];
   DevBuf split_idx, long_cols, split_tab, heavy_cols, sub, units, ucnt, uspan, ulist, fb_units, fb_list, uovf_list;
-  DevBuf nunits, segsz, segoff, useg, icnt, itemoff, items;
+  DevBuf nunits, segsz, segoff, useg, icnt, itemoff, items, parts, wide_win;
 };
 
 inline hipError_t launch_cfg_lds(const void* fn, size_t lds) {
@@ -257,6 +257,17 @@ hipError_t launch_sym_block(hipStream_t st, const int32_t* l, int64_t n, const i
   hipError_t e = launch_cfg_lds((const void*)k_sym_block<LOGT, NT>, lds);
   if (e != hipSuccess) return e;
   k_sym_block<LOGT, NT><<<(int)grid_for(n, 1, kMaxGrid), NT, lds, st>>>(l, n, Acp, Air, Bcp, Bir, span, nnz, ho);
+  return hipGetLastError();
+}
+template <int NT>
+hipError_t launch_sym_part(hipStream_t st, const PartItem* items, const int* count_dev, int64_t cap,
+                           const int64_t* Acp, const int32_t* Air, const int64_t* Bcp, const int32_t* Bir,
+                           const int2* span, const Split& spl, int64_t* nnz, const HeavyOut& ho) {
+  const size_t lds = sym_part_lds<NT>();
+  hipError_t e = launch_cfg_lds((const void*)k_sym_part<NT>, lds);
+  if (e != hipSuccess) return e;
+  k_sym_part<NT><<<(int)grid_for(cap, 1, kMaxGrid * 2), NT, lds, st>>>(items, count_dev, Acp, Air, Bcp, Bir, span,
+                                                                       spl, nnz, ho);
   return hipGetLastError();
 }
 template <int LOGT, class SRT, typename V, bool UNIT>
@@ -400,12 +411,23 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
   HIPCHK(hipMemsetAsync(hist, 0, sizeof(unsigned long long) * 64, st));
   bin_count(st, N, flop, span, sbp, hist, list);
   HIPCHK(hipMemcpyAsync(hh, hist, sizeof(unsigned long long) * 32, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(hh + 32, sc, 32, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
+  const int NL = ((int*)&hh[34])[1];
   if ((s = bin_fill(st, N, flop, span, sbp, hist, hh, list, &cs)) != CBG_OK) return s;
   const int64_t hcap = (int64_t)cs.hist[31];
   HIPCHK(ctx->heavy_cols.reserve(sizeof(int32_t) * (hcap + 1)));
   HIPCHK(ctx->sub.reserve(sizeof(int32_t) * (hcap * nsub + 1)));
   HeavyOut ho{heavy_n, ctx->heavy_cols.as<int32_t>(), ctx->sub.as<int32_t>(), nsub, slog};
+  // split table (unit segments, wide-column parts): needed whenever a column can be heavy
+  Split spl{ctx->split_idx.as<int32_t>(), nullptr, nsub, slog};
+  if (hcap > 0) {
+    HIPCHK(ctx->split_tab.reserve(sizeof(int32_t) * ((int64_t)NL * (nsub + 1) + 1)));
+    spl.tab = ctx->split_tab.as<int32_t>();
+    if (NL > 0)
+      k_split_fill<<<(int)grid_for(NL, 4, kMaxGrid * 2), 256, 0, st>>>(NL, ctx->long_cols.as<int32_t>(), A.cp, A.ir,
+                                                                        ctx->split_tab.as<int32_t>(), nsub, slog);
+  }
   HIPCHK(hipEventRecord(ctx->ev[2], st));
   {
     auto L = [&](int c) { return list + cs.off[c]; };
@@ -419,14 +441,31 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
     if (n(6) && e == hipSuccess) e = launch_sym_block<11, 256>(st, L(6), n(6), A.cp, A.ir, B.cp, B.ir, span, nnz, ho);
     if (n(7) && e == hipSuccess) e = launch_sym_block<12, 256>(st, L(7), n(7), A.cp, A.ir, B.cp, B.ir, span, nnz, ho);
     if (n(8) && e == hipSuccess) e = launch_sym_block<13, 512>(st, L(8), n(8), A.cp, A.ir, B.cp, B.ir, span, nnz, ho);
-    if (n(9) && e == hipSuccess) e = launch_sym_block<14, 1024>(st, L(9), n(9), A.cp, A.ir, B.cp, B.ir, span, nnz, ho);
-    if (n(10) && e == hipSuccess) e = launch_sym_block<15, 1024>(st, L(10), n(10), A.cp, A.ir, B.cp, B.ir, span, nnz, ho);
-    if (n(11) && e == hipSuccess) {
-      HIPCHK(ctx->cur.reserve(sizeof(int64_t) * (B.nnz + 1)));
-      HIPCHK(ctx->nxt.reserve(sizeof(int32_t) * (B.nnz + 1)));
-      e = launch_window<0, SRT, V, kSymWinRows>(st, L(11), nullptr, n(11), grid_for(n(11), 1, 1024), A, B, span,
-                                                nullptr, ctx->cur.as<int64_t>(), ctx->nxt.as<int32_t>(), nnz, ho,
-                                                NumOut<V>{});
+    // wide columns (classes kWideClass..11, contiguous in the list): (column, part) items; the
+    // widest (more than kMaxParts parts), or all of them when a subwindow is larger than a part
+    // (nrow > 2^(kPartLog+11)), go to the windowed kernel
+    if (kWideClass > 9 && n(9) && e == hipSuccess)
+      e = launch_sym_block<14, 1024>(st, L(9), n(9), A.cp, A.ir, B.cp, B.ir, span, nnz, ho);
+    int64_t nwide = 0;
+    for (int c = kWideClass; c <= 11; ++c) nwide += n(c);
+    if (nwide && e == hipSuccess) {
+      HIPCHK(ctx->parts.reserve(sizeof(PartItem) * (nwide * kMaxParts + 1)));
+      HIPCHK(ctx->wide_win.reserve(sizeof(int32_t) * (nwide + 1)));
+      int *nparts = si + 8, *nwin = si + 9;
+      k_part_items<<<(int)grid_for(nwide, 256, kMaxGrid), 256, 0, st>>>(L(kWideClass), nwide, slog <= kPartLog ? kMaxParts : 0, span, ho,
+                                                                         ctx->parts.as<PartItem>(), nparts,
+                                                                         ctx->wide_win.as<int32_t>(), nwin);
+      e = launch_sym_part<kPartNT>(st, ctx->parts.as<PartItem>(), nparts, nwide * kMaxParts, A.cp, A.ir, B.cp, B.ir,
+                               span, spl, nnz, ho);
+      const int64_t nw_cap = slog <= kPartLog ? n(11) : nwide;
+      if (nw_cap && e == hipSuccess) {
+        HIPCHK(ctx->cur.reserve(sizeof(int64_t) * (B.nnz + 1)));
+        HIPCHK(ctx->nxt.reserve(sizeof(int32_t) * (B.nnz + 1)));
+        e = launch_window<0, SRT, V, kSymWinRows>(st, ctx->wide_win.as<int32_t>(), nwin, nw_cap,
+                                                  grid_for(nw_cap, 1, 1024), A, B, span, nullptr,
+                                                  ctx->cur.as<int64_t>(), ctx->nxt.as<int32_t>(), nnz, ho,
+                                                  NumOut<V>{});
+      }
     }
     if (e != hipSuccess) { fprintf(stderr, "cbgpu: symbolic launch: %s\n", hipGetErrorString(e)); return CBG_EDEVICE; }
     HIPCHK(hipGetLastError());
@@ -445,21 +484,15 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
   HIPCHK(hipStreamSynchronize(st));
   HIPCHK(hipEventRecord(ctx->ev[4], st));
   const int64_t mults = (int64_t)hsc[0], nnzc = (int64_t)hsc[1];
-  const int H = ((int*)&hsc[2])[0], NL = ((int*)&hsc[2])[1];
+  const int H = ((int*)&hsc[2])[0];
   pf.multiplies = mults; pf.nnz_out = nnzc;
   HIPCHK(own->ir.reserve(sizeof(int32_t) * (nnzc + 1)));
   HIPCHK(own->val.reserve(sizeof(V) * (nnzc + 1)));
 
   // 4. heavy columns -> units (split table + greedy subwindow grouping)
-  Split spl{ctx->split_idx.as<int32_t>(), nullptr, nsub, slog};
   const int64_t nunit_cap = (int64_t)H * nsub;
   Unit* units = nullptr;
   if (H > 0) {
-    HIPCHK(ctx->split_tab.reserve(sizeof(int32_t) * ((int64_t)NL * (nsub + 1) + 1)));
-    spl.tab = ctx->split_tab.as<int32_t>();
-    if (NL > 0)
-      k_split_fill<<<(int)grid_for(NL, 4, kMaxGrid * 2), 256, 0, st>>>(NL, ctx->long_cols.as<int32_t>(), A.cp, A.ir,
-                                                                        ctx->split_tab.as<int32_t>(), nsub, slog);
     HIPCHK(ctx->units.reserve(sizeof(Unit) * (nunit_cap + 1)));
     HIPCHK(ctx->ucnt.reserve(sizeof(int64_t) * (nunit_cap + 1)));
     HIPCHK(ctx->uspan.reserve(sizeof(int2) * (nunit_cap + 1)));

@@ -47,10 +47,10 @@ constexpr int kGroupSym = 4;       // consecutive A entries per lane group (one 
 constexpr int kGroupNum = 2;       // same, numeric
 constexpr int kGroupHeavy = 2;     // same, k_num_heavy
 constexpr int64_t kHeavy = 4096;   // nnz(C(:,j)) above which a column is split into units
-constexpr int64_t kUnitCap = 4096; // max outputs of a multi-subwindow unit (T = 8192, load <= 0.5)
+constexpr int64_t kUnitCap = 4096; // max outputs of a multi-subwindow unit (k_num_heavy T = 8192, load <= 0.5)
 constexpr int kSplitMin = 16;      // A columns at least this long get split-table rows
-constexpr int kMaxSub = 2048;
-constexpr int kItemUnits = 8;      // units of one heavy column per workgroup item (k_num_heavy)      // max subwindows per column (SUBW chosen so nrow/SUBW <= kMaxSub)
+constexpr int kMaxSub = 2048;      // max subwindows per column (SUBW chosen so nrow/SUBW <= kMaxSub)
+constexpr int kItemUnits = 8;      // units of one heavy column per workgroup item (k_num_heavy)
 
 template <typename V>
 struct DevCsc {
@@ -639,6 +639,121 @@ __global__ void __launch_bounds__(NT) k_sym_block(const int32_t* __restrict__ li
   }
 }
 
+// Wide columns (bitmap > 16384 words): the row space is cut into aligned parts of 2^kPartLog rows and
+// each (column, part) is one work item with a 64 KB bitmap, so two workgroups share a CU and hide
+// each other's gather latency (one 128 KB bitmap per CU left the CU idle on every dependent load).
+// A long A column contributes only its entries inside the part (split table, exact); a short one is
+// read whole and filtered at insert.  Every wide column is registered as heavy up front; its parts
+// write disjoint subwindow counts and add their totals into nnz[j].
+#ifndef CBG_PART_LOG
+#define CBG_PART_LOG 18
+#endif
+#ifndef CBG_PART_NT
+#define CBG_PART_NT 512
+#endif
+constexpr int kPartLog = CBG_PART_LOG;
+constexpr int kPartNT = CBG_PART_NT;
+// first symbolic class (LOGT = class + 5) cut into parts: bitmaps larger than one part; every such
+// column has flop > kHeavy (2*flop > 2^(class+4) words), so the heavy lists can hold it
+constexpr int kWideClass = kPartLog - 9 > 9 ? kPartLog - 9 : 9;
+static_assert(kPartLog >= 17 && kPartLog <= 19, "part bitmap 16..64 KB");
+constexpr int kMaxParts = 32;   // wider columns (hypersparse, > 8M-row spans) take the windowed path
+struct PartItem {
+  int32_t j, p, h;
+};
+
+__global__ void k_part_items(const int32_t* __restrict__ list, int64_t count, int maxparts, const int2* __restrict__ span,
+                             HeavyOut ho, PartItem* __restrict__ items, int* __restrict__ nitems,
+                             int32_t* __restrict__ wlist, int* __restrict__ nwin) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < count; i += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t j = list[i];
+    const int2 sp = span[j];
+    const int np = (sp.y >> kPartLog) - (sp.x >> kPartLog) + 1;
+    if (np <= maxparts) {
+      const int h = atomicAdd(ho.n, 1);
+      ho.cols[h] = j;
+      const int e = atomicAdd(nitems, np);
+      for (int p = 0; p < np; ++p) items[e + p] = PartItem{j, p, h};
+    } else {
+      wlist[atomicAdd(nwin, 1)] = j;
+    }
+  }
+}
+
+template <int NT>
+constexpr size_t sym_part_lds() {
+  return (size_t)(1 << (kPartLog - 5)) * 4 + (size_t)NT * 21 + (size_t)(NT / kWave + 1) * 8 +
+         (size_t)((1 << (kPartLog - 13)) + 8) * 4 + 64;
+}
+
+template <int NT>
+__global__ void __launch_bounds__(NT) k_sym_part(const PartItem* __restrict__ items, const int* __restrict__ count_dev,
+                                                 const int64_t* __restrict__ Acp, const int32_t* __restrict__ Air,
+                                                 const int64_t* __restrict__ Bcp, const int32_t* __restrict__ Bir,
+                                                 const int2* __restrict__ span, Split spl, int64_t* __restrict__ nnz,
+                                                 HeavyOut ho) {
+  constexpr int T = 1 << (kPartLog - 5);   // bitmap words
+  constexpr int WPT = T / NT;              // words per thread in the subwindow count (<= SUBW / 32)
+  static_assert(WPT * 32 <= (1 << 13), "a thread's words must lie in one subwindow");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  int64_t* qb = (int64_t*)smem;                    // NT
+  int64_t* off = qb + NT;                          // NT
+  int64_t* scr = off + NT;                         // NT/64 + 1
+  uint32_t* tab = (uint32_t*)(scr + NT / kWave + 1);// T
+  int32_t* scnt = (int32_t*)(tab + T);             // part subwindows (<= 2^(kPartLog-13))
+  int* misc = scnt + (1 << (kPartLog - 13));       // [0] total
+  int32_t* lens = misc + 8;                        // NT
+  uint8_t* bvs = (uint8_t*)(lens + NT);            // NT
+  const SegBuf<uint8_t> sb{qb, off, bvs, scr, lens};
+  const int count = *count_dev;
+  for (int i = blockIdx.x; i < count; i += gridDim.x) {
+    const PartItem it = items[i];
+    const int2 sp = span[it.j];
+    const int32_t r0 = ((sp.x >> kPartLog) + it.p) << kPartLog;
+    const int32_t s0 = r0 >> spl.log;
+    const int32_t s1 = min(spl.nsub, (int32_t)(((int64_t)r0 + (1 << kPartLog)) >> spl.log));
+    for (int s = threadIdx.x; s < T; s += NT) tab[s] = 0;
+    if (threadIdx.x < s1 - s0) scnt[threadIdx.x] = 0;
+    if (threadIdx.x == 0) misc[0] = 0;
+    __syncthreads();
+    for_each_multiply<NT, false, kUnrollSym, kGroupSym, uint8_t>(
+        Bcp[it.j], Bcp[it.j + 1], sb,
+        [&](int64_t b, int64_t& a0, int64_t& a1, uint8_t&) {
+          const int32_t k = Bir[b];
+          const int64_t c0 = Acp[k], c1 = Acp[k + 1];
+          if (c1 - c0 >= kSplitMin) {
+            const int32_t* t = spl.tab + (int64_t)spl.idx[k] * (spl.nsub + 1);
+            a0 = c0 + t[s0];
+            a1 = c0 + t[s1];
+          } else {
+            a0 = c0;
+            a1 = c1;
+          }
+        },
+        [&](int64_t q) { return Air[q]; },
+        [&](int32_t r, uint8_t, int64_t, int64_t) {
+          const uint32_t o = (uint32_t)(r - r0);
+          if (o < (1u << kPartLog)) {
+            const uint32_t bit = 1u << (o & 31);
+            if (!(tab[o >> 5] & bit)) atomicOr(&tab[o >> 5], bit);
+          }
+        });
+    __syncthreads();
+    int c = 0;
+#pragma unroll 8
+    for (int w = 0; w < WPT; ++w) c += __popc(tab[threadIdx.x * WPT + w]);
+    if (c) atomicAdd(&scnt[((r0 + threadIdx.x * WPT * 32) >> spl.log) - s0], c);
+    const int64_t wc = wave_sum64(c);
+    if (lane_id() == 0 && wc) atomicAdd(&misc[0], (int)wc);
+    __syncthreads();
+    if (threadIdx.x == 0 && misc[0]) atomicAdd((unsigned long long*)&nnz[it.j], (unsigned long long)misc[0]);
+    const int32_t sf = max(s0, sp.x >> spl.log), sl = min(s1 - 1, sp.y >> spl.log);
+    int32_t* dst = ho.sub + (int64_t)it.h * ho.nsub;
+    for (int s = sf + (int)threadIdx.x; s <= sl; s += NT) dst[s] = scnt[s - s0];
+    __syncthreads();
+  }
+}
+
 // ============================================================================ 4. scan
 // exclusive scan of int64 counts into colptr[n+1]; 3 kernels, tile = 1024 elements
 constexpr int kScanTile = 1024;
@@ -757,6 +872,12 @@ __global__ void k_build_units(int H, const int32_t* __restrict__ cols, const int
   const int h = blockIdx.x * blockDim.x + threadIdx.x;
   if (h >= H) return;
   const int32_t j = cols[h];
+  if (nnz[j] <= kHeavy) {   // a wide column (registered before its count was known) that stayed light
+    nunits[h] = 0;
+    segsz[h] = 0;
+    icnt[h] = 0;
+    return;
+  }
   const int2 sp = span[j];
   const int32_t sf = sp.x >> log, sl = sp.y >> log;
   const int32_t* c = sub + (int64_t)h * nsub;

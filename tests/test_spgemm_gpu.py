@@ -185,6 +185,35 @@ def test_gpu_heavy_column_window_kernel(gpu_ctx):
     _check_vs_oracle(gpu_ctx, A, B)
 
 
+@pytest.mark.parametrize("n,sr,dt", [(1 << 21, "plus_times", "f64"), (3 << 19, "min_plus", "i64"),
+                                      (1 << 21, "select_max", "i64"), (1 << 24, "plus_times", "i64")])
+def test_gpu_wide_column_parts(gpu_ctx, n, sr, dt):
+    """Wide output columns (bitmap > 16384 words): symbolic runs as (column, 2^19-row part) items with
+    split-table segments for long A columns and filtered short ones; spans not aligned to parts,
+    columns touching 1..all parts.  n = 2^24 puts 32 parts in one column -> windowed symbolic."""
+    rng = np.random.default_rng(n % 1000 + len(sr))
+    ncolA = 120
+    lens = np.where(rng.random(ncolA) < 0.4, rng.integers(16, 2500, ncolA), rng.integers(1, 16, ncolA))
+    cols = []
+    for c, L in enumerate(lens):
+        lo = int(rng.integers(0, n // 2)) if c % 4 == 0 else 0
+        hi = n if c % 5 else int(rng.integers(lo + L + 1, n))
+        cols.append(np.sort(lo + rng.choice(hi - lo, int(L), replace=False)).astype(np.int32))
+    cp = np.r_[0, np.cumsum(lens)]
+    vals = rng.integers(-4, 5, cp[-1]).astype(np.int64) if dt == "i64" else rng.uniform(-1, 1, cp[-1])
+    A = Csc(n, ncolA, cp, np.concatenate(cols), vals)
+    nb = 12
+    bcp, bir = [0], []
+    for j in range(nb):
+        k = np.sort(rng.choice(ncolA, int(rng.integers(3, 60)), replace=False))
+        bir.append(k.astype(np.int32))
+        bcp.append(bcp[-1] + len(k))
+    bv = rng.integers(-4, 5, bcp[-1]).astype(np.int64) if dt == "i64" else rng.uniform(-1, 1, bcp[-1])
+    B = Csc(ncolA, nb, bcp, np.concatenate(bir), bv)
+    _check_vs_oracle(gpu_ctx, A, B, sr, dt)
+    assert gpu_ctx.last_profile()["bins"][12] > 0
+
+
 @pytest.mark.parametrize("scale", [12, 14, 16])
 def test_gpu_rmat_vs_oracle(gpu_ctx, scale):
     n, cp, ir, val = cb.generate_rmat_host(scale, 16, seed=scale)
