@@ -312,3 +312,8 @@ def generate_rmat_host(scale, edgefactor=16, seed=1):
     finally:
         L.cbg_host_free(ctypes.byref(h))
     return n, cp, ir, val
+
+
+from .mcl import MCLPruneRecoverySelect, MemEfficientSpGEMM, MCL_DEFAULTS  # noqa: E402
+
+__all__ += ["MCLPruneRecoverySelect", "MemEfficientSpGEMM", "MCL_DEFAULTS"]

@@ -43,6 +43,11 @@ class HostCsc(ctypes.Structure):
                 ("colptr", ctypes.c_void_p), ("row", ctypes.c_void_p), ("val", ctypes.c_void_p)]
 
 
+class MclStats(ctypes.Structure):
+    _fields_ = [("recovered", ctypes.c_int64), ("selected", ctypes.c_int64),
+                ("recovered_after_select", ctypes.c_int64), ("nnz_in", ctypes.c_int64), ("nnz_out", ctypes.c_int64)]
+
+
 # name -> (restype, argtypes); must match include/cbgpu.h exactly
 SIGNATURES = {
     "cbg_abi_version": (ctypes.c_int32, []),
@@ -68,6 +73,13 @@ SIGNATURES = {
                                          ctypes.POINTER(CscResult)]),
     "cbg_rmat_host": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_uint64, ctypes.POINTER(HostCsc)]),
     "cbg_host_free": (None, [ctypes.POINTER(HostCsc)]),
+    "cbg_mcl_prune": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(CscResult), ctypes.c_double, ctypes.c_int64,
+                                     ctypes.c_int64, ctypes.c_double, ctypes.POINTER(CscResult),
+                                     ctypes.POINTER(MclStats)]),
+    "cbg_col_range": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(CscResult), ctypes.c_int64, ctypes.c_int64,
+                                     ctypes.POINTER(CscResult)]),
+    "cbg_col_concat": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(CscResult), ctypes.c_int32,
+                                      ctypes.POINTER(CscResult)]),
 }
 
 _lib = None

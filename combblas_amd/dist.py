@@ -207,16 +207,17 @@ def _allgather_nnz(blk, group, size, backend):
     return [int(x.item()) for x in out]
 
 
-def _fiber_exchange(C, grid, ncol_global, backend, sr):
+def _fiber_exchange(C, grid, backend, sr):
     """Reduce the L layers' partials of C(i, j) (Reductions.h:36-130 / ParFriends.h SUMMA3D fiber
     all-to-all): layer part m of the local partial's columns goes to the fiber's rank m, and each
-    rank merges the L pieces it receives (MultiwayMergeHash semantics: SR::add in layer order)."""
-    L, q = grid.L, grid.q
-    b0, _ = block_range(ncol_global, q, grid.col)
-    bounds = [piece_range(ncol_global, q, L, grid.col, m) for m in range(L)]
+    rank merges the L pieces it receives (MultiwayMergeHash semantics: SR::add in layer order).
+    Layer part m of the local columns = block_range(ncol_local, L, m), which is piece_range of the
+    global column block (CalculateColSplitDistributionOfLayer, SpParMat3D.cpp:576-606)."""
+    L = grid.L
+    bounds = [block_range(C.ncol, L, m) for m in range(L)]
     cp_host = C.cp.cpu().numpy()
     col_cnt = torch.diff(C.cp)
-    nnz_split = [int(cp_host[c1 - b0] - cp_host[c0 - b0]) for (c0, c1) in bounds]
+    nnz_split = [int(cp_host[c1] - cp_host[c0]) for (c0, c1) in bounds]
     col_split = [c1 - c0 for (c0, c1) in bounds]
     cd = backend.comm_device
     send_n = torch.tensor(nnz_split, dtype=torch.int64, device=cd)
@@ -256,12 +257,12 @@ def Mult_AnXBn_SUMMA3D(SR, A, B, stats=None):
     a_nnz = _allgather_nnz(A.block, g.row_group, q, be)   # pieces (l, i, k), k = 0..q-1
     b_nnz = _allgather_nnz(B.block, g.col_group, q, be)   # pieces (l, k, j)
     r0, r1 = block_range(A.nrow, q, g.row)
-    c0, c1 = block_range(B.ncol, q, g.col)
+    ncl = B.block.ncol   # local columns of B (= of C): block `col` of B, or a phase piece of it
 
     def issue(k):
         k0, k1 = piece_range(A.ncol, q, L, k, g.layer)
         a = _BlockBcast(A.block, r1 - r0, k1 - k0, a_nnz[k], g.rank_of(g.layer, g.row, k), g.row_group, be, g.rank)
-        b = _BlockBcast(B.block, k1 - k0, c1 - c0, b_nnz[k], g.rank_of(g.layer, k, g.col), g.col_group, be, g.rank)
+        b = _BlockBcast(B.block, k1 - k0, ncl, b_nnz[k], g.rank_of(g.layer, k, g.col), g.col_group, be, g.rank)
         return a, b
 
     partials = []
@@ -277,7 +278,7 @@ def Mult_AnXBn_SUMMA3D(SR, A, B, stats=None):
         partials.append(be.multiply(Ak, Bk, SR, stats))
     C = partials[0] if q == 1 else be.merge(partials, SR)
     if L > 1:
-        C = _fiber_exchange(C, g, B.ncol, be, SR)
+        C = _fiber_exchange(C, g, be, SR)
     return SpParMat3D(g, A.nrow, B.ncol, C, True, be)
 
 
@@ -296,6 +297,152 @@ def PSpGEMM(SR, A, B, stats=None):
 def multiply(SR, A, B, stats=None):
     """3DSpGEMM driver entry (Multiplier.h:10-61): split-3D product on the grid A and B live on."""
     return Mult_AnXBn_SUMMA3D(SR, A, B, stats)
+
+
+# ------------------------------------------------------------------------------ HipMCL expansion
+def _col_slice(b, c0, c1):
+    """Columns [c0, c1) of a Block (one ColSplit piece, SpDCCols.cpp:927-1086)."""
+    e0, e1 = int(b.cp[c0]), int(b.cp[c1])
+    return Block(b.nrow, c1 - c0, b.cp[c0:c1 + 1] - b.cp[c0], b.ir[e0:e1], b.val[e0:e1])
+
+
+def _col_concat(blocks, device):
+    """ColConcatenate (SpDCCols.cpp:1087-1185) of Blocks with equal nrow."""
+    cps, off = [torch.zeros(1, dtype=torch.int64, device=device)], 0
+    for b in blocks:
+        cps.append(b.cp[1:] + off)
+        off += b.nnz
+    return Block(blocks[0].nrow, sum(b.ncol for b in blocks), torch.cat(cps),
+                 torch.cat([b.ir for b in blocks]), torch.cat([b.val for b in blocks]))
+
+
+def _gather_columns(blk, grid, nrow_global, be):
+    """Complete columns for the prune: the q ranks of a processor column (col_group) each hold one
+    row block of the same local columns.  Column group m = block_range(ncol, q, m) goes to column
+    rank m, which stacks the q row blocks (rows offset to global).  Plays the role of the
+    processor-column reductions/gathers inside Reduce(Column) and Kselect1 (SpParMat.cpp:1413-1700)."""
+    q, dev, cd = grid.q, be.device, be.comm_device
+    ncl = blk.ncol
+    groups = [block_range(ncl, q, m) for m in range(q)]
+    cp_h = blk.cp.cpu().numpy()
+    nnz_split = [int(cp_h[g1] - cp_h[g0]) for (g0, g1) in groups]
+    col_split = [g1 - g0 for (g0, g1) in groups]
+    send_n = torch.tensor(nnz_split, dtype=torch.int64, device=cd)
+    recv_n = torch.empty(q, dtype=torch.int64, device=cd)
+    dist.all_to_all_single(recv_n, send_n, group=grid.col_group)
+    recv_nnz = [int(x) for x in recv_n.cpu().tolist()]
+    g0, g1 = groups[grid.row]
+    ng = g1 - g0
+    r_cnt = torch.empty(q * ng, dtype=torch.int64, device=cd)
+    r_ir = torch.empty(sum(recv_nnz), dtype=torch.int32, device=cd)
+    r_val = torch.empty(sum(recv_nnz), dtype=be.val_dtype, device=cd)
+    dist.all_to_all_single(r_cnt, _to_comm(torch.diff(blk.cp), be), [ng] * q, col_split, group=grid.col_group)
+    dist.all_to_all_single(r_ir, _to_comm(blk.ir, be), recv_nnz, nnz_split, group=grid.col_group)
+    dist.all_to_all_single(r_val, _to_comm(blk.val, be), recv_nnz, nnz_split, group=grid.col_group)
+    cnt = _from_comm(r_cnt, be).view(q, ng)
+    r_ir, r_val = _from_comm(r_ir, be), _from_comm(r_val, be)
+    cp = torch.zeros(ng + 1, dtype=torch.int64, device=dev)
+    torch.cumsum(cnt.sum(0), 0, out=cp[1:])
+    before = torch.cumsum(cnt, 0) - cnt             # entries of column c from sources < i
+    out_ir = torch.empty_like(r_ir)
+    out_val = torch.empty_like(r_val)
+    off = 0
+    cols = torch.arange(ng, device=dev)
+    for i in range(q):
+        n_i = recv_nnz[i]
+        if n_i:
+            col = torch.repeat_interleave(cols, cnt[i])
+            scp = torch.zeros(ng + 1, dtype=torch.int64, device=dev)
+            torch.cumsum(cnt[i], 0, out=scp[1:])
+            local = torch.arange(n_i, device=dev) - scp[col]
+            dst = cp[col] + before[i, col] + local
+            r0, _ = block_range(nrow_global, q, i)
+            out_ir[dst] = r_ir[off:off + n_i] + r0
+            out_val[dst] = r_val[off:off + n_i]
+        off += n_i
+    return Block(nrow_global, ng, cp, out_ir, out_val), groups
+
+
+def _scatter_columns(P, grid, groups, nrow_local, be):
+    """Inverse of _gather_columns: row block i of the pruned complete columns goes back to column
+    rank i; each rank concatenates the q column groups of its row block."""
+    q, dev, cd = grid.q, be.device, be.comm_device
+    ng = P.ncol
+    bounds = torch.tensor([block_range(P.nrow, q, i)[0] for i in range(1, q)], dtype=torch.int32, device=dev)
+    col = torch.repeat_interleave(torch.arange(ng, device=dev), torch.diff(P.cp))
+    blk = torch.bucketize(P.ir, bounds, right=True).to(torch.int64)
+    key = blk * ng + col
+    order = torch.argsort(key, stable=True)
+    cnt = torch.bincount(key, minlength=q * ng).view(q, ng)
+    starts = torch.tensor([block_range(P.nrow, q, i)[0] for i in range(q)], dtype=torch.int32, device=dev)
+    s_ir = P.ir[order] - starts[blk[order]]
+    s_val = P.val[order]
+    send_nnz = [int(x) for x in cnt.sum(1).cpu().tolist()]
+    send_n = torch.tensor(send_nnz, dtype=torch.int64, device=cd)
+    recv_n = torch.empty(q, dtype=torch.int64, device=cd)
+    dist.all_to_all_single(recv_n, send_n, group=grid.col_group)
+    recv_nnz = [int(x) for x in recv_n.cpu().tolist()]
+    col_split = [g1 - g0 for (g0, g1) in groups]
+    r_cnt = torch.empty(sum(col_split), dtype=torch.int64, device=cd)
+    r_ir = torch.empty(sum(recv_nnz), dtype=torch.int32, device=cd)
+    r_val = torch.empty(sum(recv_nnz), dtype=be.val_dtype, device=cd)
+    dist.all_to_all_single(r_cnt, _to_comm(cnt.reshape(-1), be), col_split, [ng] * q, group=grid.col_group)
+    dist.all_to_all_single(r_ir, _to_comm(s_ir.to(torch.int32), be), recv_nnz, send_nnz, group=grid.col_group)
+    dist.all_to_all_single(r_val, _to_comm(s_val, be), recv_nnz, send_nnz, group=grid.col_group)
+    cp = torch.zeros(sum(col_split) + 1, dtype=torch.int64, device=dev)
+    torch.cumsum(_from_comm(r_cnt, be), 0, out=cp[1:])
+    return Block(nrow_local, sum(col_split), cp, _from_comm(r_ir, be), _from_comm(r_val, be))
+
+
+def MCLPruneRecoverySelect(A, hardThreshold, selectNum, recoverNum, recoverPct, kselectVersion=1):
+    """Distributed prune/select/recover (ParFriends.h:185-353) of a colsplit SpParMat3D, in place.
+    Columns are completed along the processor column (one all-to-all each way), pruned on device
+    (backend.mcl_prune = cbg_mcl_prune), and returned.  Returns the global branch counts."""
+    g, be = A.grid, A.backend
+    if recoverPct > 1:
+        recoverPct = recoverPct / 100.0
+    if g.q == 1:
+        P, st = be.mcl_prune(A.block, hardThreshold, selectNum, recoverNum, recoverPct)
+        A.block = P
+    else:
+        full, groups = _gather_columns(A.block, g, A.nrow, be)
+        P, st = be.mcl_prune(full, hardThreshold, selectNum, recoverNum, recoverPct)
+        A.block = _scatter_columns(P, g, groups, A.block.nrow, be)
+    t = torch.tensor([st["recovered"], st["selected"], st["recovered_after_select"]], dtype=torch.int64,
+                     device=be.comm_device)
+    dist.all_reduce(t)
+    r = [int(x) for x in t.cpu().tolist()]
+    return {"recovered": r[0], "selected": r[1], "recovered_after_select": r[2]}
+
+
+def MemEfficientSpGEMM(SR, A, B, phases, hardThreshold, selectNum, recoverNum, recoverPct, kselectVersion=1,
+                       computationKernel=1, perProcessMemory=0, stats=None):
+    """HipMCL expansion (ParFriends.h:449-730): B's local columns are cut into `phases` pieces
+    (ColSplit); each phase is a full SUMMA product A * B_p followed by MCLPruneRecoverySelect, and
+    the pruned pieces are concatenated (ColConcatenate).  On a 3D grid (L > 1) the layer exchange
+    would interleave phase pieces, so phases = 1 there (MemEfficientSpGEMM3D's own phasing is not
+    mirrored); the product is phase-count independent either way."""
+    g, be = A.grid, A.backend
+    if A.ncol != B.nrow:
+        raise _abi.CbgError(_abi.EDIM, "MemEfficientSpGEMM")
+    if phases < 1 or phases >= A.ncol or g.L > 1:
+        phases = 1
+    ncl = B.block.ncol
+    pieces = []
+    counts = {"recovered": 0, "selected": 0, "recovered_after_select": 0}
+    for p in range(phases):
+        c0, c1 = block_range(ncl, phases, p)
+        Bp = SpParMat3D(g, B.nrow, B.ncol, _col_slice(B.block, c0, c1) if phases > 1 else B.block, False, be)
+        Cp = Mult_AnXBn_SUMMA3D(SR, A, Bp, stats)
+        st = MCLPruneRecoverySelect(Cp, hardThreshold, selectNum, recoverNum, recoverPct, kselectVersion)
+        for k in counts:
+            counts[k] += st[k]
+        pieces.append(Cp.block)
+    blk = pieces[0] if phases == 1 else _col_concat(pieces, be.device)
+    if stats is not None:
+        stats.update(counts)
+        stats["phases"] = phases
+    return SpParMat3D(g, A.nrow, B.ncol, blk, True, be)
 
 
 # -------------------------------------------------------------------------------------- backends
@@ -401,6 +548,15 @@ class GpuBackend:
         if stats is not None:
             stats["multiplies"] = stats.get("multiplies", 0) + int(m.value)
         return self._take(res)
+
+    def mcl_prune(self, blk, thr, select, recover, pct):
+        res = _abi.CscResult()
+        st = _abi.MclStats()
+        _abi.check(self.ctx._lib.cbg_mcl_prune(self.ctx._ptr, ctypes.byref(self._res_view(blk)), float(thr),
+                                               int(select), int(recover), float(pct), ctypes.byref(res),
+                                               ctypes.byref(st)), "cbg_mcl_prune")
+        return self._take(res, "merge"), {"recovered": st.recovered, "selected": st.selected,
+                                          "recovered_after_select": st.recovered_after_select}
 
     def merge(self, parts, sr):
         arr = (_abi.CscResult * len(parts))(*[self._res_view(p) for p in parts])

@@ -13,8 +13,11 @@
  *                      MultiwayMergeHash<SR>(lists, m, n, delarrs, sorted) include/CombBLAS/MultiwayMerge.h:536-537
  *   cbg_generate_rmat  DistEdgeList::GenGraph500Data + SpParMat(DEL)     include/CombBLAS/DistEdgeList.cpp:223-280,
  *                                                                        include/CombBLAS/SpParMat.cpp:3082-3196
- *   cbg_grid_*         CommGrid / CommGrid3D / ProductGrid (rank layout) src/CommGrid.cpp:37-76,164-180,
- *                                                                        include/CombBLAS/CommGrid3D.h:21-80
+ *   cbg_mcl_prune      MCLPruneRecoverySelect(A, thr, select, recover, pct, kselectVersion)
+ *                                                                        include/CombBLAS/ParFriends.h:185-353
+ *                      (Kselect1 SpParMat.cpp:1413-1700, PruneColumn SpParMat.cpp:2567-2720)
+ *   cbg_col_range      SpDCCols::ColSplit (one piece)                    include/CombBLAS/SpDCCols.cpp:927-1086
+ *   cbg_col_concat     SpDCCols::ColConcatenate                          include/CombBLAS/SpDCCols.cpp:1087-1185
  *
  * Semantics (SURVEY §8a parity rules):
  *   - Output columns are row-sorted and duplicate-free when CBG_SORTED_COLS is set (the reference
@@ -161,6 +164,32 @@ cbg_status cbg_generate_rmat(cbg_ctx* ctx, int32_t scale, int32_t edgefactor, ui
 /* The same matrix built on the host only (no GPU needed). */
 cbg_status cbg_rmat_host(int32_t scale, int32_t edgefactor, uint64_t seed, cbg_host_csc* out);
 void       cbg_host_free(cbg_host_csc* m);
+
+/*
+ * HipMCL expansion support (MemEfficientSpGEMM, ParFriends.h:449-730).
+ *
+ * cbg_mcl_prune: per column of a column-complete local matrix (every row of each column present,
+ * e.g. a 1-rank product or a column-gathered piece), exactly MCLPruneRecoverySelect's rule:
+ *   P = {v > hardThreshold}; recover if |P| < recoverNum && nnz > |P| && sum(P) < recoverPct
+ *   (threshold = recoverNum-th largest); else select if selectNum > 0 && |P| > selectNum
+ *   (threshold = selectNum-th largest, then recovery-after-selection as ParFriends.h:290-333);
+ *   else threshold = hardThreshold.  Entries v < threshold are dropped (PruneColumn with less<>).
+ * k-th largest follows Kselect1: fewer than k entries -> the column minimum.  Values f32/f64.
+ * The output is a new library-owned result (same nrow/ncol); row order within columns is kept.
+ */
+typedef struct {
+  int64_t recovered;               /* columns taking the recovery branch */
+  int64_t selected;                /* columns taking the selection branch */
+  int64_t recovered_after_select;  /* selected columns recovered again */
+  int64_t nnz_in, nnz_out;
+} cbg_mcl_stats;
+
+cbg_status cbg_mcl_prune(cbg_ctx* ctx, const cbg_csc_result* in, double hardThreshold, int64_t selectNum,
+                         int64_t recoverNum, double recoverPct, cbg_csc_result* out, cbg_mcl_stats* stats);
+/* Columns [c0, c1) of a device CSC as a new result (colptr rebased).  c out of range -> CBG_EDIM. */
+cbg_status cbg_col_range(cbg_ctx* ctx, const cbg_csc_result* in, int64_t c0, int64_t c1, cbg_csc_result* out);
+/* Horizontal concatenation of nparts device CSCs with equal nrow/val_type. */
+cbg_status cbg_col_concat(cbg_ctx* ctx, const cbg_csc_result* parts, int32_t nparts, cbg_csc_result* out);
 
 #ifdef __cplusplus
 }

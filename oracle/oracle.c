@@ -24,6 +24,11 @@
  *                    include/CombBLAS/PBBS/radixSort.h:116-120).
  *   orc_merge        MultiwayMerge              include/CombBLAS/MultiwayMerge.h:411-526
  *                    (duplicates combined with SR::add in list order).
+ *   orc_mcl_prune    MCLPruneRecoverySelect     include/CombBLAS/ParFriends.h:185-353 on one
+ *                    rank (column statistics of Prune(less_equal thr) in storage order,
+ *                    Kselect1 SpParMat.cpp:1413-1700: sort descending, k-th item, fewer than
+ *                    k -> last item, empty -> numeric_limits<double>::min(); final PruneColumn
+ *                    SpParMat.cpp:2567-2720 drops v < threshold).
  * Semirings restate include/CombBLAS/Semirings.h:
  *   PLUS_TIMES 212-233, MIN_PLUS 235-255 (inf_plus 40-47), SELECT2ND 143-163,
  *   SELECT_MAX 165-190, SELECT_MAX_BOOL (SelectMaxSRing<bool,T>) 191-210,
@@ -333,3 +338,70 @@ int orc_merge(int sr, int dt, int nlists, const orc_csc* lists, int64_t* cp_out,
 }
 
 void orc_free(void* p) { free(p); }
+
+/* ------------------------------------------------------------------ MCLPruneRecoverySelect */
+static int cmp_desc(const void* a, const void* b) {
+  const double x = *(const double*)a, y = *(const double*)b;
+  return (x < y) - (x > y);
+}
+
+/* Kselect1 on one column (SpParMat.cpp:1536-1548 partial_sort greater<>, :1660-1668 pick) */
+static double kth_largest(const double* v, int64_t n, int64_t k, double* scratch) {
+  if (n == 0) return DBL_MIN;
+  memcpy(scratch, v, sizeof(double) * (size_t)n);
+  qsort(scratch, (size_t)n, sizeof(double), cmp_desc);
+  return n >= k ? scratch[k - 1] : scratch[n - 1];
+}
+
+/* in: f64 CSC (column-complete).  out arrays: cp_out[ncol+1]; ir_out, val_out malloc'd.
+   stats[0..2] = recovered, selected, recovered after selection. */
+int orc_mcl_prune(const orc_csc* A, double thr, int64_t S, int64_t R, double pct, int64_t* cp_out,
+                  int32_t** ir_out, double** val_out, int64_t* stats) {
+  const double* val = (const double*)A->val;
+  double* th = (double*)malloc(sizeof(double) * (size_t)(A->ncol + 1));
+  double* scratch = (double*)malloc(sizeof(double) * (size_t)(A->nnz + 1));
+  if (!th || !scratch) { free(th); free(scratch); return ORC_ENOMEM; }
+  stats[0] = stats[1] = stats[2] = 0;
+  for (int64_t j = 0; j < A->ncol; ++j) {
+    const int64_t a = A->cp[j], b = A->cp[j + 1], nu = b - a;
+    int64_t np = 0;
+    double sp = 0.0;
+    for (int64_t k = a; k < b; ++k)
+      if (!(val[k] <= thr)) { ++np; sp += val[k]; }   /* Prune(bind2nd(less_equal, thr)) keeps v > thr */
+    th[j] = thr;
+    if (np < R && nu > np && sp < pct) {              /* ParFriends.h:207-233 */
+      th[j] = kth_largest(val + a, nu, R, scratch);
+      stats[0]++;
+    } else if (S > 0 && np > S) {                     /* ParFriends.h:251-267 */
+      const double t = kth_largest(val + a, nu, S, scratch);
+      th[j] = t;
+      stats[1]++;
+      if (R > 0) {                                    /* ParFriends.h:290-333 */
+        int64_t n1 = 0;
+        double s1 = 0.0;
+        for (int64_t k = a; k < b; ++k)
+          if (!(val[k] < t)) { ++n1; s1 += val[k]; }
+        if (n1 < R && s1 < pct) { th[j] = kth_largest(val + a, nu, R, scratch); stats[2]++; }
+      }
+    }
+  }
+  cp_out[0] = 0;
+  for (int64_t j = 0; j < A->ncol; ++j) {
+    int64_t c = 0;
+    for (int64_t k = A->cp[j]; k < A->cp[j + 1]; ++k) c += !(val[k] < th[j]);
+    cp_out[j + 1] = cp_out[j] + c;
+  }
+  const int64_t nnz = cp_out[A->ncol];
+  int32_t* ir = (int32_t*)malloc(sizeof(int32_t) * (size_t)(nnz + 1));
+  double* v = (double*)malloc(sizeof(double) * (size_t)(nnz + 1));
+  if (!ir || !v) { free(ir); free(v); free(th); free(scratch); return ORC_ENOMEM; }
+  int64_t o = 0;
+  for (int64_t j = 0; j < A->ncol; ++j)
+    for (int64_t k = A->cp[j]; k < A->cp[j + 1]; ++k)
+      if (!(val[k] < th[j])) { ir[o] = A->ir[k]; v[o] = val[k]; ++o; }
+  *ir_out = ir;
+  *val_out = v;
+  free(th);
+  free(scratch);
+  return ORC_OK;
+}

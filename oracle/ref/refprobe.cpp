@@ -12,6 +12,8 @@
 //   Mult_AnXBn_Synch include/CombBLAS/ParFriends.h:1004-1108
 //   DistEdgeList::GenGraph500Data include/CombBLAS/DistEdgeList.cpp:223-280
 //   SpParMat::ParallelReadMM include/CombBLAS/SpParMat.cpp:3922
+//   MCLPruneRecoverySelect include/CombBLAS/ParFriends.h:185-353 (kselectVersion 1)
+//   MemEfficientSpGEMM include/CombBLAS/ParFriends.h:449-730 (hash kernel, phases)
 // Because of the reference's integerSort off-by-one every product is
 // re-sorted column-major with SpTuples::SortColBased before it is written, so
 // fixtures hold the mathematically defined product (rows ascending per column).
@@ -175,6 +177,31 @@ static int run_readmm(const char* mtx, const char* out) {
   return 0;
 }
 
+// HipMCL prune/select/recover on a 1-rank SpParMat (ParFriends.h:185-353), in place.
+static int run_mcl(const char* fa, double thr, long sel, long rec, double pct, const char* out) {
+  typedef SpDCCols<I, double> DCC; typedef SpParMat<I, double, DCC> PM;
+  RawCsc RA = read_bin(fa);
+  std::shared_ptr<CommGrid> g(new CommGrid(MPI_COMM_WORLD, 0, 0));
+  PM A(to_dcc<double>(RA), g);
+  MCLPruneRecoverySelect(A, thr, (I)sel, (I)rec, pct, 1);
+  write_dcc<double>(out, *A.seqptr());
+  printf("{\"mcl\":1,\"nnz\":%ld}\n", (long)A.getnnz());
+  return 0;
+}
+
+// HipMCL expansion A*A in `phases` column phases with prune after each (ParFriends.h:449-730).
+static int run_memeff(const char* fa, int phases, double thr, long sel, long rec, double pct, const char* out) {
+  typedef SpDCCols<I, double> DCC; typedef SpParMat<I, double, DCC> PM;
+  typedef PlusTimesSRing<double, double> PTFF;
+  RawCsc RA = read_bin(fa);
+  std::shared_ptr<CommGrid> g(new CommGrid(MPI_COMM_WORLD, 0, 0));
+  PM A(to_dcc<double>(RA), g), B(to_dcc<double>(RA), g);
+  PM C = MemEfficientSpGEMM<PTFF, double, DCC>(A, B, phases, thr, (I)sel, (I)rec, pct, 1, 1, 0);
+  write_dcc<double>(out, *C.seqptr());
+  printf("{\"memeff\":%d,\"nnz\":%ld}\n", phases, (long)C.getnnz());
+  return 0;
+}
+
 int main(int argc, char** argv) {
   int prov; MPI_Init_thread(&argc, &argv, MPI_THREAD_SERIALIZED, &prov);
   int rc = 2;
@@ -184,9 +211,13 @@ int main(int argc, char** argv) {
     else if (cmd == "synch" && argc == 5) rc = run_synch(argv[2], argv[3], argv[4]);
     else if (cmd == "gen" && argc == 5) rc = run_gen(atoi(argv[2]), atoi(argv[3]), argv[4]);
     else if (cmd == "readmm" && argc == 4) rc = run_readmm(argv[2], argv[3]);
+    else if (cmd == "mcl" && argc == 8)
+      rc = run_mcl(argv[2], atof(argv[3]), atol(argv[4]), atol(argv[5]), atof(argv[6]), argv[7]);
+    else if (cmd == "memeff" && argc == 9)
+      rc = run_memeff(argv[2], atoi(argv[3]), atof(argv[4]), atol(argv[5]), atol(argv[6]), atof(argv[7]), argv[8]);
   }
   if (rc == 2 && argc < 3)
-    fprintf(stderr, "usage: refprobe mult <sr> <hash|hash_unsorted|heap|hybrid> A.bin B.bin C.bin | synch A B C | gen scale ef out | readmm in.mtx out\n");
+    fprintf(stderr, "usage: refprobe mult <sr> <hash|hash_unsorted|heap|hybrid> A.bin B.bin C.bin | synch A B C | gen scale ef out | readmm in.mtx out | mcl A thr sel rec pct out | memeff A phases thr sel rec pct out\n");
   MPI_Finalize();
   return rc;
 }

@@ -49,6 +49,13 @@ class ScipyBackend:
             stats["multiplies"] = stats.get("multiplies", 0) + m
         return self._block(P, A.val.numpy().dtype)
 
+    def mcl_prune(self, blk, thr, select, recover, pct):
+        from helpers import Csc, oracle_mcl_prune
+        P, st = oracle_mcl_prune(Csc(blk.nrow, blk.ncol, blk.cp.numpy(), blk.ir.numpy(), blk.val.numpy()),
+                                 thr, select, recover, pct)
+        return (Block(blk.nrow, blk.ncol, torch.as_tensor(P.cp), torch.as_tensor(P.ir), torch.as_tensor(P.val)),
+                {"recovered": st[0], "selected": st[1], "recovered_after_select": st[2]})
+
     def merge(self, parts, sr):
         S = self._csc(parts[0])
         for p in parts[1:]:
@@ -110,16 +117,59 @@ def run_dist_case(rank, world, port, backend_kind, cases, errq):
         raise
 
 
+def run_mcl_case(rank, world, port, backend_kind, cases, errq):
+    """Per-rank body of the distributed HipMCL expansion (MemEfficientSpGEMM + prune): every rank
+    checks its piece against the oracle's prune of the global product (complete columns)."""
+    try:
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        L, q, _ = cbd.grid_for(world)
+        grid = cbd.CommGrid3D(L, q, q)
+        if backend_kind == "scipy":
+            be = ScipyBackend()
+        else:
+            import combblas_amd as cb
+            be = cbd.GpuBackend(cb.Context(0))
+        from combblas_amd.inputs import protein_like_graph
+        from helpers import Csc, oracle_mcl_prune
+        for (n, seed, phases, params) in cases:
+            n, cp, ir, val = protein_like_graph(n, seed=seed, cmin=10, cmax=120, density=0.25, noise=1e-3)
+            Ad = cbd.SpParMat3D.from_global_csc(grid, n, n, cp, ir, val, True, be)
+            Bd = cbd.SpParMat3D.from_global_csc(grid, n, n, cp, ir, val, False, be)
+            stats = {}
+            C = cbd.MemEfficientSpGEMM(cb_sr(backend_kind), Ad, Bd, phases, *params, stats=stats)
+            A = sp.csc_matrix((val, ir, cp), shape=(n, n))
+            G = (A @ A).tocsc()
+            G.sort_indices()
+            O, ost = oracle_mcl_prune(Csc(n, n, G.indptr, G.indices, G.data), *params)
+            R = sp.csc_matrix((O.val, O.ir, O.cp), shape=(n, n))
+            (r0, r1), (c0, c1) = C.local_range()
+            Rl = R[r0:r1, c0:c1].tocsc()
+            Rl.sort_indices()
+            blk = C.block
+            assert np.array_equal(blk.cp.cpu().numpy(), Rl.indptr), f"rank {rank}: colptr differs"
+            assert np.array_equal(blk.ir.cpu().numpy(), Rl.indices), f"rank {rank}: rows differ"
+            assert np.allclose(blk.val.cpu().numpy(), Rl.data, rtol=1e-12, atol=0), f"rank {rank}: values"
+            assert (stats["recovered"], stats["selected"], stats["recovered_after_select"]) == ost, (stats, ost)
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:
+        import traceback
+        errq.put(f"rank {rank}: {e!r}\n{traceback.format_exc()}")
+        raise
+
+
 def cb_sr(kind):
     import combblas_amd as cb
     return cb.PlusTimesSRing("f64")
 
 
-def spawn_case(world, backend_kind, cases, port):
+def spawn_case(world, backend_kind, cases, port, body=None):
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     errq = ctx.SimpleQueue()
-    procs = [ctx.Process(target=run_dist_case, args=(r, world, port, backend_kind, cases, errq)) for r in range(world)]
+    procs = [ctx.Process(target=body or run_dist_case, args=(r, world, port, backend_kind, cases, errq)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:

@@ -179,3 +179,25 @@ def sorted_dedup_ok(C):
         if len(seg) > 1 and not np.all(seg[1:] > seg[:-1]):
             return False
     return True
+
+
+def oracle_mcl_prune(A, thr, select, recover, pct):
+    """orc_mcl_prune (MCLPruneRecoverySelect restated): returns (Csc, (recovered, selected, rec2))."""
+    lib = oracle_lib()
+    keep = []
+    va = _orc_view(A, keep)
+    cp = np.zeros(A.ncol + 1, np.int64)
+    ir_p, val_p = ctypes.c_void_p(), ctypes.c_void_p()
+    st = np.zeros(3, np.int64)
+    lib.orc_mcl_prune.argtypes = [ctypes.c_void_p, ctypes.c_double, ctypes.c_int64, ctypes.c_int64,
+                                  ctypes.c_double, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                  ctypes.c_void_p]
+    rc = lib.orc_mcl_prune(ctypes.byref(va), thr, select, recover, pct, cp.ctypes.data,
+                           ctypes.byref(ir_p), ctypes.byref(val_p), st.ctypes.data)
+    assert rc == 0
+    n = int(cp[-1])
+    ir = np.ctypeslib.as_array(ctypes.cast(ir_p, ctypes.POINTER(ctypes.c_int32)), (max(n, 1),))[:n].copy()
+    val = np.frombuffer(ctypes.string_at(val_p, n * 8), np.float64).copy()
+    lib.orc_free(ir_p)
+    lib.orc_free(val_p)
+    return Csc(A.nrow, A.ncol, cp, ir, val), tuple(int(x) for x in st)

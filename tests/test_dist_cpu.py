@@ -15,3 +15,12 @@ CASES = [(60, 50, 40, 0.08, 0.1, 3), (33, 17, 29, 0.2, 0.15, 5), (7, 5, 9, 0.3, 
 @pytest.mark.parametrize("world,port", [(2, 29611), (4, 29612), (8, 29613)])
 def test_summa_layouts_gloo_cpu(world, port):
     spawn_case(world, "scipy", CASES, port)
+
+
+MCL_CASES = [(300, 3, 1, (1e-3, 8, 12, 0.9)), (257, 4, 3, (1e-3, 8, 12, 0.9)), (200, 5, 2, (0.05, 5, 9, 0.99))]
+
+
+@pytest.mark.parametrize("world,port", [(2, 29614), (4, 29615), (8, 29616)])
+def test_mcl_expansion_gloo_cpu(world, port):
+    from dist_support import run_mcl_case
+    spawn_case(world, "scipy", MCL_CASES, port, body=run_mcl_case)

@@ -13,3 +13,12 @@ CASES = [(300, 280, 260, 0.03, 0.03, 21), (33, 17, 29, 0.2, 0.15, 5), (5, 64, 6,
 @pytest.mark.parametrize("world,port", [(2, 29621), (4, 29622), (8, 29623)])
 def test_summa_layouts_gloo_gpu(world, port):
     spawn_case(world, "gpu", CASES, port)
+
+
+MCL_CASES = [(600, 3, 1, (1e-3, 8, 12, 0.9)), (513, 4, 3, (1e-3, 8, 12, 0.9)), (400, 5, 2, (0.05, 5, 9, 0.99))]
+
+
+@pytest.mark.parametrize("world,port", [(2, 29624), (4, 29625), (8, 29626)])
+def test_mcl_expansion_gloo_gpu(world, port):
+    from dist_support import run_mcl_case
+    spawn_case(world, "gpu", MCL_CASES, port, body=run_mcl_case)

@@ -1,0 +1,177 @@
+"""GPU parity of the HipMCL expansion (BASELINE config 4) and the Galerkin triple product (config 5).
+
+cbg_mcl_prune / MemEfficientSpGEMM / cbg_col_range / cbg_col_concat through the C ABI against
+  * the reference's own outputs (tests/golden/mcl.npz, galerkin.npz; oracle/_ref/refprobe), and
+  * the oracle's MCLPruneRecoverySelect restatement on larger seeded graphs.
+Bars: structure exact; pruned values are the product's values (PlusTimes<double>: <= 1e-12 rel).
+The prune itself is checked bit-exact by feeding the oracle the GPU's own product.
+"""
+import numpy as np
+import pytest
+
+import combblas_amd as cb
+from combblas_amd import mcl as cmcl
+from combblas_amd.inputs import aggregation_restriction, poisson3d, protein_like_graph
+from helpers import Csc, assert_same_product, load_fixture, oracle_mcl_prune, oracle_spgemm
+
+pytestmark = pytest.mark.gpu
+PT = cb.PlusTimesSRing("f64")
+
+
+def up(ctx, M, dtype=None):
+    return cb.SpDCCols.from_csc(ctx, M.nrow, M.ncol, M.cp, M.ir, M.val, dtype=dtype)
+
+
+def host(M, nrow):
+    cp, ir, val = M.to_host()
+    return Csc(nrow, len(cp) - 1, cp, ir, val)
+
+
+def mcl_fixture():
+    z = load_fixture("mcl")
+    n = int(z["A_shape"][0])
+    return z, Csc(n, n, z["A_cp"], z["A_ir"], z["A_val"])
+
+
+@pytest.mark.parametrize("i", [0, 1, 2])
+def test_prune_matches_reference(gpu_ctx, i):
+    z, A = mcl_fixture()
+    thr, sel, rec, pct = (float(x) for x in z[f"P{i}_params"])
+    dA = up(gpu_ctx, A)
+    C = cb.LocalSpGEMMHash(PT, dA, dA)
+    Ch = host(C, A.nrow)
+    st = cb.MCLPruneRecoverySelect(C, thr, int(sel), int(rec), pct)
+    P = host(C, A.nrow)
+    R = Csc(A.nrow, A.ncol, z[f"P{i}_cp"], z[f"P{i}_ir"], z[f"P{i}_val"])
+    assert_same_product(P, R, "f64", what=f"P{i} vs reference")
+    O, ost = oracle_mcl_prune(Ch, thr, int(sel), int(rec), pct)
+    assert_same_product(P, O, "f64", rtol=0.0, what=f"P{i} vs oracle")
+    assert (st["recovered"], st["selected"], st["recovered_after_select"]) == ost
+
+
+@pytest.mark.parametrize("ph", [1, 3])
+def test_memeff_matches_reference(gpu_ctx, ph):
+    z, A = mcl_fixture()
+    thr, sel, rec, pct = (float(x) for x in z["P1_params"])
+    dA = up(gpu_ctx, A)
+    stats = {}
+    C = cb.MemEfficientSpGEMM(PT, dA, dA, ph, thr, int(sel), int(rec), pct, stats=stats)
+    assert stats["phases"] == ph and stats["multiplies"] == int(z["C2_flops"])
+    R = Csc(A.nrow, A.ncol, z[f"M{ph}_cp"], z[f"M{ph}_ir"], z[f"M{ph}_val"])
+    assert_same_product(host(C, A.nrow), R, "f64", what=f"memeff phases={ph}")
+
+
+@pytest.mark.parametrize("n,seed,params", [
+    (20000, 11, (1e-4, 1100, 1400, 0.9)),     # MCL defaults
+    (20000, 12, (1e-3, 50, 80, 0.9)),         # selection-heavy
+    (8000, 13, (0.05, 20, 40, 0.99)),         # recovery-heavy
+])
+def test_prune_matches_oracle_large(gpu_ctx, n, seed, params):
+    thr, sel, rec, pct = params
+    n, cp, ir, val = protein_like_graph(n, seed=seed, cmin=20, cmax=600, density=0.2, noise=1e-5)
+    A = Csc(n, n, cp, ir, val)
+    dA = up(gpu_ctx, A)
+    C = cb.LocalSpGEMMHash(PT, dA, dA)
+    Ch = host(C, n)
+    st = cb.MCLPruneRecoverySelect(C, thr, sel, rec, pct)
+    O, ost = oracle_mcl_prune(Ch, thr, sel, rec, pct)
+    assert_same_product(host(C, n), O, "f64", rtol=0.0, what="prune vs oracle")
+    assert (st["recovered"], st["selected"], st["recovered_after_select"]) == ost
+
+
+def test_memeff_phases_large(gpu_ctx):
+    n, cp, ir, val = protein_like_graph(30000, seed=5, cmin=20, cmax=800)
+    A = Csc(n, n, cp, ir, val)
+    dA = up(gpu_ctx, A)
+    outs = []
+    for ph in (1, 4, 7):
+        C = cb.MemEfficientSpGEMM(PT, dA, dA, ph, 1e-3, 60, 90, 0.9)
+        outs.append(host(C, n))
+    for o in outs[1:]:   # pruning is per column, so the phase count cannot change the result
+        assert np.array_equal(o.cp, outs[0].cp) and np.array_equal(o.ir, outs[0].ir)
+        assert np.array_equal(o.val, outs[0].val)
+
+
+def test_prune_edge_cases(gpu_ctx):
+    # columns: empty; all <= thr (recovery -> keep all); fewer than select; ties at the k-th value;
+    # negative values; an entry exactly equal to thr (kept by the final PruneColumn, v < thr drops)
+    cols = [[], [0.001, 0.002], [0.5, 0.4], [0.3, 0.3, 0.3, 0.3, 0.1], [-1.0, 2.0, 0.5, 0.25], [0.01, 0.5, 0.49]]
+    cp = np.cumsum([0] + [len(c) for c in cols]).astype(np.int64)
+    ir = np.concatenate([np.arange(len(c)) for c in cols]).astype(np.int32)
+    val = np.concatenate([np.array(c, np.float64) for c in cols])
+    M = Csc(8, len(cols), cp, ir, val)
+    for params in [(0.01, 2, 3, 0.9), (0.01, 0, 0, 0.9), (0.3, 1, 0, 0.5), (1e-4, 3, 5, 0.99)]:
+        D = up(gpu_ctx, M)
+        st = cb.MCLPruneRecoverySelect(D, *params)
+        O, ost = oracle_mcl_prune(M, *params)
+        assert_same_product(host(D, 8), O, "f64", rtol=0.0, what=f"edge {params}")
+        assert (st["recovered"], st["selected"], st["recovered_after_select"]) == ost
+
+
+def test_prune_f32_and_empty(gpu_ctx):
+    n, cp, ir, val = protein_like_graph(3000, seed=2, cmax=200)
+    A32 = Csc(n, n, cp, ir, val.astype(np.float32))
+    D = up(gpu_ctx, A32)
+    C = cb.LocalSpGEMMHash(cb.PlusTimesSRing("f32"), D, D)
+    cp2, ir2, v2 = C.to_host()
+    W = Csc(n, n, cp2, ir2, v2.astype(np.float64))   # f32 values widened exactly
+    # rules that involve no float sums (pure threshold; selection without recovery) are exact in f32
+    for (thr, sel, rec) in ((1e-3, 0, 0), (1e-3, 30, 0)):
+        D2 = cb.SpDCCols._from_result(gpu_ctx, cmcl._col_range(gpu_ctx, C._res, 0, n))
+        cb.MCLPruneRecoverySelect(D2, thr, sel, rec, 0.9)
+        cp3, ir3, v3 = D2.to_host()
+        O, _ = oracle_mcl_prune(W, float(np.float32(thr)), sel, rec, 0.9)
+        assert np.array_equal(cp3, O.cp) and np.array_equal(ir3, O.ir)
+        assert np.array_equal(v3.astype(np.float64), O.val)
+    E = up(gpu_ctx, Csc(5, 4, np.zeros(5, np.int64), np.zeros(0, np.int32), np.zeros(0)))
+    st = cb.MCLPruneRecoverySelect(E, 1e-4, 10, 20, 0.9)
+    assert E.getnnz() == 0 and st["nnz_out"] == 0
+
+
+def test_col_range_concat_roundtrip(gpu_ctx):
+    n, cp, ir, val = protein_like_graph(2000, seed=4, cmax=100)
+    D = up(gpu_ctx, Csc(n, n, cp, ir, val))
+    ranges = cmcl.phase_ranges(n, 7)
+    parts = [cmcl._col_range(gpu_ctx, D._res, c0, c1) for (c0, c1) in ranges]
+    for (c0, c1), p in zip(ranges, parts):
+        assert p.ncol == c1 - c0 and p.nnz == cp[c1] - cp[c0]
+    out = cmcl._col_concat(gpu_ctx, parts)
+    for p in parts:
+        gpu_ctx._lib.cbg_result_free(gpu_ctx._ptr, __import__("ctypes").byref(p))
+    R = cb.SpDCCols._from_result(gpu_ctx, out)
+    cp2, ir2, v2 = R.to_host()
+    assert np.array_equal(cp2, cp) and np.array_equal(ir2, ir) and np.array_equal(v2, val)
+    with pytest.raises(cb.CbgError):
+        cmcl._col_range(gpu_ctx, D._res, 5, n + 1)
+
+
+def _transpose(M):
+    import scipy.sparse as sp
+    T = sp.csc_matrix((M.val, M.ir, M.cp), shape=(M.nrow, M.ncol)).T.tocsc()
+    T.sort_indices()
+    return Csc(M.ncol, M.nrow, T.indptr, T.indices, T.data)
+
+
+def test_galerkin_matches_reference(gpu_ctx):
+    z = load_fixture("galerkin")
+    n, nagg = (int(x) for x in z["R_shape"])
+    A = Csc(n, n, z["A_cp"], z["A_ir"], z["A_val"])
+    R = Csc(n, nagg, z["R_cp"], z["R_ir"], z["R_val"])
+    RA = cb.LocalSpGEMMHash(PT, up(gpu_ctx, _transpose(R)), up(gpu_ctx, A))
+    C = cb.LocalSpGEMMHash(PT, RA, up(gpu_ctx, R))
+    assert (RA.multiplies, C.multiplies) == (int(z["RA_flops"]), int(z["C_flops"]))
+    assert_same_product(host(C, nagg), Csc(nagg, nagg, z["C_cp"], z["C_ir"], z["C_val"]), "f64", what="RtAR")
+
+
+def test_galerkin_large_vs_oracle(gpu_ctx):
+    n, acp, air, aval = poisson3d(24)
+    nagg, rcp, rir, rval = aggregation_restriction(n, acp, air, seed=9)
+    A, R = Csc(n, n, acp, air, aval), Csc(n, nagg, rcp, rir, rval)
+    Rt = _transpose(R)
+    RA = cb.LocalSpGEMMHash(PT, up(gpu_ctx, Rt), up(gpu_ctx, A))
+    RAh = host(RA, nagg)
+    C = cb.LocalSpGEMMHash(PT, RA, up(gpu_ctx, R))
+    ORA, _, _ = oracle_spgemm(Rt, A, "plus_times", "f64")
+    OC, _, _ = oracle_spgemm(ORA, R, "plus_times", "f64")
+    assert_same_product(RAh, ORA, "f64", what="RtA")   # small integer sums: exact in f64
+    assert_same_product(host(C, nagg), OC, "f64", what="RtAR")
