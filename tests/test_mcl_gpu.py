@@ -89,7 +89,8 @@ def test_memeff_phases_large(gpu_ctx):
         outs.append(host(C, n))
     for o in outs[1:]:   # pruning is per column, so the phase count cannot change the result
         assert np.array_equal(o.cp, outs[0].cp) and np.array_equal(o.ir, outs[0].ir)
-        assert np.array_equal(o.val, outs[0].val)
+        # LDS atomic accumulation makes f64 sums order-dependent: values agree to the 1e-12 bar
+        assert np.allclose(o.val, outs[0].val, rtol=1e-12, atol=0)
 
 
 def test_prune_edge_cases(gpu_ctx):
