@@ -7,7 +7,7 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libcbgpu.so")
+LIB_PATH = os.environ.get("CBG_LIB_PATH") or os.path.join(_HERE, "libcbgpu.so")   # override: tuning variants
 
 # cbg_status
 OK, EDIM, EALIAS, ENOMEM, EUNSUP, EDEVICE, EADD, EINVAL, ECOMM = 0, 3002, 3005, 10, 11, 12, 13, 14, 15

@@ -371,6 +371,9 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
   if ((s = stage<V>(ctx, Bv, ctx->stageB, &B)) != CBG_OK) return s;
 
   // subwindow geometry of the row space (heavy-column units)
+  // SUBW >= 2^13: k_sym_part's per-part subwindow counters assume it, and a single-subwindow unit
+  // must fit k_num_heavy's dense table (2^CBG_HEAVY_LOGT rows)
+  static_assert(CBG_HEAVY_LOGT >= 13, "k_num_heavy table must cover a 2^13-row subwindow");
   int32_t slog = 13;
   while (((M - 1) >> slog) + 1 > kMaxSub) ++slog;
   const int32_t nsub = (int32_t)(((M - 1) >> slog) + 1);
@@ -560,7 +563,7 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
     if (e == hipSuccess && H > 0) {
       NumOut<V> ou{own->ir.as<int32_t>(), own->val.as<V>(), adderr, uovf_n, ctx->uovf_list.as<int32_t>()};
       HIPCHK(hipEventRecord(ctx->ev[6], st));
-      e = launch_num_heavy<13, 1024, SRT, V>(st, nitems, ctx->items.as<HeavyItem>(), ctx->heavy_cols.as<int32_t>(),
+      e = launch_num_heavy<CBG_HEAVY_LOGT, CBG_HEAVY_NT, SRT, V>(st, nitems, ctx->items.as<HeavyItem>(), ctx->heavy_cols.as<int32_t>(),
                                              units, nsub, A, B, span, spl, ou);
       HIPCHK(hipEventRecord(ctx->ev[7], st));
       // overflowed hash units -> single-subwindow (dense) units

@@ -42,15 +42,34 @@ constexpr int32_t kEmpty = -1;
 constexpr int kLong = 64;          // k_window: segment length handed to a whole wavefront
 constexpr int kUnroll = 2;         // groups of G multiplies in flight per lane (numeric)
 constexpr int kUnrollSym = 2;      // same, symbolic (4-byte items)
-constexpr int kUnrollHeavy = 2;    // same, k_num_heavy
+#ifndef CBG_UNROLL_HEAVY
+#define CBG_UNROLL_HEAVY 2
+#endif
+#ifndef CBG_GROUP_HEAVY
+#define CBG_GROUP_HEAVY 2
+#endif
+constexpr int kUnrollHeavy = CBG_UNROLL_HEAVY;    // same, k_num_heavy
 constexpr int kGroupSym = 4;       // consecutive A entries per lane group (one segment search each), symbolic
 constexpr int kGroupNum = 2;       // same, numeric
-constexpr int kGroupHeavy = 2;     // same, k_num_heavy
+constexpr int kGroupHeavy = CBG_GROUP_HEAVY;     // same, k_num_heavy
 constexpr int64_t kHeavy = 4096;   // nnz(C(:,j)) above which a column is split into units
-constexpr int64_t kUnitCap = 4096; // max outputs of a multi-subwindow unit (k_num_heavy T = 8192, load <= 0.5)
+// k_num_heavy geometry: table 2^CBG_HEAVY_LOGT slots, CBG_HEAVY_NT threads (LDS decides WGs per CU)
+#ifndef CBG_HEAVY_LOGT
+#define CBG_HEAVY_LOGT 13
+#endif
+#ifndef CBG_HEAVY_NT
+#define CBG_HEAVY_NT 1024
+#endif
+#ifndef CBG_ITEM_UNITS
+#define CBG_ITEM_UNITS 8
+#endif
+#ifndef CBG_UNIT_CAP
+#define CBG_UNIT_CAP (1 << (CBG_HEAVY_LOGT - 1))
+#endif
+constexpr int64_t kUnitCap = CBG_UNIT_CAP;   // max outputs of a multi-subwindow unit (load <= kUnitCap/T)
 constexpr int kSplitMin = 16;      // A columns at least this long get split-table rows
 constexpr int kMaxSub = 2048;      // max subwindows per column (SUBW chosen so nrow/SUBW <= kMaxSub)
-constexpr int kItemUnits = 8;      // units of one heavy column per workgroup item (k_num_heavy)
+constexpr int kItemUnits = CBG_ITEM_UNITS; // units of one heavy column per workgroup item (k_num_heavy)
 
 template <typename V>
 struct DevCsc {

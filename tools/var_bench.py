@@ -27,7 +27,7 @@ if __name__ == "__main__":
         if r.returncode == 0:
             import json
             j = json.loads(line)
-            print(n, "ms/step %.2f" % j["ms_per_step"], j.get("phases_ms"), flush=True)
+            print(n, "ms/step %.2f" % j["ms_per_step"], "nnz_C", j["config"].get("nnz_C"), j.get("phases_ms"), flush=True)
         else:
             print(n, "rc", r.returncode, r.stderr[-2000:], flush=True)
         if r.returncode != 0:
