@@ -7,10 +7,10 @@
   product (config 5; 3DSpGEMM/RestrictionOp.cpp drives R^T A R).
 * aggregation_restriction: the restriction operator R (n x nagg, one 1 per row) of a distance-2
   maximal-independent-set aggregation (RestrictionOp.h:116-427: MIS-2 roots, every vertex joins the
-  aggregate of a root within distance 2).  Our MIS-2 is a deterministic greedy pass over a seeded
-  random vertex order; the reference's distributed MIS-2 uses its own random priorities, so R is a
+  aggregate of a root within distance 2).  Our MIS-2 runs Luby-style rounds on seeded random
+  priorities (vectorised); the reference's distributed MIS-2 draws its own priorities, so R is a
   valid aggregation of the same kind, not the reference's bit pattern (config 5 parity is about the
-  R^T A R product, checked against the oracle on identical R).
+  R^T A R product, checked against the reference and the oracle on identical R).
 All return host CSC arrays (int64 colptr, int32 rows, float64 values).
 """
 import numpy as np
@@ -86,37 +86,47 @@ def poisson3d(k):
 
 
 def aggregation_restriction(n, cp, ir, seed=1):
-    """(nagg, colptr, rows, vals) of R (n x nagg): MIS-2 aggregation of the graph of a symmetric
-    CSC (RestrictionOp.h:116-427 shape).  R[i, agg(i)] = 1."""
+    """(nagg, colptr, rows, vals) of R (n x nagg): MIS-2 aggregation of the graph of a symmetric CSC,
+    the shape RestrictionOp.h:116-427 builds.  Vectorised Luby-style rounds: an undecided vertex
+    whose random priority is the largest among the undecided vertices within distance 2 becomes a
+    root, and its distance-2 neighbourhood is decided; then every vertex joins the highest-priority
+    root within distance 1, else within distance 2.  R[i, agg(i)] = 1."""
     import scipy.sparse as sp
-    G = sp.csc_matrix((np.ones(len(ir)), ir, cp), shape=(n, n))
-    G2 = (G @ G).tocsr()        # distance <= 2 neighbourhoods
+    G = sp.csr_matrix((np.ones(len(ir)), ir, cp), shape=(n, n))
+    G = G + sp.identity(n, format="csr")
+    G2 = (G @ G).tocsr()
+    G.sort_indices()
     G2.sort_indices()
     rng = np.random.default_rng(seed)
-    order = rng.permutation(n)
+    prio = rng.permutation(n).astype(np.int64) + 1      # distinct priorities
+    state = np.zeros(n, np.int8)                        # 0 undecided, 1 root, 2 covered
+
+    def rowmax(M, v):
+        out = np.zeros(M.shape[0], np.int64)
+        nz = np.diff(M.indptr) > 0
+        if M.nnz:
+            out[nz] = np.maximum.reduceat(v[M.indices], M.indptr[:-1][nz])
+        return out
+
+    while (state == 0).any():
+        p = np.where(state == 0, prio, 0)
+        m2 = rowmax(G2, p)
+        new = (state == 0) & (p == m2)
+        state[new] = 1
+        covered = (G2 @ new.astype(np.float64)) > 0
+        state[(state == 0) & covered] = 2
+    roots = np.nonzero(state == 1)[0]
+    rid = np.full(n, -1, np.int64)
+    rid[roots] = np.arange(len(roots))
+    rp = np.where(state == 1, prio, 0)
     agg = np.full(n, -1, np.int64)
-    blocked = np.zeros(n, bool)
-    roots = []
-    for v in order:             # greedy MIS-2: a root blocks its distance-2 neighbourhood
-        if blocked[v]:
-            continue
-        roots.append(v)
-        nb = G2.indices[G2.indptr[v]:G2.indptr[v + 1]]
-        blocked[nb] = True
-        blocked[v] = True
-    roots = np.array(roots, np.int64)
-    agg[roots] = np.arange(len(roots))
-    G1 = G.tocsr()
-    for v in roots:             # distance-1 neighbours join their root
-        nb = G1.indices[G1.indptr[v]:G1.indptr[v + 1]]
-        free = nb[agg[nb] < 0]
-        agg[free] = agg[v]
-    for v in np.nonzero(agg < 0)[0]:   # distance-2 leftovers join a neighbour's aggregate
-        nb = G1.indices[G1.indptr[v]:G1.indptr[v + 1]]
-        got = agg[nb][agg[nb] >= 0]
-        agg[v] = got.min() if len(got) else len(roots)
-        if not len(got):
-            roots = np.append(roots, v)
-    nagg = int(agg.max()) + 1
+    for M in (G, G2):                                   # nearest: distance 1, then 2
+        best = rowmax(M, rp)
+        undone = (agg < 0) & (best > 0)
+        inv = np.zeros(n + 1, np.int64)
+        inv[prio[roots]] = rid[roots]
+        agg[undone] = inv[best[undone]]
+    assert (agg >= 0).all()
+    nagg = len(roots)
     rcp, rir, rval = _csc_from_coo(n, nagg, np.arange(n), agg, np.ones(n))
     return nagg, rcp, rir, rval
