@@ -7,6 +7,10 @@
  *   combblas::gpu::LocalSpGEMM<SR, NTO>(A, B, clearA, clearB)             mtSpGEMM.h:73-78
  *   combblas::gpu::MultiwayMerge<SR>(lists, mdim, ndim, delarrs)          MultiwayMerge.h:411-412
  *   combblas::gpu::EstimateLocalFLOP<SR>(A, B)                             mtSpGEMM.h:667-694
+ *   combblas::gpu::MCLPruneRecoverySelect(A, thr, select, recover, pct, v) ParFriends.h:185-353
+ *
+ * MemEfficientSpGEMM (ParFriends.h:449-730) gets the device path by calling the first and the last
+ * of these in place of the reference's LocalSpGEMMHash / MCLPruneRecoverySelect.
  *
  * with the reference's signatures and conventions: A, B are SpDCCols<IT, NT> (their DCSC arrays are
  * handed to the device as they are, GetArrays order cp, jc, ir, numx); the product comes back as a
@@ -190,6 +194,54 @@ SpTuples<IT, NT>* MultiwayMerge(std::vector<SpTuples<IT, NT>*>& lists, IT mdim =
     if (delarrs)
       for (auto* T : lists) delete T;
     return to_tuples<IT, NT>(ctx, C);
+  }
+}
+
+// MCLPruneRecoverySelect (ParFriends.h:185-353) on an SpParMat whose local blocks hold complete
+// columns (one processor row: every column's nonzeros are on one rank) -> cbg_mcl_prune on the
+// device, in place.  Otherwise (columns split over processor rows, or a non-float NT) the
+// reference's own distributed version runs.
+template <class IT, class NT, class DER>
+void MCLPruneRecoverySelect(SpParMat<IT, NT, DER>& A, NT hardThreshold, IT selectNum, IT recoverNum,
+                            NT recoverPct, int kselectVersion) {
+  constexpr bool dev = std::is_same<NT, double>::value || std::is_same<NT, float>::value;
+  if constexpr (!dev) {
+    combblas::MCLPruneRecoverySelect(A, hardThreshold, selectNum, recoverNum, recoverPct, kselectVersion);
+  } else {
+    if (A.getcommgrid()->GetGridRows() != 1) {
+      combblas::MCLPruneRecoverySelect(A, hardThreshold, selectNum, recoverNum, recoverPct, kselectVersion);
+      return;
+    }
+    typedef typename DER::LocalIT LIT;
+    DER& L = A.seq();
+    cbg_ctx* ctx = context();
+    // local block -> host CSC (int64 colptr, int32 rows) -> device
+    SpTuples<LIT, NT> T(L);
+    T.SortColBased();
+    const int64_t ncol = L.getncol(), nnz = T.getnnz();
+    std::vector<int64_t> cp(ncol + 1, 0);
+    std::vector<int32_t> row(nnz > 0 ? nnz : 1);
+    std::vector<NT> val(nnz > 0 ? nnz : 1);
+    for (int64_t k = 0; k < nnz; ++k) {
+      ++cp[T.colindex(k) + 1];
+      row[k] = (int32_t)T.rowindex(k);
+      val[k] = T.numvalue(k);
+    }
+    for (int64_t j = 0; j < ncol; ++j) cp[j + 1] += cp[j];
+    cbg_dcsc_view v{};
+    v.nrow = L.getnrow(); v.ncol = ncol; v.nnz = nnz; v.nzc = ncol;
+    v.cp = cp.data(); v.ir = row.data(); v.idx_bytes = 4; v.ptr_bytes = 8;
+    v.val = val.data(); v.val_type = DeviceType<NT>::code; v.on_device = 0;
+    cbg_csc_result D{}, P{};
+    check(cbg_upload(ctx, &v, &D), "cbg_upload");
+    cbg_status s = cbg_mcl_prune(ctx, &D, (double)hardThreshold, (int64_t)selectNum, (int64_t)recoverNum,
+                                 (double)recoverPct, &P, nullptr);
+    cbg_result_free(ctx, &D);
+    check(s, "cbg_mcl_prune");
+    SpTuples<LIT, NT>* pt = to_tuples<LIT, NT>(ctx, P);
+    L = DER(*pt, false);
+    delete pt;
+    (void)kselectVersion;   // Kselect1 / Kselect2 pick the same k-th value
   }
 }
 

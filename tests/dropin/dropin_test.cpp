@@ -105,6 +105,28 @@ int main(int argc, char** argv) {
     if (f != fr) rc = 1;
     delete ref; delete dev; delete ri; delete di; delete rc1; delete dc1; delete mr; delete md;
     delete A; delete B; delete Ai; delete Bi;
+
+    // MCLPruneRecoverySelect on a 1-rank SpParMat: reference (CPU, ParFriends.h:185-353) vs drop-in
+    {
+      typedef SpDCCols<I, double> DCC;
+      typedef SpParMat<I, double, DCC> PM;
+      std::shared_ptr<CommGrid> grid(new CommGrid(MPI_COMM_WORLD, 0, 0));
+      auto* P = random_dccols<double>(400, 300, 0.08, 5);
+      SpTuples<I, double>* sq = LocalSpGEMMHash<PT, double>(*P, *P, false, false, true);
+      sq->SortColBased();
+      for (I k = 0; k < sq->getnnz(); ++k) std::get<2>(sq->tuples[k]) = 1.0 / (1.0 + std::get<2>(sq->tuples[k]));
+      const double params[3][4] = {{1e-4, 1100, 1400, 0.9}, {0.05, 10, 15, 0.9}, {0.3, 5, 8, 0.99}};
+      for (auto& p : params) {
+        PM R(new DCC(*sq, false), grid), D(new DCC(*sq, false), grid);
+        combblas::MCLPruneRecoverySelect(R, p[0], (I)p[1], (I)p[2], p[3], 1);
+        gpu::MCLPruneRecoverySelect(D, p[0], (I)p[1], (I)p[2], p[3], 1);
+        SpTuples<I, double>* a = new SpTuples<I, double>(R.seq());
+        SpTuples<I, double>* b = new SpTuples<I, double>(D.seq());
+        if (!same(b, a, "MCLPruneRecoverySelect")) rc = 1;
+        delete a; delete b;
+      }
+      delete sq; delete P;
+    }
   }
   MPI_Finalize();
   printf(rc == 0 ? "DROPIN OK\n" : "DROPIN FAILED\n");
