@@ -111,7 +111,7 @@ int main(int argc, char** argv) {
       typedef SpDCCols<I, double> DCC;
       typedef SpParMat<I, double, DCC> PM;
       std::shared_ptr<CommGrid> grid(new CommGrid(MPI_COMM_WORLD, 0, 0));
-      auto* P = random_dccols<double>(400, 300, 0.08, 5);
+      auto* P = random_dccols<double>(300, 300, 0.08, 5);
       SpTuples<I, double>* sq = LocalSpGEMMHash<PT, double>(*P, *P, false, false, true);
       sq->SortColBased();
       for (I k = 0; k < sq->getnnz(); ++k) std::get<2>(sq->tuples[k]) = 1.0 / (1.0 + std::get<2>(sq->tuples[k]));
