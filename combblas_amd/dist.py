@@ -161,6 +161,10 @@ class SpParMat3D:
         self.block = block_from_host(r1 - r0, c1 - c0, lcp, lir, lval, backend.device)
         return self
 
+    def __call__(self, ri, ci):
+        """SpParMat::operator()(ri, ci) (SpParMat.h) = SubsRef_SR with PlusTimes semirings."""
+        return SubsRef_SR(self, ri, ci)
+
     def getnnz(self):
         t = torch.tensor([self.block.nnz], dtype=torch.int64, device=self.backend.comm_device)
         dist.all_reduce(t)
@@ -243,7 +247,72 @@ def _fiber_exchange(C, grid, backend, sr):
 
 
 # ----------------------------------------------------------------------------------- multiplies
-def Mult_AnXBn_SUMMA3D(SR, A, B, stats=None):
+def _row_slice(b, r0, r1):
+    """Rows [r0, r1) of a Block, rebased (the row half of a transposed Split, SpDCCols.cpp:897)."""
+    keep = (b.ir >= r0) & (b.ir < r1)
+    cnt = torch.diff(b.cp)
+    col = torch.repeat_interleave(torch.arange(b.ncol, device=b.cp.device), cnt)
+    kc = torch.bincount(col[keep], minlength=b.ncol) if b.nnz else torch.zeros(b.ncol, dtype=torch.int64,
+                                                                                  device=b.cp.device)
+    cp = torch.zeros(b.ncol + 1, dtype=torch.int64, device=b.cp.device)
+    torch.cumsum(kc, 0, out=cp[1:])
+    return Block(r1 - r0, b.ncol, cp, (b.ir[keep] - r0).to(torch.int32), b.val[keep])
+
+
+def _summa_partials(SR, A, B, stats, halves):
+    """The q SUMMA stages of one layer.  halves=False: one broadcast pair per stage; halves=True
+    (Mult_AnXBn_DoubleBuff, ParFriends.h:799-997): every rank Splits its A piece by columns and its
+    B piece by rows at half the inner width (SpDCCols::Split, cut = n/2) and the stages run once per
+    half, so only half a stage's operands is in flight at a time.  Each stage's broadcasts are
+    issued one stage ahead (async) so they overlap the current local multiply."""
+    g, be = A.grid, A.backend
+    q, L = g.q, g.L
+    r0, r1 = block_range(A.nrow, q, g.row)
+    ncl = B.block.ncol   # local columns of B (= of C): block `col` of B, or a phase piece of it
+    widths = [piece_range(A.ncol, q, L, k, g.layer) for k in range(q)]
+    widths = [k1 - k0 for (k0, k1) in widths]
+    if halves:
+        ca, cb = A.block.ncol // 2, B.block.nrow // 2   # this rank's A piece is inner block `col`, its B piece `row`
+        mine = [(_col_slice(A.block, 0, ca), _row_slice(B.block, 0, cb)),
+                (_col_slice(A.block, ca, A.block.ncol), _row_slice(B.block, cb, B.block.nrow))]
+        spans = [[(w // 2) for w in widths], [w - w // 2 for w in widths]]
+    else:
+        mine = [(A.block, B.block)]
+        spans = [widths]
+    rounds = []
+    for (ab, bb), sp_ in zip(mine, spans):
+        a_nnz = _allgather_nnz(ab, g.row_group, q, be)   # pieces (l, i, k), k = 0..q-1
+        b_nnz = _allgather_nnz(bb, g.col_group, q, be)   # pieces (l, k, j)
+        rounds.append((ab, bb, sp_, a_nnz, b_nnz))
+
+    def issue(h, k):
+        ab, bb, sp_, a_nnz, b_nnz = rounds[h]
+        a = _BlockBcast(ab, r1 - r0, sp_[k], a_nnz[k], g.rank_of(g.layer, g.row, k), g.row_group, be, g.rank)
+        b = _BlockBcast(bb, sp_[k], ncl, b_nnz[k], g.rank_of(g.layer, k, g.col), g.col_group, be, g.rank)
+        return a, b
+
+    steps = [(h, k) for h in range(len(rounds)) for k in range(q)]
+    partials = []
+    pending = issue(*steps[0]) if q > 1 else None
+    for s, (h, k) in enumerate(steps):
+        if q > 1:
+            a, b = pending
+            Ak, Bk = a.wait(), b.wait()
+            if s + 1 < len(steps):
+                pending = issue(*steps[s + 1])   # double buffering: the next stage travels during this one
+        else:
+            Ak, Bk = rounds[h][0], rounds[h][1]
+        if Ak.ncol == 0:   # an empty half (Split of a one-column piece): nothing to multiply
+            partials.append(Block(r1 - r0, ncl, torch.zeros(ncl + 1, dtype=torch.int64, device=be.device),
+                                  torch.zeros(0, dtype=torch.int32, device=be.device),
+                                  torch.zeros(0, dtype=be.val_dtype, device=be.device)))
+        else:
+            partials.append(be.multiply(Ak, Bk, SR, stats))
+    nonempty = [p for p in partials if p.nnz]
+    return nonempty or partials[:1]
+
+
+def Mult_AnXBn_SUMMA3D(SR, A, B, stats=None, halves=False):
     """C = A * B over the semiring on the 3D grid (ParFriends.h:2918-3208).  A must be colsplit,
     B rowsplit, on the same grid; C comes back colsplit.  Dimension checks as CheckSpGEMMCompliance
     (ParFriends.h:160-181): a mismatch raises (the reference aborts with DIMMISMATCH 3002)."""
@@ -253,50 +322,202 @@ def Mult_AnXBn_SUMMA3D(SR, A, B, stats=None):
     if not A.colsplit or B.colsplit or B.grid is not g:
         raise ValueError("A must be colsplit and B rowsplit on the same CommGrid3D")
     be = A.backend
-    q, L = g.q, g.L
-    a_nnz = _allgather_nnz(A.block, g.row_group, q, be)   # pieces (l, i, k), k = 0..q-1
-    b_nnz = _allgather_nnz(B.block, g.col_group, q, be)   # pieces (l, k, j)
-    r0, r1 = block_range(A.nrow, q, g.row)
-    ncl = B.block.ncol   # local columns of B (= of C): block `col` of B, or a phase piece of it
-
-    def issue(k):
-        k0, k1 = piece_range(A.ncol, q, L, k, g.layer)
-        a = _BlockBcast(A.block, r1 - r0, k1 - k0, a_nnz[k], g.rank_of(g.layer, g.row, k), g.row_group, be, g.rank)
-        b = _BlockBcast(B.block, k1 - k0, ncl, b_nnz[k], g.rank_of(g.layer, k, g.col), g.col_group, be, g.rank)
-        return a, b
-
-    partials = []
-    pending = issue(0) if q > 1 else None
-    for k in range(q):
-        if q > 1:
-            a, b = pending
-            Ak, Bk = a.wait(), b.wait()
-            if k + 1 < q:
-                pending = issue(k + 1)   # double buffering: stage k+1 travels while stage k multiplies
-        else:
-            Ak, Bk = A.block, B.block
-        partials.append(be.multiply(Ak, Bk, SR, stats))
-    C = partials[0] if q == 1 else be.merge(partials, SR)
-    if L > 1:
+    partials = _summa_partials(SR, A, B, stats, halves)
+    C = partials[0] if len(partials) == 1 else be.merge(partials, SR)
+    if g.L > 1:
         C = _fiber_exchange(C, g, be, SR)
     return SpParMat3D(g, A.nrow, B.ncol, C, True, be)
 
 
-def Mult_AnXBn_Synch(SR, A, B, stats=None):
-    """2D SUMMA (ParFriends.h:1004-1108) = the one-layer case of the 3D driver."""
+def _as_2d_operands(A, B, name):
+    """On a one-layer grid the A-side and B-side distributions coincide (both are the q x q block
+    distribution of SpParMat), so any two SpParMat3D on it can be multiplied as in the 2D drivers."""
     if A.grid.L != 1:
-        raise ValueError("Mult_AnXBn_Synch needs a 2D (one-layer) grid")
-    return Mult_AnXBn_SUMMA3D(SR, A, B, stats)
+        raise ValueError(f"{name} needs a 2D (one-layer) grid")
+    if A.ncol != B.nrow:
+        raise _abi.CbgError(_abi.EDIM, name)
+    return (SpParMat3D(A.grid, A.nrow, A.ncol, A.block, True, A.backend),
+            SpParMat3D(B.grid, B.nrow, B.ncol, B.block, False, B.backend))
+
+
+def Mult_AnXBn_Synch(SR, A, B, clearA=False, clearB=False, stats=None):
+    """2D SUMMA (ParFriends.h:1004-1108) = the one-layer case of the 3D driver.  clearA/clearB drop
+    the operands' local blocks after the product (the reference deletes them)."""
+    a, b = _as_2d_operands(A, B, "Mult_AnXBn_Synch")
+    C = Mult_AnXBn_SUMMA3D(SR, a, b, stats)
+    _clear(A, clearA)
+    _clear(B, clearB and B is not A)
+    return C
+
+
+def Mult_AnXBn_DoubleBuff(SR, A, B, clearA=False, clearB=False, stats=None):
+    """ParFriends.h:799-997: 2D SUMMA with each operand Split in two along the inner dimension and
+    2q stages (half the operand memory in flight); 2q partials merged.  Same product as Synch."""
+    a, b = _as_2d_operands(A, B, "Mult_AnXBn_DoubleBuff")
+    C = Mult_AnXBn_SUMMA3D(SR, a, b, stats, halves=True)
+    _clear(A, clearA)
+    _clear(B, clearB and B is not A)
+    return C
+
+
+def Mult_AnXBn_Overlap(SR, A, B, clearA=False, clearB=False, stats=None):
+    """ParFriends.h:1110-1235: 2D SUMMA with the next stage's non-blocking broadcasts posted before
+    the current local multiply -- what every driver here does (stage k+1 is issued async)."""
+    return Mult_AnXBn_Synch(SR, A, B, clearA, clearB, stats)
+
+
+def _clear(M, flag):
+    if flag:
+        M.block = Block(M.block.nrow, M.block.ncol, torch.zeros(M.block.ncol + 1, dtype=torch.int64,
+                                                                device=M.block.cp.device),
+                        M.block.ir[:0], M.block.val[:0])
 
 
 def PSpGEMM(SR, A, B, stats=None):
     """SpParMat.h:451-464: the default distributed SpGEMM (Mult_AnXBn_Synch)."""
-    return Mult_AnXBn_Synch(SR, A, B, stats)
+    return Mult_AnXBn_Synch(SR, A, B, stats=stats)
 
 
 def multiply(SR, A, B, stats=None):
     """3DSpGEMM driver entry (Multiplier.h:10-61): split-3D product on the grid A and B live on."""
     return Mult_AnXBn_SUMMA3D(SR, A, B, stats)
+
+
+# --------------------------------------------------------------------------- indexing via SpGEMM
+# SpParMat's indexing operations are SpGEMMs with 0/1 selection matrices (SpParMat.cpp:2028-2562):
+# A(ri, ci) = P * A * Q with P(k, ri[k]) = 1 and Q(ci[k], k) = 1.  Index vectors are replicated
+# numpy arrays here (the reference's FullyDistVec is distributed; each rank only needs the entries
+# that land in its own block, which it selects locally -- the alltoallv that routes them in the
+# reference, SpParMat.cpp:2083-2127, is not needed).  2D (one-layer) grids, like SpParMat.
+
+def _sr_for(be, cls_name):
+    import combblas_amd as cb
+    code = {torch.float64: "f64", torch.float32: "f32", torch.int64: "i64", torch.int32: "i32",
+            torch.uint8: "bool"}[be.val_dtype]
+    return getattr(cb, cls_name)(code)
+
+
+def _index_vector(v, bound, what):
+    v = np.asarray(v, dtype=np.int64).reshape(-1)
+    if v.size and (int(v.min()) < 0 or int(v.max()) >= bound):
+        # the reference throws outofrangeexception for max > total (SpParMat.cpp:2051); an index equal
+        # to the dimension would build an out-of-range selection matrix there, so it is rejected too
+        raise IndexError(f"{what}: index out of range [0, {bound})")
+    return v
+
+
+def _selection(grid, be, nrow, ncol, rows, cols):
+    """This rank's block of the nrow x ncol 0/1 matrix with ones at (rows[k], cols[k]); duplicate
+    positions collapse to one entry (the matrices are bool-valued in the reference)."""
+    (r0, r1), (c0, c1) = block_range(nrow, grid.q, grid.row), block_range(ncol, grid.q, grid.col)
+    m = (rows >= r0) & (rows < r1) & (cols >= c0) & (cols < c1)
+    nr, nc = r1 - r0, c1 - c0
+    key = np.unique((cols[m] - c0) * max(nr, 1) + (rows[m] - r0))
+    c, r = key // max(nr, 1), key % max(nr, 1)
+    cp = np.zeros(nc + 1, np.int64)
+    np.cumsum(np.bincount(c, minlength=nc), out=cp[1:])
+    vals = np.ones(key.size, dtype=torch.empty(0, dtype=be.val_dtype).numpy().dtype)
+    return SpParMat3D(grid, nrow, ncol, block_from_host(nr, nc, cp, r.astype(np.int32), vals, be.device), True, be)
+
+
+def _keys(b):
+    col = torch.repeat_interleave(torch.arange(b.ncol, device=b.cp.device), torch.diff(b.cp))
+    return col, col * max(b.nrow, 1) + b.ir.to(torch.int64)
+
+
+def _set_difference(blk, other):
+    """SpParMat::SetDifference: drop the entries of blk whose (row, col) also appear in other."""
+    if blk.nnz == 0 or other.nnz == 0:
+        return blk
+    col, ka = _keys(blk)
+    _, kb = _keys(other)
+    keep = ~torch.isin(ka, kb)
+    cp = torch.zeros(blk.ncol + 1, dtype=torch.int64, device=blk.cp.device)
+    torch.cumsum(torch.bincount(col[keep], minlength=blk.ncol), 0, out=cp[1:])
+    return Block(blk.nrow, blk.ncol, cp, blk.ir[keep], blk.val[keep])
+
+
+def SubsRef_SR(A, ri, ci, PTNTBOOL=None, PTBOOLNT=None, inplace=False):
+    """A(ri, ci) (SpParMat.cpp:2028-2247): PA = P*A over PTBOOLNT, then (PA)*Q over PTNTBOOL (both
+    Mult_AnXBn_DoubleBuff).  Default semirings PlusTimes on A's value type (the reference's
+    operator() uses PlusTimesSRing<bool,NT>).  Returns a len(ri) x len(ci) matrix, or replaces A."""
+    g, be = A.grid, A.backend
+    ri = _index_vector(ri, A.nrow, "SubsRef_SR ri")
+    ci = _index_vector(ci, A.ncol, "SubsRef_SR ci")
+    PTBOOLNT = PTBOOLNT or _sr_for(be, "PlusTimesSRing")
+    PTNTBOOL = PTNTBOOL or _sr_for(be, "PlusTimesSRing")
+    P = _selection(g, be, ri.size, A.nrow, np.arange(ri.size, dtype=np.int64), ri)
+    PA = Mult_AnXBn_DoubleBuff(PTBOOLNT, P, A, clearA=True)
+    Q = _selection(g, be, A.ncol, ci.size, ci, np.arange(ci.size, dtype=np.int64))
+    C = Mult_AnXBn_DoubleBuff(PTNTBOOL, PA, Q, clearA=True, clearB=True)
+    if inplace:
+        A.nrow, A.ncol, A.block = C.nrow, C.ncol, C.block
+        return SpParMat3D(g, 0, 0, None, True, be)   # dummy, as the reference
+    return C
+
+
+def SubsRef_SR_dim(A, v, dim, PTNTBOOL=None, PTBOOLNT=None, inplace=False):
+    """Row or column extraction (SpParMat.cpp:2251-2422): dim "row" -> A(v, :) = V*A over PTBOOLNT,
+    dim "column" -> A(:, v) = A*V' over PTNTBOOL."""
+    g, be = A.grid, A.backend
+    if dim in ("row", "Row", 0):
+        v = _index_vector(v, A.nrow, "SubsRef_SR row")
+        V = _selection(g, be, v.size, A.nrow, np.arange(v.size, dtype=np.int64), v)
+        C = Mult_AnXBn_DoubleBuff(PTBOOLNT or _sr_for(be, "PlusTimesSRing"), V, A, clearA=True)
+    elif dim in ("column", "Column", 1):
+        v = _index_vector(v, A.ncol, "SubsRef_SR column")
+        V = _selection(g, be, A.ncol, v.size, v, np.arange(v.size, dtype=np.int64))
+        C = Mult_AnXBn_DoubleBuff(PTNTBOOL or _sr_for(be, "PlusTimesSRing"), A, V, clearB=True)
+    else:
+        raise ValueError("dim must be 'row' or 'column'")
+    if inplace:
+        A.nrow, A.ncol, A.block = C.nrow, C.ncol, C.block
+        return SpParMat3D(g, 0, 0, None, True, be)
+    return C
+
+
+def Prune(A, ri, ci):
+    """Remove A[ri, ci] in place (SpParMat.cpp:2474-2514): SA = S*A over BoolCopy2nd, SAT = SA*T over
+    BoolCopy1st with S = diag(ri), T = diag(ci), then SetDifference(SAT)."""
+    g, be = A.grid, A.backend
+    ri = _index_vector(ri, A.nrow, "Prune ri")
+    ci = _index_vector(ci, A.ncol, "Prune ci")
+    S = _selection(g, be, A.nrow, A.nrow, ri, ri)
+    SA = Mult_AnXBn_DoubleBuff(_sr_for(be, "BoolCopy2ndSRing"), S, A, clearA=True)
+    T = _selection(g, be, A.ncol, A.ncol, ci, ci)
+    SAT = Mult_AnXBn_DoubleBuff(_sr_for(be, "BoolCopy1stSRing"), SA, T, clearA=True, clearB=True)
+    A.block = _set_difference(A.block, SAT.block)
+
+
+def PruneFull(A, ri, ci):
+    """Remove every nonzero of the rows ri and of the columns ci (SpParMat.cpp:2521-2562)."""
+    g, be = A.grid, A.backend
+    ri = _index_vector(ri, A.nrow, "PruneFull ri")
+    ci = _index_vector(ci, A.ncol, "PruneFull ci")
+    S = _selection(g, be, A.nrow, A.nrow, ri, ri)
+    SA = Mult_AnXBn_DoubleBuff(_sr_for(be, "BoolCopy2ndSRing"), S, A, clearA=True)
+    T = _selection(g, be, A.ncol, A.ncol, ci, ci)
+    AT = Mult_AnXBn_DoubleBuff(_sr_for(be, "BoolCopy1stSRing"), A, T, clearB=True)
+    A.block = _set_difference(_set_difference(A.block, SA.block), AT.block)
+
+
+def SpAsgn(A, ri, ci, B):
+    """A(ri, ci) = B in place (SpParMat.cpp:2426-2467): Prune(ri, ci) makes the hole, B is embedded
+    as R*B*Q over PlusTimes (R(ri[k], k) = 1, Q(k, ci[k]) = 1) and extend-added (+=)."""
+    g, be = A.grid, A.backend
+    if B.grid is not g:
+        raise ValueError("SpAsgn: grids are not comparable")
+    ri = _index_vector(ri, A.nrow, "SpAsgn ri")
+    ci = _index_vector(ci, A.ncol, "SpAsgn ci")
+    if B.nrow != ri.size or B.ncol != ci.size:
+        raise _abi.CbgError(_abi.EDIM, "SpAsgn")   # DIMMISMATCH (SpParMat.cpp:2441-2450)
+    Prune(A, ri, ci)
+    pt = _sr_for(be, "PlusTimesSRing")
+    R = _selection(g, be, A.nrow, B.nrow, ri, np.arange(ri.size, dtype=np.int64))
+    RB = Mult_AnXBn_DoubleBuff(pt, R, B, clearA=True)
+    Q = _selection(g, be, B.ncol, A.ncol, np.arange(ci.size, dtype=np.int64), ci)
+    RBQ = Mult_AnXBn_DoubleBuff(pt, RB, Q, clearA=True, clearB=True)
+    A.block = be.merge([A.block, RBQ.block], pt) if RBQ.block.nnz else A.block
 
 
 # ------------------------------------------------------------------------------ HipMCL expansion

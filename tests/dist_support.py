@@ -182,3 +182,94 @@ def spawn_case(world, backend_kind, cases, port, body=None):
         if p.is_alive():
             p.kill()
     assert not errs and all(c == 0 for c in codes), "\n".join(errs) + f"\nexit codes {codes}"
+
+
+def _check_piece(M, R, rank, what):
+    """M's local piece (block distribution) equals the same block of the global scipy matrix R."""
+    R = sp.csc_matrix(R)
+    R.sum_duplicates()
+    (r0, r1), (c0, c1) = M.local_range()
+    Rl = R[r0:r1, c0:c1].tocsc()
+    Rl.sort_indices()
+    blk = M.block
+    assert (M.nrow, M.ncol) == R.shape, (what, M.nrow, M.ncol, R.shape)
+    assert (blk.nrow, blk.ncol) == (r1 - r0, c1 - c0), (what, blk.nrow, blk.ncol)
+    assert np.array_equal(blk.cp.cpu().numpy(), Rl.indptr), f"rank {rank} {what}: colptr differs"
+    assert np.array_equal(blk.ir.cpu().numpy(), Rl.indices), f"rank {rank} {what}: rows differ"
+    assert np.array_equal(blk.val.cpu().numpy(), Rl.data), f"rank {rank} {what}: values differ"
+
+
+def _pruned(A, ri, ci):
+    """Global expectation of Prune: A without the entries (i, j), i in ri, j in ci."""
+    C = sp.coo_matrix(A)
+    drop = np.isin(C.row, ri) & np.isin(C.col, ci)
+    return sp.csc_matrix((C.data[~drop], (C.row[~drop], C.col[~drop])), shape=A.shape)
+
+
+def run_index_case(rank, world, port, backend_kind, cases, errq):
+    """Per-rank body of the 2D drivers (Synch / DoubleBuff / Overlap) and of the SpGEMM-based
+    indexing (SubsRef_SR, Prune, PruneFull, SpAsgn; SpParMat.cpp:2028-2562) on a one-layer grid."""
+    try:
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        q = int(round(world ** 0.5))
+        grid = cbd.CommGrid(q, q)
+        if backend_kind == "scipy":
+            be = ScipyBackend()
+        else:
+            import combblas_amd as cb
+            be = cbd.GpuBackend(cb.Context(0))
+        sr = cb_sr(backend_kind)
+        for (n, m, density, seed) in cases:
+            rng = np.random.default_rng(seed)
+            A = random_csc(n, m, density, seed)
+            B = random_csc(m, n, density, seed + 1)
+
+            def dmat(M):
+                return cbd.SpParMat3D.from_global_csc(grid, M.shape[0], M.shape[1], M.indptr, M.indices, M.data,
+                                                      True, be)
+            for f in (cbd.Mult_AnXBn_Synch, cbd.Mult_AnXBn_DoubleBuff, cbd.Mult_AnXBn_Overlap):
+                _check_piece(f(sr, dmat(A), dmat(B)), A @ B, rank, f.__name__)
+            ri = rng.integers(0, n, max(1, n // 3))          # duplicates allowed, unsorted
+            ci = rng.permutation(m)[: max(1, m // 2)]
+            _check_piece(cbd.SubsRef_SR(dmat(A), ri, ci), A[ri][:, ci], rank, "SubsRef_SR")
+            _check_piece(dmat(A)(ri, ci), A[ri][:, ci], rank, "A(ri,ci)")
+            _check_piece(cbd.SubsRef_SR_dim(dmat(A), ri, "row"), A[ri], rank, "SubsRef_SR row")
+            _check_piece(cbd.SubsRef_SR_dim(dmat(A), ci, "column"), A[:, ci], rank, "SubsRef_SR column")
+            D = dmat(A)
+            cbd.SubsRef_SR(D, ri, ci, inplace=True)
+            _check_piece(D, A[ri][:, ci], rank, "SubsRef_SR inplace")
+            D = dmat(A)
+            cbd.Prune(D, ri, ci)
+            _check_piece(D, _pruned(A, ri, ci), rank, "Prune")
+            D = dmat(A)
+            cbd.PruneFull(D, ri, ci)
+            Af = sp.coo_matrix(A)
+            keep = ~(np.isin(Af.row, ri) | np.isin(Af.col, ci))
+            _check_piece(D, sp.csc_matrix((Af.data[keep], (Af.row[keep], Af.col[keep])), shape=A.shape), rank,
+                         "PruneFull")
+            ru = rng.permutation(n)[: max(1, n // 4)]
+            cu = rng.permutation(m)[: max(1, m // 3)]
+            Bs = random_csc(ru.size, cu.size, 0.5, seed + 2)
+            D = dmat(A)
+            cbd.SpAsgn(D, ru, cu, dmat(Bs))
+            Rm = sp.csc_matrix((np.ones(ru.size), (ru, np.arange(ru.size))), shape=(n, ru.size))
+            Qm = sp.csc_matrix((np.ones(cu.size), (np.arange(cu.size), cu)), shape=(cu.size, m))
+            _check_piece(D, _pruned(A, ru, cu) + Rm @ Bs @ Qm, rank, "SpAsgn")
+            try:
+                cbd.SubsRef_SR(dmat(A), [n], ci)
+                raise AssertionError("out-of-range index accepted")
+            except IndexError:
+                pass
+            try:
+                cbd.SpAsgn(dmat(A), ru, cu, dmat(random_csc(ru.size + 1, cu.size, 0.5, seed)))
+                raise AssertionError("SpAsgn dimension mismatch accepted")
+            except Exception as e:
+                assert getattr(e, "status", None) == 3002, e
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:
+        import traceback
+        errq.put(f"rank {rank}: {e!r}\n{traceback.format_exc()}")
+        raise

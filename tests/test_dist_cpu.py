@@ -24,3 +24,14 @@ MCL_CASES = [(300, 3, 1, (1e-3, 8, 12, 0.9)), (257, 4, 3, (1e-3, 8, 12, 0.9)), (
 def test_mcl_expansion_gloo_cpu(world, port):
     from dist_support import run_mcl_case
     spawn_case(world, "scipy", MCL_CASES, port, body=run_mcl_case)
+
+
+INDEX_CASES = [(40, 30, 0.1, 21), (9, 13, 0.3, 23), (3, 4, 0.5, 25)]
+
+
+@pytest.mark.parametrize("world,port", [(1, 29617), (4, 29618)])
+def test_2d_drivers_and_indexing_gloo_cpu(world, port):
+    """Mult_AnXBn_Synch / DoubleBuff / Overlap and SubsRef_SR / Prune / PruneFull / SpAsgn on 1x1 and
+    2x2 grids (SpParMat.cpp:2028-2562, ParFriends.h:799-1235) against scipy on the global matrices."""
+    from dist_support import run_index_case
+    spawn_case(world, "scipy", INDEX_CASES, port, body=run_index_case)

@@ -22,3 +22,14 @@ MCL_CASES = [(600, 3, 1, (1e-3, 8, 12, 0.9)), (513, 4, 3, (1e-3, 8, 12, 0.9)), (
 def test_mcl_expansion_gloo_gpu(world, port):
     from dist_support import run_mcl_case
     spawn_case(world, "gpu", MCL_CASES, port, body=run_mcl_case)
+
+
+INDEX_CASES = [(300, 250, 0.03, 31), (9, 13, 0.3, 23), (3, 4, 0.5, 25)]
+
+
+@pytest.mark.parametrize("world,port", [(1, 29627), (4, 29628)])
+def test_2d_drivers_and_indexing_gloo_gpu(world, port):
+    """DoubleBuff / Overlap / Synch and the SpGEMM-based indexing (BoolCopy1st/2nd for Prune,
+    PlusTimes for SubsRef_SR / SpAsgn) through libcbgpu, exact against scipy."""
+    from dist_support import run_index_case
+    spawn_case(world, "gpu", INDEX_CASES, port, body=run_index_case)
