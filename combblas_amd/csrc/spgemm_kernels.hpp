@@ -63,6 +63,18 @@ constexpr int64_t kHeavy = 4096;   // nnz(C(:,j)) above which a column is split 
 #ifndef CBG_ITEM_UNITS
 #define CBG_ITEM_UNITS 8
 #endif
+// k_num_heavy rank mode: single-chunk units whose span fits a 32*T-row bitmap get exact slots
+#ifndef CBG_RANK_MODE
+#define CBG_RANK_MODE 1
+#endif
+// rank mode: register-resident sweeps for chunks of <= NT*U*CBG_RANK_REGS groups
+#ifndef CBG_RANK_REGS
+#define CBG_RANK_REGS 4
+#endif
+// units also end where their span would exceed the rank-mode bitmap (32*T rows)
+#ifndef CBG_RANK_SPAN_CAP
+#define CBG_RANK_SPAN_CAP 0
+#endif
 #ifndef CBG_UNIT_CAP
 #define CBG_UNIT_CAP (1 << (CBG_HEAVY_LOGT - 1))
 #endif
@@ -434,6 +446,60 @@ __device__ __forceinline__ void expand_staged(const SegBuf<V>& sb, int tid, int6
       }
     }
   }
+}
+
+// Two sweeps over one staged chunk with the loaded items kept in registers (F <= NT*U*RI groups):
+// load every item once, mark(item) each, then mid() (block-uniform: barrier + whatever must see all
+// marks; false aborts), then acc(item, bv, q, b) each -- the rank mode's mark and accumulate sweeps
+// without gathering A twice.
+template <int NT, int U, int G, int RI, typename V, class LdF, class MarkF, class MidF, class AccF>
+__device__ __forceinline__ bool expand_staged_twice(const SegBuf<V>& sb, int tid, int64_t F, int64_t base, int nseg,
+                                                    LdF ld, MarkF mark, MidF mid, AccF acc) {
+  using Item = decltype(ld(int64_t(0)));
+  int P = 1;
+  while (P < nseg) P <<= 1;
+  Item it[RI][U][G];
+  int ss[RI][U];
+  int64_t qq[RI][U];
+  int nv[RI][U];
+#pragma unroll
+  for (int r = 0; r < RI; ++r)
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t g = (int64_t)(r * U + u) * NT + tid;
+      nv[r][u] = 0;
+      ss[r][u] = 0;
+      qq[r][u] = 0;
+      if (g < F) {
+        const int sg = seg_search<NT>(sb.off, g, P);
+        const int64_t k0 = (g - sb.off[sg]) * G;
+        ss[r][u] = sg;
+        qq[r][u] = sb.qb[sg] + k0;
+        nv[r][u] = (int)min<int64_t>(G, sb.len[sg] - k0);
+#pragma unroll
+        for (int i = 0; i < G; ++i)
+          if (i < nv[r][u]) it[r][u][i] = ld(qq[r][u] + i);
+      }
+    }
+#pragma unroll
+  for (int r = 0; r < RI; ++r)
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int i = 0; i < G; ++i)
+        if (i < nv[r][u]) mark(it[r][u][i]);
+  if (!mid()) return false;
+#pragma unroll
+  for (int r = 0; r < RI; ++r)
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (nv[r][u] > 0) {
+        const V bv = sb.bv[ss[r][u]];
+#pragma unroll
+        for (int i = 0; i < G; ++i)
+          if (i < nv[r][u]) acc(it[r][u][i], bv, qq[r][u] + i, base + ss[r][u]);
+      }
+  return true;
 }
 
 template <int NT, bool WAVE, int U, int G, typename V, class SegF, class LdF, class InsF>
@@ -915,7 +981,8 @@ __global__ void k_build_units(int H, const int32_t* __restrict__ cols, const int
   };
   for (int32_t s = sf; s <= sl; ++s) {
     const int64_t n = c[s];
-    if (acc > 0 && acc + n > kUnitCap) {
+    const bool wide = CBG_RANK_SPAN_CAP && (((int64_t)(s + 1 - st) << log) > (32LL << CBG_HEAVY_LOGT));
+    if (acc > 0 && (acc + n > kUnitCap || wide)) {
       emit(st, s, acc);
       st = s;
       acc = 0;
@@ -1393,16 +1460,19 @@ __global__ void __launch_bounds__(NT) k_num_heavy(const HeavyItem* __restrict__ 
   using Acc = typename SRT::Acc;
   constexpr int T = 1 << LOGT;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  Acc* vals = (Acc*)smem;                        // T + NT
-  int64_t* qb = (int64_t*)(vals + T + NT);       // NT
+  // vals and keys are adjacent: rank mode uses the pair as one region (values, then the bitmap)
+  int64_t* qb = (int64_t*)smem;                  // NT
   int64_t* off = qb + NT;                        // NT
   int64_t* scr = off + NT;                       // NT/64 + 1
-  int32_t* lens = (int32_t*)(scr + NT / kWave + 1); // NT
-  V* bvs = (V*)(lens + NT);                      // NT
-  int32_t* keys = (int32_t*)(bvs + NT);          // T + NT
-  int* misc = keys + T + NT;                     // [1] overflow, [2] adderr, [8..] int scan (64 ints)
+  V* bvs = (V*)(scr + NT / kWave + 1);           // NT
+  int32_t* lens = (int32_t*)(bvs + NT);          // NT
+  int* misc = lens + NT;                         // [1] overflow, [2] adderr, [8..] int scan (64 ints)
   Unit* s_units = (Unit*)(misc + 64);            // kItemUnits
-  uint32_t* hc = (uint32_t*)(s_units + kItemUnits); // T/2 packed home counters (compaction)
+  Acc* vals = (Acc*)(s_units + kItemUnits);      // T + NT
+  int32_t* keys = (int32_t*)(vals + T + NT);     // T + NT
+  uint32_t* hc = (uint32_t*)(keys + T + NT);     // T/2 packed home counters (compaction) / rank directory
+  static_assert(sizeof(Unit) % 8 == 0 && (NT % 2) == 0, "LDS carve-up must keep 8-byte alignment");
+  constexpr int64_t kRankBytes = (int64_t)(T + NT) * (int64_t)(sizeof(Acc) + 4);
   const SegBuf<V> sb{qb, off, bvs, scr, lens};
   STAMP_DECL
   STAMP(0);
@@ -1445,9 +1515,21 @@ __global__ void __launch_bounds__(NT) k_num_heavy(const HeavyItem* __restrict__ 
     const int TC = Te + NT;
     const uint32_t mult = dense ? 0u : (uint32_t)(((uint64_t)Te << 32) / (uint64_t)spn);
     Table<Acc> t{keys, vals, Te, TC};
+    // rank mode: presence bitmap of the unit's span (keys, <= T+NT words) + per-word rank directory
+    // (16-bit, in hc: <= T words) give every output row its exact slot; no probing, no sort.
+    // (values: cnt slots; bitmap: nw words right after them in the vals+keys region; directory: one
+    // 16-bit prefix per word PAIR in hc, T entries -> spans up to 64*T rows)
+    const int nw = (int)min<int64_t>((spn + 31) >> 5, 1 << 30);
+    const int cpad = (un.cnt + 1) & ~1;
+    const bool rank = CBG_RANK_MODE && !SRT::kAddIsError && !dense && un.cnt <= T &&
+                      nw <= 2 * T && (int64_t)cpad * (int64_t)sizeof(Acc) + 4LL * nw <= kRankBytes;
+    uint32_t* bm = (uint32_t*)(vals + cpad);
     if (dense) {
       for (int s = threadIdx.x; s < T / 32; s += NT) keys[s] = 0;
       for (int s = threadIdx.x; s < spn; s += NT) vals[s] = SRT::identity();
+    } else if (rank) {
+      for (int s = threadIdx.x; s < nw; s += NT) bm[s] = 0u;
+      for (int s = threadIdx.x; s < un.cnt; s += NT) vals[s] = SRT::identity();
     } else {
       for (int s = threadIdx.x; s < TC; s += NT) { keys[s] = kEmpty; vals[s] = SRT::identity(); }
       for (int s = threadIdx.x; s < (Te >> 1); s += NT) hc[s] = 0u;
@@ -1457,22 +1539,99 @@ __global__ void __launch_bounds__(NT) k_num_heavy(const HeavyItem* __restrict__ 
     STAMP(2);
     STAMP_COUNT(10, 1);
     int ovf = 0, aerr = 0;
-    for (int64_t c = 0; c < nb; c += NT) {
-      const int64_t a0 = pa0, a1 = pa1;
-      const V bv = pbv;
-      if (c + NT < nb) fetch(u, c + NT, pa0, pa1, pbv);
-      else fetch(u + 1, 0, pa0, pa1, pbv);
-      const int64_t F = stage_segments<NT, false, kGroupHeavy, V>(sb, a0, a1, bv);
-      STAMP(3);
-      STAMP_COUNT(11, 1);
-      STAMP_COUNT(12, F);
+    uint16_t* pre = (uint16_t*)hc;
+    auto mark = [&](int64_t F, int64_t c, int ns) {   // sweep 1: mark the rows (row ids only)
       expand_staged<NT, kUnrollHeavy, kGroupHeavy, V>(
-          sb, threadIdx.x, F, bs + c, (int)min<int64_t>(NT, nb - c), [&](int64_t q) { return NumItem<V>{A.ir[q], load_val(A.val, q)}; },
-          [&](const NumItem<V>& it, V bv2, int64_t q, int64_t b) {
-            num_insert<SRT, V, true>(t, dense, wk, mult, it, bv2, q, b, ovf, aerr);
+          sb, threadIdx.x, F, bs + c, ns, [&](int64_t q) { return A.ir[q]; },
+          [&](int32_t r, V, int64_t, int64_t) {
+            if (r < wk.lo || r > wk.hi) return;
+            const int o = r - wk.lo;
+            atomicOr(&bm[o >> 5], 1u << (o & 31));
           });
+    };
+    auto accum = [&](int64_t F, int64_t c, int ns) {  // sweep 2: accumulate at the exact slots
+      expand_staged<NT, kUnrollHeavy, kGroupHeavy, V>(
+          sb, threadIdx.x, F, bs + c, ns, [&](int64_t q) { return NumItem<V>{A.ir[q], load_val(A.val, q)}; },
+          [&](const NumItem<V>& it, V bv2, int64_t q, int64_t b) {
+            if (it.r < wk.lo || it.r > wk.hi) return;
+            const int o = it.r - wk.lo, w = o >> 5;
+            const int slot = (int)pre[w >> 1] + ((w & 1) ? __popc(bm[w - 1]) : 0) +
+                             __popc(bm[w] & ((1u << (o & 31)) - 1u));
+            SRT::acc(&vals[slot], SRT::mul(it.a, bv2, q, b));
+          });
+    };
+    // rank directory: exclusive popcount prefix per word pair (contiguous even word ranges per
+    // thread); false if the bitmap disagrees with the symbolic count (cannot happen: it is exact)
+    auto directory = [&]() -> bool {
+      const int WPT = (((nw + NT - 1) / NT) + 1) & ~1;
+      const int w0 = min(nw, (int)threadIdx.x * WPT), w1 = min(nw, w0 + WPT);
+      int local = 0;
+      for (int w = w0; w < w1; ++w) local += __popc(bm[w]);
+      int tot;
+      int run = block_excl_scan<NT>(local, misc + 8, &tot);
+      for (int w = w0; w < w1; ++w) {
+        if (!(w & 1)) pre[w >> 1] = (uint16_t)run;
+        run += __popc(bm[w]);
+      }
       __syncthreads();
-      STAMP(4);
+      return tot == un.cnt;
+    };
+    // a multi-chunk rank unit streams its segments twice (mark pass, then accumulate pass); a
+    // single-chunk one stages them once and runs both sweeps on the staged chunk
+    const bool multi = rank && nb > NT;
+    for (int pass = 0; pass < (multi ? 2 : 1); ++pass) {
+      for (int64_t c = 0; c < nb; c += NT) {
+        const int64_t a0 = pa0, a1 = pa1;
+        const V bv = pbv;
+        if (c + NT < nb) fetch(u, c + NT, pa0, pa1, pbv);
+        else if (multi && pass == 0) fetch(u, 0, pa0, pa1, pbv);
+        else fetch(u + 1, 0, pa0, pa1, pbv);
+        const int64_t F = stage_segments<NT, false, kGroupHeavy, V>(sb, a0, a1, bv);
+        const int ns = (int)min<int64_t>(NT, nb - c);
+        STAMP(3);
+        STAMP_COUNT(11, 1);
+        STAMP_COUNT(12, F);
+        if (!rank) {
+          expand_staged<NT, kUnrollHeavy, kGroupHeavy, V>(
+              sb, threadIdx.x, F, bs + c, ns, [&](int64_t q) { return NumItem<V>{A.ir[q], load_val(A.val, q)}; },
+              [&](const NumItem<V>& it, V bv2, int64_t q, int64_t b) {
+                num_insert<SRT, V, true>(t, dense, wk, mult, it, bv2, q, b, ovf, aerr);
+              });
+        } else if (!multi && F <= (int64_t)NT * kUnrollHeavy * CBG_RANK_REGS) {
+          const bool ok = expand_staged_twice<NT, kUnrollHeavy, kGroupHeavy, CBG_RANK_REGS, V>(
+              sb, threadIdx.x, F, bs + c, ns, [&](int64_t q) { return NumItem<V>{A.ir[q], load_val(A.val, q)}; },
+              [&](const NumItem<V>& it) {
+                if (it.r < wk.lo || it.r > wk.hi) return;
+                const int o = it.r - wk.lo;
+                atomicOr(&bm[o >> 5], 1u << (o & 31));
+              },
+              [&]() { __syncthreads(); return directory(); },
+              [&](const NumItem<V>& it, V bv2, int64_t q, int64_t b) {
+                if (it.r < wk.lo || it.r > wk.hi) return;
+                const int o = it.r - wk.lo, w = o >> 5;
+                const int slot = (int)pre[w >> 1] + ((w & 1) ? __popc(bm[w - 1]) : 0) +
+                                 __popc(bm[w] & ((1u << (o & 31)) - 1u));
+                SRT::acc(&vals[slot], SRT::mul(it.a, bv2, q, b));
+              });
+          if (!ok) ovf = 1;
+        } else if (!multi) {
+          mark(F, c, ns);
+          __syncthreads();
+          if (directory()) accum(F, c, ns);
+          else ovf = 1;
+        } else if (pass == 0) {
+          mark(F, c, ns);
+        } else {
+          accum(F, c, ns);
+        }
+        __syncthreads();
+        STAMP(4);
+      }
+      if (multi && pass == 0 && !directory()) {
+        ovf = 1;
+        fetch(u + 1, 0, pa0, pa1, pbv);   // the prefetched chunk was this unit's: take the next unit's
+        break;
+      }
     }
     if (ovf) misc[1] = 1;
     if (aerr) misc[2] = 1;
@@ -1495,6 +1654,21 @@ __global__ void __launch_bounds__(NT) k_num_heavy(const HeavyItem* __restrict__ 
         out.val[ob + o] = SRT::out(vals[rr], A.val, B.val);
         ++o;
       }
+    } else if (rank) {
+      // rows: word w's set bits go to pre[w].. in bit order (interleaved words: neighbouring lanes
+      // write neighbouring positions); values: the slot array is already in row order
+      const uint16_t* pre = (const uint16_t*)hc;
+      for (int w = threadIdx.x; w < nw; w += NT) {
+        uint32_t wd = bm[w];
+        int o = (int)pre[w >> 1] + ((w & 1) ? __popc(bm[w - 1]) : 0);
+        while (wd) {
+          const int bpos = __ffs(wd) - 1;
+          wd &= wd - 1;
+          out.row[ob + o] = wk.lo + w * 32 + bpos;
+          ++o;
+        }
+      }
+      for (int i = threadIdx.x; i < un.cnt; i += NT) out.val[ob + i] = SRT::out(vals[i], A.val, B.val);
     } else {
       STAMP(7);
       compact_hash_homes<SRT, V, NT, T / NT + 1>(keys, vals, TC, Te, wk.lo, mult, hc, misc + 8, ob,

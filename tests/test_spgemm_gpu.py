@@ -258,7 +258,11 @@ def test_gpu_unit_overflow_fallback(gpu_ctx):
     n = 1 << 20
     A = Csc(n, 1, [0, len(rows)], rows, np.arange(1, len(rows) + 1, dtype=np.float64))
     B = Csc(1, 1, [0, 1], [0], np.array([2.0]))
+    # PlusTimes takes the rank mode (exact slots: no hash, nothing overflows)
     _check_vs_oracle(gpu_ctx, A, B)
+    assert gpu_ctx.last_profile()["bins"][12] == 1          # one heavy column
+    # BoolCopy semirings keep the hash mode (it detects a second contribution): overflow + dense re-run
+    _check_vs_oracle(gpu_ctx, A, B, sr="bool_copy1st")
     prof = gpu_ctx.last_profile()
     assert prof["bins"][12] == 1          # one heavy column
     assert prof["bins"][14] >= 1          # at least one unit re-run densely
