@@ -61,7 +61,7 @@ constexpr int64_t kHeavy = 4096;   // nnz(C(:,j)) above which a column is split 
 #define CBG_HEAVY_NT 1024
 #endif
 #ifndef CBG_ITEM_UNITS
-#define CBG_ITEM_UNITS 8
+#define CBG_ITEM_UNITS 4
 #endif
 // k_num_heavy rank mode: single-chunk units whose span fits a 32*T-row bitmap get exact slots
 #ifndef CBG_RANK_MODE
@@ -71,12 +71,12 @@ constexpr int64_t kHeavy = 4096;   // nnz(C(:,j)) above which a column is split 
 #ifndef CBG_RANK_REGS
 #define CBG_RANK_REGS 4
 #endif
-// units also end where their span would exceed the rank-mode bitmap (32*T rows)
+// units also end before their row span exceeds CBG_RANK_SPAN_CAP rows (0 = no span limit)
 #ifndef CBG_RANK_SPAN_CAP
-#define CBG_RANK_SPAN_CAP 0
+#define CBG_RANK_SPAN_CAP 425984   // f64, T=8192, NT=1024, unit cap 7168: (9216*12 - 7168*8)/4 words
 #endif
 #ifndef CBG_UNIT_CAP
-#define CBG_UNIT_CAP (1 << (CBG_HEAVY_LOGT - 1))
+#define CBG_UNIT_CAP (7 << (CBG_HEAVY_LOGT - 3))   // rank mode holds up to T outputs; 7/8 T measured best
 #endif
 constexpr int64_t kUnitCap = CBG_UNIT_CAP;   // max outputs of a multi-subwindow unit (load <= kUnitCap/T)
 constexpr int kSplitMin = 16;      // A columns at least this long get split-table rows
@@ -448,37 +448,33 @@ __device__ __forceinline__ void expand_staged(const SegBuf<V>& sb, int tid, int6
   }
 }
 
-// Two sweeps over one staged chunk with the loaded items kept in registers (F <= NT*U*RI groups):
-// load every item once, mark(item) each, then mid() (block-uniform: barrier + whatever must see all
-// marks; false aborts), then acc(item, bv, q, b) each -- the rank mode's mark and accumulate sweeps
-// without gathering A twice.
-template <int NT, int U, int G, int RI, typename V, class LdF, class MarkF, class MidF, class AccF>
+// Two sweeps over one staged chunk (F <= NT*U*RI groups) with the row ids kept in registers:
+// sweep 1 gathers the rows (ldr) and mark(row)s them; mid() (block-uniform: barrier + whatever must
+// see all marks; false aborts); sweep 2 gathers the values (ldv) and acc(row, value, bv, q, b)s --
+// the rank mode's two sweeps with each A entry's row and value gathered once.  Only the rows and a
+// packed (segment, count) word per group stay live across mid(); q is recomputed from LDS.
+template <int NT, int U, int G, int RI, typename V, class LdR, class LdV, class MarkF, class MidF, class AccF>
 __device__ __forceinline__ bool expand_staged_twice(const SegBuf<V>& sb, int tid, int64_t F, int64_t base, int nseg,
-                                                    LdF ld, MarkF mark, MidF mid, AccF acc) {
-  using Item = decltype(ld(int64_t(0)));
+                                                    LdR ldr, LdV ldv, MarkF mark, MidF mid, AccF acc) {
   int P = 1;
   while (P < nseg) P <<= 1;
-  Item it[RI][U][G];
-  int ss[RI][U];
-  int64_t qq[RI][U];
-  int nv[RI][U];
+  int32_t rr[RI][U][G];
+  int sn[RI][U];   // segment << 8 | count (count <= G), 0 = no group
 #pragma unroll
   for (int r = 0; r < RI; ++r)
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int64_t g = (int64_t)(r * U + u) * NT + tid;
-      nv[r][u] = 0;
-      ss[r][u] = 0;
-      qq[r][u] = 0;
+      sn[r][u] = 0;
       if (g < F) {
         const int sg = seg_search<NT>(sb.off, g, P);
         const int64_t k0 = (g - sb.off[sg]) * G;
-        ss[r][u] = sg;
-        qq[r][u] = sb.qb[sg] + k0;
-        nv[r][u] = (int)min<int64_t>(G, sb.len[sg] - k0);
+        const int64_t q = sb.qb[sg] + k0;
+        const int nv = (int)min<int64_t>(G, sb.len[sg] - k0);
+        sn[r][u] = (sg << 8) | nv;
 #pragma unroll
         for (int i = 0; i < G; ++i)
-          if (i < nv[r][u]) it[r][u][i] = ld(qq[r][u] + i);
+          if (i < nv) rr[r][u][i] = ldr(q + i);
       }
     }
 #pragma unroll
@@ -487,18 +483,27 @@ __device__ __forceinline__ bool expand_staged_twice(const SegBuf<V>& sb, int tid
     for (int u = 0; u < U; ++u)
 #pragma unroll
       for (int i = 0; i < G; ++i)
-        if (i < nv[r][u]) mark(it[r][u][i]);
+        if (i < (sn[r][u] & 0xff)) mark(rr[r][u][i]);
   if (!mid()) return false;
 #pragma unroll
   for (int r = 0; r < RI; ++r)
 #pragma unroll
-    for (int u = 0; u < U; ++u)
-      if (nv[r][u] > 0) {
-        const V bv = sb.bv[ss[r][u]];
+    for (int u = 0; u < U; ++u) {
+      const int nv = sn[r][u] & 0xff;
+      if (nv > 0) {
+        const int sg = sn[r][u] >> 8;
+        const int64_t g = (int64_t)(r * U + u) * NT + tid;
+        const int64_t q = sb.qb[sg] + (g - sb.off[sg]) * G;
+        const V bv = sb.bv[sg];
+        V av[G];
 #pragma unroll
         for (int i = 0; i < G; ++i)
-          if (i < nv[r][u]) acc(it[r][u][i], bv, qq[r][u] + i, base + ss[r][u]);
+          if (i < nv) av[i] = ldv(q + i);
+#pragma unroll
+        for (int i = 0; i < G; ++i)
+          if (i < nv) acc(rr[r][u][i], av[i], bv, q + i, base + sg);
       }
+    }
   return true;
 }
 
@@ -981,7 +986,7 @@ __global__ void k_build_units(int H, const int32_t* __restrict__ cols, const int
   };
   for (int32_t s = sf; s <= sl; ++s) {
     const int64_t n = c[s];
-    const bool wide = CBG_RANK_SPAN_CAP && (((int64_t)(s + 1 - st) << log) > (32LL << CBG_HEAVY_LOGT));
+    const bool wide = CBG_RANK_SPAN_CAP > 0 && (((int64_t)(s + 1 - st) << log) > (int64_t)CBG_RANK_SPAN_CAP);
     if (acc > 0 && (acc + n > kUnitCap || wide)) {
       emit(st, s, acc);
       st = s;
@@ -1599,19 +1604,20 @@ __global__ void __launch_bounds__(NT) k_num_heavy(const HeavyItem* __restrict__ 
               });
         } else if (!multi && F <= (int64_t)NT * kUnrollHeavy * CBG_RANK_REGS) {
           const bool ok = expand_staged_twice<NT, kUnrollHeavy, kGroupHeavy, CBG_RANK_REGS, V>(
-              sb, threadIdx.x, F, bs + c, ns, [&](int64_t q) { return NumItem<V>{A.ir[q], load_val(A.val, q)}; },
-              [&](const NumItem<V>& it) {
-                if (it.r < wk.lo || it.r > wk.hi) return;
-                const int o = it.r - wk.lo;
+              sb, threadIdx.x, F, bs + c, ns, [&](int64_t q) { return A.ir[q]; },
+              [&](int64_t q) { return load_val(A.val, q); },
+              [&](int32_t r) {
+                if (r < wk.lo || r > wk.hi) return;
+                const int o = r - wk.lo;
                 atomicOr(&bm[o >> 5], 1u << (o & 31));
               },
               [&]() { __syncthreads(); return directory(); },
-              [&](const NumItem<V>& it, V bv2, int64_t q, int64_t b) {
-                if (it.r < wk.lo || it.r > wk.hi) return;
-                const int o = it.r - wk.lo, w = o >> 5;
+              [&](int32_t r, V a, V bv2, int64_t q, int64_t b) {
+                if (r < wk.lo || r > wk.hi) return;
+                const int o = r - wk.lo, w = o >> 5;
                 const int slot = (int)pre[w >> 1] + ((w & 1) ? __popc(bm[w - 1]) : 0) +
                                  __popc(bm[w] & ((1u << (o & 31)) - 1u));
-                SRT::acc(&vals[slot], SRT::mul(it.a, bv2, q, b));
+                SRT::acc(&vals[slot], SRT::mul(a, bv2, q, b));
               });
           if (!ok) ovf = 1;
         } else if (!multi) {
