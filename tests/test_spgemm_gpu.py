@@ -290,6 +290,35 @@ def test_gpu_heavy_units_many_columns(gpu_ctx):
     assert gpu_ctx.last_profile()["bins"][12] > 0
 
 
+@pytest.mark.parametrize("sr,dt", [("plus_times", "f64"), ("min_plus", "i64"), ("select2nd", "i64"),
+                                   ("select_max", "i64"), ("bool_copy2nd", "f64")])
+def test_gpu_heavy_rank_mode_multichunk(gpu_ctx, sr, dt):
+    """Heavy columns whose B column holds > 1024 nonzeros (the rank mode streams the unit's segments
+    twice: mark pass, accumulate pass), spans below and above the rank-mode limit, plus a column
+    whose units are single-chunk.  BoolCopy2nd keeps the hash mode (A columns have disjoint rows,
+    so no output gets a second contribution)."""
+    rng = np.random.default_rng(23)
+    n = 1 << 20
+    ncolA = 6000
+    if sr == "bool_copy2nd":   # disjoint rows per A column -> each output has exactly one product
+        perm = rng.permutation(n)[: ncolA * 2]
+        cols = [np.sort(perm[2 * k: 2 * k + 2]).astype(np.int32) for k in range(ncolA)]
+    else:
+        hi = np.where(np.arange(ncolA) < 3000, 300_000, n)   # first half: narrow span, second: full
+        cols = [np.sort(rng.choice(int(hi[k]), int(rng.integers(1, 6)), replace=False)).astype(np.int32)
+                for k in range(ncolA)]
+    cp = np.r_[0, np.cumsum([len(c) for c in cols])]
+    A = Csc(n, ncolA, cp, np.concatenate(cols), rng.integers(1, 9, cp[-1]).astype(np.float64 if dt == "f64" else np.int64))
+    pick = [np.arange(0, 3000, dtype=np.int32),                      # nb = 3000, span <= 300k rows
+            np.arange(3000, 6000, 2, dtype=np.int32),                # nb = 1500, full span
+            np.sort(rng.choice(3000, 900, replace=False)).astype(np.int32)]   # single chunk
+    bcp = np.r_[0, np.cumsum([len(x) for x in pick])]
+    B = Csc(ncolA, len(pick), bcp, np.concatenate(pick),
+            rng.integers(1, 9, bcp[-1]).astype(np.float64 if dt == "f64" else np.int64))
+    _check_vs_oracle(gpu_ctx, A, B, sr, dt)
+    assert gpu_ctx.last_profile()["bins"][12] >= 1   # heavy columns present
+
+
 @pytest.mark.parametrize("sr,dt", [("plus_times", "f64"), ("plus_times", "i64"), ("min_plus", "i64"),
                                    ("select2nd", "i64"), ("select_max", "f64")])
 @pytest.mark.parametrize("nparts", [1, 2, 4])
