@@ -43,10 +43,10 @@ constexpr int kLong = 64;          // k_window: segment length handed to a whole
 constexpr int kUnroll = 2;         // groups of G multiplies in flight per lane (numeric)
 constexpr int kUnrollSym = 2;      // same, symbolic (4-byte items)
 #ifndef CBG_UNROLL_HEAVY
-#define CBG_UNROLL_HEAVY 2
+#define CBG_UNROLL_HEAVY 1
 #endif
 #ifndef CBG_GROUP_HEAVY
-#define CBG_GROUP_HEAVY 2
+#define CBG_GROUP_HEAVY 4
 #endif
 constexpr int kUnrollHeavy = CBG_UNROLL_HEAVY;    // same, k_num_heavy
 constexpr int kGroupSym = 4;       // consecutive A entries per lane group (one segment search each), symbolic
@@ -69,7 +69,7 @@ constexpr int64_t kHeavy = 4096;   // nnz(C(:,j)) above which a column is split 
 #endif
 // rank mode: register-resident sweeps for chunks of <= NT*U*CBG_RANK_REGS groups
 #ifndef CBG_RANK_REGS
-#define CBG_RANK_REGS 4
+#define CBG_RANK_REGS 6
 #endif
 // units also end before their row span exceeds CBG_RANK_SPAN_CAP rows (0 = no span limit)
 #ifndef CBG_RANK_SPAN_CAP
