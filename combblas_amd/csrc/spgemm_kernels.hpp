@@ -73,10 +73,10 @@ constexpr int64_t kHeavy = 4096;   // nnz(C(:,j)) above which a column is split 
 #endif
 // units also end before their row span exceeds CBG_RANK_SPAN_CAP rows (0 = no span limit)
 #ifndef CBG_RANK_SPAN_CAP
-#define CBG_RANK_SPAN_CAP 425984   // f64, T=8192, NT=1024, unit cap 7168: (9216*12 - 7168*8)/4 words
+#define CBG_RANK_SPAN_CAP 458752   // f64, T=8192, NT=1024, unit cap 6144: <= (9216*12 - 6144*8)/4 words
 #endif
 #ifndef CBG_UNIT_CAP
-#define CBG_UNIT_CAP (7 << (CBG_HEAVY_LOGT - 3))   // rank mode holds up to T outputs; 7/8 T measured best
+#define CBG_UNIT_CAP (3 << (CBG_HEAVY_LOGT - 2))   // rank mode holds up to T outputs; 3/4 T measured best
 #endif
 constexpr int64_t kUnitCap = CBG_UNIT_CAP;   // max outputs of a multi-subwindow unit (load <= kUnitCap/T)
 constexpr int kSplitMin = 16;      // A columns at least this long get split-table rows
