@@ -74,13 +74,19 @@ def col_flops(cp, ir):
     return csum[cp[1:]] - csum[cp[:-1]]
 
 
-def cpu_baseline(cp, ir, val, n, flop_col, target_mults):
-    """Oracle (CPU restatement, oracle/oracle.c) on a bounded sample: every s-th column of B."""
-    sys.path.insert(0, os.path.join(HERE, "tests"))
-    from helpers import Csc, oracle_spgemm  # test infrastructure: checker/baseline only
+def sample_columns(n, flop_col, target_mults):
+    """Every s-th column of B, s chosen so the sample holds about target_mults multiplies."""
     tot = int(flop_col.sum())
     stride = max(1, int(np.ceil(tot / max(target_mults, 1))))
-    cols = np.arange(0, n, stride)
+    return np.arange(0, n, stride), stride
+
+
+def cpu_baseline(cp, ir, val, n, flop_col, target_mults):
+    """Oracle (CPU restatement, oracle/oracle.c) on a bounded sample: every s-th column of B.
+    Returns (baseline JSON, the oracle's product of the sampled columns)."""
+    sys.path.insert(0, os.path.join(HERE, "tests"))
+    from helpers import Csc, oracle_spgemm  # test infrastructure: checker/baseline only
+    cols, stride = sample_columns(n, flop_col, target_mults)
     bcp = np.concatenate([[0], np.cumsum(np.diff(cp)[cols])]).astype(np.int64)
     idx = np.concatenate([np.arange(cp[c], cp[c + 1]) for c in cols]) if len(cols) else np.zeros(0, np.int64)
     A = Csc(n, n, cp, ir, val)
@@ -90,9 +96,21 @@ def cpu_baseline(cp, ir, val, n, flop_col, target_mults):
     C, mults, rc = oracle_spgemm(A, B, "plus_times", "f64")
     dt = time.perf_counter() - t0
     assert rc == 0
-    return {"value": mults / dt, "unit": "multiplies/s", "cores": threads, "kind": "port",
-            "sample": f"oracle/oracle.c (CPU restatement of LocalSpGEMMHash, OpenMP, {threads} threads) on "
-                      f"every {stride}-th column of B ({len(cols)} columns, {mults} multiplies, {dt:.2f} s)"}
+    return ({"value": mults / dt, "unit": "multiplies/s", "cores": threads, "kind": "port",
+             "sample": f"oracle/oracle.c (CPU restatement of LocalSpGEMMHash, OpenMP, {threads} threads) on "
+                       f"every {stride}-th column of B ({len(cols)} columns, {mults} multiplies, {dt:.2f} s)"},
+            (cols, C))
+
+
+def verify_sample(Cdev, cols, R):
+    """Bit-exact check of the benchmarked product on the sampled columns against the oracle's product
+    of the same columns (R-MAT values are multiplicities, so PlusTimes<double> sums are exact)."""
+    S = Cdev.select_columns(cols)
+    scp, sir, sval = S.to_host()
+    S.free()
+    ok = bool(np.array_equal(scp, R.cp) and np.array_equal(sir, R.ir) and np.array_equal(sval, R.val))
+    return {"columns": int(len(cols)), "nnz": int(R.cp[-1]), "bit_exact": ok,
+            "against": "oracle/oracle.c product of the cpu_baseline sample columns"}
 
 
 def workload(scale, edgefactor, parallelism):
@@ -114,7 +132,7 @@ def bench_local(args):
     lib = ctx._lib
     keep = {}
 
-    def step(keep_colptr=False):
+    def step(keep_colptr=False, keep_result=False):
         res = _abi.CscResult()
         m = ctypes.c_int64()
         _abi.check(lib.cbg_spgemm_local(ctx._ptr, ctypes.byref(va), ctypes.byref(va), _abi.SR_PLUS_TIMES,
@@ -126,7 +144,10 @@ def bench_local(args):
             _abi.check(lib.cbg_result_to_host(ctx._ptr, ctypes.byref(res), ccp.ctypes.data, None, None))
             keep["cp"] = ccp
         nnzc = int(res.nnz)
-        lib.cbg_result_free(ctx._ptr, ctypes.byref(res))
+        if keep_result:   # the last timed product is kept for the parity check (no extra work timed)
+            keep["C"] = cb.SpDCCols._from_result(ctx, res)
+        else:
+            lib.cbg_result_free(ctx._ptr, ctypes.byref(res))
         return int(m.value), nnzc, prof
 
     for w in range(max(args.warmup, 1)):
@@ -135,8 +156,8 @@ def bench_local(args):
     t0 = time.perf_counter()
     mults = nnzc = 0
     profs = []
-    for _ in range(args.steps):
-        m, z, prof = step()
+    for s in range(args.steps):
+        m, z, prof = step(keep_result=(s == args.steps - 1))
         mults += m
         nnzc += z
         profs.append(prof)
@@ -168,8 +189,12 @@ def bench_local(args):
                      "heavy_nnz_C": int(nnz_c_col[heavy].sum())},
     }
     if not args.no_cpu:
-        out["cpu_baseline"] = cpu_baseline(cp, ir, val, n, flop_col, args.cpu_mults)
+        out["cpu_baseline"], (cols, R) = cpu_baseline(cp, ir, val, n, flop_col, args.cpu_mults)
+        out["verified"] = verify_sample(keep["C"], cols, R)
+    keep.pop("C").free()
     print(json.dumps(out), flush=True)
+    if not args.no_cpu and not out["verified"]["bit_exact"]:
+        sys.exit("bench: the benchmarked product differs from the oracle on the sampled columns")
 
 
 # ------------------------------------------------------------------------------------------ N > 1

@@ -220,6 +220,14 @@ class SpDCCols:
                    "cbg_result_to_host")
         return cp, ir[:n], (None if val is None else val[:n])
 
+    def select_columns(self, cols):
+        """Columns `cols` (any order) as a new device matrix (cbg_col_select)."""
+        c = np.ascontiguousarray(cols, np.int64)
+        res = _abi.CscResult()
+        _abi.check(self._ctx._lib.cbg_col_select(self._ctx._ptr, ctypes.byref(self._res), c.ctypes.data, len(c),
+                                                 ctypes.byref(res)), "cbg_col_select")
+        return SpDCCols._from_result(self._ctx, res)
+
     def free(self):
         if self._res is not None and self._res._owner:
             self._ctx._lib.cbg_result_free(self._ctx._ptr, ctypes.byref(self._res))

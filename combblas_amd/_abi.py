@@ -80,6 +80,8 @@ SIGNATURES = {
                                      ctypes.POINTER(CscResult)]),
     "cbg_col_concat": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(CscResult), ctypes.c_int32,
                                       ctypes.POINTER(CscResult)]),
+    "cbg_col_select": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(CscResult), ctypes.c_void_p, ctypes.c_int64,
+                                      ctypes.POINTER(CscResult)]),
 }
 
 _lib = None

@@ -260,6 +260,27 @@ __global__ void k_col_rebase(int64_t n, const int64_t* __restrict__ cp, int64_t 
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i <= n; i += (int64_t)gridDim.x * blockDim.x)
     out[i] = cp[c0 + i] - base;
 }
+// column subset: cnt[i] = nnz of column cols[i]
+__global__ void k_sel_count(int64_t n, const int64_t* __restrict__ cp, const int64_t* __restrict__ cols,
+                            int64_t* __restrict__ cnt) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    cnt[i] = cp[cols[i] + 1] - cp[cols[i]];
+}
+// one wavefront per selected column copies its rows and values
+template <typename T>
+__global__ void __launch_bounds__(256) k_sel_copy(int64_t n, const int64_t* __restrict__ cp,
+                                                  const int32_t* __restrict__ ir, const T* __restrict__ val,
+                                                  const int64_t* __restrict__ cols, const int64_t* __restrict__ ocp,
+                                                  int32_t* __restrict__ oir, T* __restrict__ oval) {
+  const int w = threadIdx.x / kWave, l = lane_id();
+  for (int64_t i = blockIdx.x * 4 + w; i < n; i += (int64_t)gridDim.x * 4) {
+    const int64_t s = cp[cols[i]], len = cp[cols[i] + 1] - s, o = ocp[i];
+    for (int64_t e = l; e < len; e += kWave) {
+      oir[o + e] = ir[s + e];
+      if (val) oval[o + e] = val[s + e];
+    }
+  }
+}
 // colptr of part q appended at column offset `coff` and entry offset `eoff`
 __global__ void k_col_shift(int64_t n, const int64_t* __restrict__ cp, int64_t eoff, int64_t* __restrict__ out) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i <= n; i += (int64_t)gridDim.x * blockDim.x)
@@ -365,6 +386,59 @@ extern "C" cbg_status cbg_col_range(cbg_ctx* ctx, const cbg_csc_result* in, int6
   out->nrow = in->nrow; out->ncol = n; out->nnz = nnz;
   out->colptr = own->cp.as<int64_t>(); out->row = own->ir.as<int32_t>(); out->val = vs ? own->val.p : nullptr;
   out->val_type = in->val_type;
+  out->_owner = own.release();
+  return CBG_OK;
+}
+
+extern "C" cbg_status cbg_col_select(cbg_ctx* ctx, const cbg_csc_result* in, const int64_t* cols, int64_t ncols,
+                                     cbg_csc_result* out) {
+  if (!ctx || !in || !out || (ncols > 0 && !cols) || ncols < 0) return CBG_EINVAL;
+  for (int64_t i = 0; i < ncols; ++i)
+    if (cols[i] < 0 || cols[i] >= in->ncol) return CBG_EDIM;
+  HIPCHK(hipSetDevice(ctx->device));
+  hipStream_t st = ctx->stream;
+  const size_t vs = in->val ? dt_size(in->val_type) : 0;
+  std::unique_ptr<Owner> own(new Owner(ctx->pool));
+  HIPCHK(own->cp.reserve(sizeof(int64_t) * (ncols + 1)));
+  DevBuf dcols, cnt, tiles;
+  HIPCHK(dcols.reserve(sizeof(int64_t) * (ncols + 1)));
+  HIPCHK(cnt.reserve(sizeof(int64_t) * (ncols + 1)));
+  HIPCHK(ctx->scalars.reserve(256));
+  int64_t nnz = 0;
+  if (ncols > 0) {
+    HIPCHK(hipMemcpyAsync(dcols.p, cols, sizeof(int64_t) * ncols, hipMemcpyHostToDevice, st));
+    k_sel_count<<<(int)grid_for(ncols, 256, kMaxGrid), 256, 0, st>>>(ncols, in->colptr, dcols.as<int64_t>(),
+                                                                     cnt.as<int64_t>());
+    const int64_t ntiles = (ncols + kScanTile - 1) / kScanTile;
+    HIPCHK(tiles.reserve(sizeof(int64_t) * (ntiles + 1)));
+    int64_t* tot = (int64_t*)ctx->scalars.p;
+    k_scan_tiles<<<(int)ntiles, 256, 0, st>>>(ncols, cnt.as<int64_t>(), tiles.as<int64_t>());
+    k_scan_sums<<<1, 1024, 0, st>>>(ntiles, tiles.as<int64_t>(), tot);
+    k_scan_apply<<<(int)ntiles, 256, 0, st>>>(ncols, cnt.as<int64_t>(), tiles.as<int64_t>(), own->cp.as<int64_t>());
+    HIPCHK(hipMemcpyAsync(&nnz, tot, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+  } else {
+    HIPCHK(hipMemsetAsync(own->cp.p, 0, sizeof(int64_t), st));
+  }
+  HIPCHK(own->ir.reserve(sizeof(int32_t) * (nnz + 1)));
+  HIPCHK(own->val.reserve(vs * (nnz + 1) + 8));
+  if (nnz > 0) {
+    const int g = (int)grid_for(ncols, 4, kMaxGrid * 2);
+    const int64_t* c = dcols.as<int64_t>();
+    int64_t* ocp = own->cp.as<int64_t>();
+    int32_t* oir = own->ir.as<int32_t>();
+    switch (vs) {
+      case 1: k_sel_copy<uint8_t><<<g, 256, 0, st>>>(ncols, in->colptr, in->row, (const uint8_t*)in->val, c, ocp, oir, (uint8_t*)own->val.p); break;
+      case 4: k_sel_copy<uint32_t><<<g, 256, 0, st>>>(ncols, in->colptr, in->row, (const uint32_t*)in->val, c, ocp, oir, (uint32_t*)own->val.p); break;
+      default: k_sel_copy<uint64_t><<<g, 256, 0, st>>>(ncols, in->colptr, in->row, (const uint64_t*)in->val, c, ocp, oir, (uint64_t*)own->val.p); break;
+    }
+  }
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(st));   // dcols/cnt/tiles are freed on return
+  memset(out, 0, sizeof(*out));
+  out->nrow = in->nrow; out->ncol = ncols; out->nnz = nnz;
+  out->colptr = own->cp.as<int64_t>(); out->row = own->ir.as<int32_t>(); out->val = vs ? own->val.p : nullptr;
+  out->val_type = in->val_type; out->multiplies = in->multiplies;
   out->_owner = own.release();
   return CBG_OK;
 }

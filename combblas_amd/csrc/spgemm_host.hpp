@@ -347,6 +347,8 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
   memset(&pf, 0, sizeof(pf));
   if (Av->ncol != Bv->nrow) return CBG_EDIM;
   const int64_t M = Av->nrow, N = Bv->ncol;
+  // Select2nd / BoolCopy2nd accumulate the (int32) position of the contributing B nonzero
+  if (SRT::kNeedsBPos && Bv->nnz >= (int64_t)INT32_MAX) return CBG_EUNSUP;
 
   std::unique_ptr<Owner> own(new Owner(ctx->pool));
   memset(C, 0, sizeof(*C));
@@ -511,7 +513,8 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
     HIPCHK(ctx->icnt.reserve(sizeof(int64_t) * (H + 1)));
     HIPCHK(ctx->itemoff.reserve(sizeof(int64_t) * (H + 1)));
     k_build_units<<<(H + 255) / 256, 256, 0, st>>>(H, ctx->heavy_cols.as<int32_t>(), ctx->sub.as<int32_t>(), nsub,
-                                                   slog, span, colptr, B.cp, units, ctx->ucnt.as<int64_t>(),
+                                                   slog, heavy_unit_cap<SRT>(), heavy_span_cap<SRT>(), span,
+                                                   colptr, B.cp, units, ctx->ucnt.as<int64_t>(),
                                                    ctx->uspan.as<int2>(), nnz, ctx->nunits.as<int32_t>(),
                                                    ctx->segsz.as<int64_t>(), ctx->icnt.as<int64_t>());
     // offsets of every heavy column's block of (unit, B nonzero) segments; total -> sc[8]

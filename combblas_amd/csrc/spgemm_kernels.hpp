@@ -953,9 +953,31 @@ __global__ void __launch_bounds__(256) k_split_fill(int nlong, const int32_t* __
     for (int s = l; s <= nsub; s += kWave) t[s] = (int32_t)(lower_bound_rows(Air, c0, c1, (int64_t)s << log) - c0);
   }
 }
-// units of a heavy column: consecutive subwindows while the running count stays <= kUnitCap
+// Unit caps per semiring.  Rank mode (k_num_heavy) needs cnt*sizeof(Acc) value slots plus a
+// span/32-word bitmap inside the (T+NT)*(sizeof(Acc)+4)-byte vals+keys region, and at most 2T
+// bitmap words (one 16-bit directory entry per word pair): span <= 8*((T+NT)*(sA+4) - cap*sA).
+// A semiring without rank mode (BoolCopy: its hash detects a second contribution) caps units at T/2
+// outputs so the order-preserving hash keeps load <= 1/2.
+template <class SRT>
+constexpr int64_t heavy_unit_cap() {
+  return SRT::kAddIsError || !CBG_RANK_MODE ? (int64_t)(1 << CBG_HEAVY_LOGT) / 2 : kUnitCap;
+}
+template <class SRT>
+constexpr int64_t heavy_span_cap() {
+  constexpr int64_t T = 1 << CBG_HEAVY_LOGT, NT = CBG_HEAVY_NT, sA = sizeof(typename SRT::Acc);
+  constexpr int64_t fit = 8 * ((T + NT) * (sA + 4) - kUnitCap * sA);
+  constexpr int64_t dir = 64 * T;
+  constexpr int64_t cap = fit < dir ? fit : dir;
+  if (SRT::kAddIsError || !CBG_RANK_MODE || CBG_RANK_SPAN_CAP <= 0) return 0;
+  return CBG_RANK_SPAN_CAP < cap ? CBG_RANK_SPAN_CAP : cap;
+}
+
+// units of a heavy column: consecutive subwindows while the running count stays <= unit_cap
+// unit_cap / span_cap come from the semiring (heavy_unit_caps): rank-mode accumulators hold up to
+// kUnitCap outputs over a bounded span; hash-only semirings (BoolCopy) keep load <= 1/2.
 __global__ void k_build_units(int H, const int32_t* __restrict__ cols, const int32_t* __restrict__ sub, int32_t nsub,
-                              int32_t log, const int2* __restrict__ span, const int64_t* __restrict__ colptr,
+                              int32_t log, int64_t unit_cap, int64_t span_cap,
+                              const int2* __restrict__ span, const int64_t* __restrict__ colptr,
                               const int64_t* __restrict__ Bcp, Unit* __restrict__ units, int64_t* __restrict__ ucnt,
                               int2* __restrict__ uspan, int64_t* __restrict__ nnz, int32_t* __restrict__ nunits,
                               int64_t* __restrict__ segsz, int64_t* __restrict__ icnt) {
@@ -986,8 +1008,9 @@ __global__ void k_build_units(int H, const int32_t* __restrict__ cols, const int
   };
   for (int32_t s = sf; s <= sl; ++s) {
     const int64_t n = c[s];
-    const bool wide = CBG_RANK_SPAN_CAP > 0 && (((int64_t)(s + 1 - st) << log) > (int64_t)CBG_RANK_SPAN_CAP);
-    if (acc > 0 && (acc + n > kUnitCap || wide)) {
+    if (acc == 0) st = s;   // a unit starts at its first non-empty subwindow (empty gaps span nothing)
+    const bool wide = span_cap > 0 && (((int64_t)(s + 1 - st) << log) > span_cap);
+    if (acc > 0 && (acc + n > unit_cap || wide)) {
       emit(st, s, acc);
       st = s;
       acc = 0;

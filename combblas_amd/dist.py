@@ -620,8 +620,6 @@ def MCLPruneRecoverySelect(A, hardThreshold, selectNum, recoverNum, recoverPct, 
     Columns are completed along the processor column (one all-to-all each way), pruned on device
     (backend.mcl_prune = cbg_mcl_prune), and returned.  Returns the global branch counts."""
     g, be = A.grid, A.backend
-    if recoverPct > 1:
-        recoverPct = recoverPct / 100.0
     if g.q == 1:
         P, st = be.mcl_prune(A.block, hardThreshold, selectNum, recoverNum, recoverPct)
         A.block = P

@@ -33,8 +33,6 @@ def MCLPruneRecoverySelect(A, hardThreshold, selectNum, recoverNum, recoverPct, 
     """Prune A (a local SpDCCols / SpTuples holding complete columns) in place, as ParFriends.h:185-353.
     kselectVersion only picks the reference's CPU selection algorithm (Kselect1 vs Kselect2, same
     k-th value), so it does not change the result.  Returns the branch statistics."""
-    if recoverPct > 1:           # MCL.cpp accepts 90 or .9 (Applications/MCL.cpp:150)
-        recoverPct = recoverPct / 100.0
     out, stats = _prune_result(A._ctx, A._res, hardThreshold, selectNum, recoverNum, recoverPct)
     A._ctx._lib.cbg_result_free(A._ctx._ptr, ctypes.byref(A._res))
     A._res = out
@@ -78,8 +76,6 @@ def MemEfficientSpGEMM(SR, A, B, phases, hardThreshold, selectNum, recoverNum, r
         phases = 1
     if perProcessMemory > 0:
         phases = _phases_for_memory(SR, A, B, selectNum, recoverNum, perProcessMemory, phases)
-    if recoverPct > 1:
-        recoverPct = recoverPct / 100.0
     pieces, totals = [], {"recovered": 0, "selected": 0, "recovered_after_select": 0, "multiplies": 0,
                           "nnz_unpruned": 0, "phases": phases}
     try:

@@ -188,6 +188,11 @@ cbg_status cbg_mcl_prune(cbg_ctx* ctx, const cbg_csc_result* in, double hardThre
                          int64_t recoverNum, double recoverPct, cbg_csc_result* out, cbg_mcl_stats* stats);
 /* Columns [c0, c1) of a device CSC as a new result (colptr rebased).  c out of range -> CBG_EDIM. */
 cbg_status cbg_col_range(cbg_ctx* ctx, const cbg_csc_result* in, int64_t c0, int64_t c1, cbg_csc_result* out);
+/* Columns cols[0..ncols) (host array, any order, repeats allowed) of a device CSC as a new result:
+ * the column form of SpParMat::SubsRef_SR (A(:, ci), SpParMat.cpp:2251-2422) on one block.
+ * A column id out of range -> CBG_EDIM. */
+cbg_status cbg_col_select(cbg_ctx* ctx, const cbg_csc_result* in, const int64_t* cols, int64_t ncols,
+                          cbg_csc_result* out);
 /* Horizontal concatenation of nparts device CSCs with equal nrow/val_type. */
 cbg_status cbg_col_concat(cbg_ctx* ctx, const cbg_csc_result* parts, int32_t nparts, cbg_csc_result* out);
 

@@ -60,6 +60,9 @@ template <> struct DeviceType<int64_t> { static constexpr bool ok = true; static
 template <> struct DeviceType<int32_t> { static constexpr bool ok = true; static constexpr cbg_dtype code = CBG_I32; };
 template <> struct DeviceType<bool> { static constexpr bool ok = true; static constexpr cbg_dtype code = CBG_BOOL; };
 
+// host staging element of a value type (std::vector<bool> has no data(): bools travel as bytes)
+template <class T> using Store = typename std::conditional<std::is_same<T, bool>::value, uint8_t, T>::type;
+
 inline void check(cbg_status s, const char* where) {
   if (s != CBG_OK) throw std::runtime_error(std::string(where) + ": " + cbg_strerror(s));
 }
@@ -95,7 +98,7 @@ template <class IT, class NTO>
 SpTuples<IT, NTO>* to_tuples(cbg_ctx* ctx, cbg_csc_result& C) {
   std::vector<int64_t> cp(C.ncol + 1);
   std::vector<int32_t> row(C.nnz > 0 ? C.nnz : 1);
-  std::vector<NTO> val(C.nnz > 0 ? C.nnz : 1);
+  std::vector<Store<NTO>> val(C.nnz > 0 ? C.nnz : 1);
   const int64_t nrow = C.nrow, ncol = C.ncol;
   cbg_status s = cbg_result_to_host(ctx, &C, cp.data(), row.data(), C.val ? (void*)val.data() : nullptr);
   cbg_result_free(ctx, &C);   // clears C
@@ -103,7 +106,7 @@ SpTuples<IT, NTO>* to_tuples(cbg_ctx* ctx, cbg_csc_result& C) {
   const int64_t nnz = cp[ncol];
   std::tuple<IT, IT, NTO>* t = new std::tuple<IT, IT, NTO>[nnz > 0 ? nnz : 1];
   for (int64_t j = 0; j < ncol; ++j)
-    for (int64_t p = cp[j]; p < cp[j + 1]; ++p) t[p] = std::make_tuple((IT)row[p], (IT)j, val[p]);
+    for (int64_t p = cp[j]; p < cp[j + 1]; ++p) t[p] = std::make_tuple((IT)row[p], (IT)j, (NTO)val[p]);
   return new SpTuples<IT, NTO>(nnz, (IT)nrow, (IT)ncol, t, /*sorted=*/true, /*isOpNew=*/false);
 }
 
@@ -165,7 +168,7 @@ SpTuples<IT, NT>* MultiwayMerge(std::vector<SpTuples<IT, NT>*>& lists, IT mdim =
     std::vector<cbg_dcsc_view> views(lists.size());
     std::vector<std::vector<int64_t>> cps(lists.size());
     std::vector<std::vector<int32_t>> rows(lists.size());
-    std::vector<std::vector<NT>> vals(lists.size());
+    std::vector<std::vector<Store<NT>>> vals(lists.size());
     for (size_t l = 0; l < lists.size(); ++l) {   // SpTuples -> host CSC -> device (cbg_upload)
       SpTuples<IT, NT>& T = *lists[l];
       const IT m = T.getnrow(), n = T.getncol();
@@ -177,7 +180,7 @@ SpTuples<IT, NT>* MultiwayMerge(std::vector<SpTuples<IT, NT>*>& lists, IT mdim =
       for (int64_t k = 0; k < T.getnnz(); ++k) {
         ++cps[l][T.colindex(k) + 1];
         rows[l][k] = (int32_t)T.rowindex(k);
-        vals[l][k] = T.numvalue(k);
+        vals[l][k] = (Store<NT>)T.numvalue(k);
       }
       for (IT j = 0; j < n; ++j) cps[l][j + 1] += cps[l][j];
       cbg_dcsc_view v{};

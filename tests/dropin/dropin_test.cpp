@@ -85,6 +85,20 @@ int main(int argc, char** argv) {
     SpTuples<I, int64_t>* di = gpu::LocalSpGEMMHash<MP, int64_t>(*Ai, *Bi, false, false, true);
     if (!same(di, ri, "MinPlus<int64>")) rc = 1;
 
+    // bool-valued product (bool values are staged as bytes on the host side of the drop-in)
+    auto* Ab = random_dccols<bool>(140, 100, 0.08, 6);
+    auto* Bb = random_dccols<bool>(100, 120, 0.08, 7);
+    typedef PlusTimesSRing<bool, bool> PTB;
+    SpTuples<I, bool>* rb = LocalSpGEMMHash<PTB, bool>(*Ab, *Bb, false, false, true);
+    SpTuples<I, bool>* db = gpu::LocalSpGEMMHash<PTB, bool>(*Ab, *Bb, false, false, true);
+    if (!same(db, rb, "PlusTimes<bool>")) rc = 1;
+    std::vector<SpTuples<I, bool>*> lb1 = {new SpTuples<I, bool>(*rb), new SpTuples<I, bool>(*db)};
+    std::vector<SpTuples<I, bool>*> lb2 = {new SpTuples<I, bool>(*rb), new SpTuples<I, bool>(*db)};
+    SpTuples<I, bool>* mbr = MultiwayMerge<PTB>(lb1, (I)140, (I)120, true);
+    SpTuples<I, bool>* mbd = gpu::MultiwayMerge<PTB>(lb2, (I)140, (I)120, true);
+    if (!same(mbd, mbr, "MultiwayMerge<bool>")) rc = 1;
+    delete rb; delete db; delete mbr; delete mbd; delete Ab; delete Bb;
+
     typedef MaxTimesSR<int64_t, int64_t> MT;   // CPU fallback inside the drop-in
     SpTuples<I, int64_t>* rc1 = LocalSpGEMMHash<MT, int64_t>(*Ai, *Bi, false, false, true);
     SpTuples<I, int64_t>* dc1 = gpu::LocalSpGEMMHash<MT, int64_t>(*Ai, *Bi, false, false, true);

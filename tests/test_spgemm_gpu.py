@@ -291,7 +291,8 @@ def test_gpu_heavy_units_many_columns(gpu_ctx):
 
 
 @pytest.mark.parametrize("sr,dt", [("plus_times", "f64"), ("min_plus", "i64"), ("select2nd", "i64"),
-                                   ("select_max", "i64"), ("bool_copy2nd", "f64")])
+                                   ("select_max", "i64"), ("bool_copy2nd", "f64"), ("plus_times", "f32"),
+                                   ("plus_times", "i32"), ("min_plus", "i32")])
 def test_gpu_heavy_rank_mode_multichunk(gpu_ctx, sr, dt):
     """Heavy columns whose B column holds > 1024 nonzeros (the rank mode streams the unit's segments
     twice: mark pass, accumulate pass), spans below and above the rank-mode limit, plus a column
@@ -308,15 +309,18 @@ def test_gpu_heavy_rank_mode_multichunk(gpu_ctx, sr, dt):
         cols = [np.sort(rng.choice(int(hi[k]), int(rng.integers(1, 6)), replace=False)).astype(np.int32)
                 for k in range(ncolA)]
     cp = np.r_[0, np.cumsum([len(c) for c in cols])]
-    A = Csc(n, ncolA, cp, np.concatenate(cols), rng.integers(1, 9, cp[-1]).astype(np.float64 if dt == "f64" else np.int64))
+    npdt = {"f64": np.float64, "f32": np.float32, "i64": np.int64, "i32": np.int32}[dt]
+    A = Csc(n, ncolA, cp, np.concatenate(cols), rng.integers(1, 9, cp[-1]).astype(npdt))
     pick = [np.arange(0, 3000, dtype=np.int32),                      # nb = 3000, span <= 300k rows
             np.arange(3000, 6000, 2, dtype=np.int32),                # nb = 1500, full span
             np.sort(rng.choice(3000, 900, replace=False)).astype(np.int32)]   # single chunk
     bcp = np.r_[0, np.cumsum([len(x) for x in pick])]
-    B = Csc(ncolA, len(pick), bcp, np.concatenate(pick),
-            rng.integers(1, 9, bcp[-1]).astype(np.float64 if dt == "f64" else np.int64))
+    B = Csc(ncolA, len(pick), bcp, np.concatenate(pick), rng.integers(1, 9, bcp[-1]).astype(npdt))
     _check_vs_oracle(gpu_ctx, A, B, sr, dt)
-    assert gpu_ctx.last_profile()["bins"][12] >= 1   # heavy columns present
+    prof = gpu_ctx.last_profile()
+    assert prof["bins"][12] >= 1   # heavy columns present
+    if sr != "bool_copy2nd":       # rank mode: units are sized per accumulator width, none re-run
+        assert prof["bins"][14] == 0
 
 
 @pytest.mark.parametrize("sr,dt", [("plus_times", "f64"), ("plus_times", "i64"), ("min_plus", "i64"),
@@ -354,3 +358,56 @@ def test_gpu_merge_of_split_products_equals_product(gpu_ctx):
     cp, ir, val = M.to_host()
     R = fixture_product(z, "pt_i64_hash")
     assert np.array_equal(cp, R.cp) and np.array_equal(ir, R.ir) and np.array_equal(val, R.val)
+
+
+def test_gpu_rmat_s18_sampled_vs_oracle(gpu_ctx):
+    """R-MAT s18 A*A on the device (SUBW subwindows, multi-unit heavy columns, 2^18-row symbolic parts):
+    every 3rd column of the full product against the oracle's product of those columns, bit-exact
+    (multiplicity values), and the total multiplies against estimateFLOP by numpy."""
+    n, cp, ir, val = cb.generate_rmat_host(18, 16, seed=1)
+    dA = cb.SpDCCols.from_csc(gpu_ctx, n, n, cp, ir, val)
+    C = cb.LocalSpGEMMHash(cb.PlusTimesSRing("f64"), dA, dA)
+    alen = np.diff(cp)
+    assert C.multiplies == int(alen[ir].sum())
+    assert gpu_ctx.last_profile()["bins"][12] > 0
+    cols = np.arange(0, n, 3)
+    sel = np.concatenate([np.arange(cp[c], cp[c + 1]) for c in cols])
+    B = Csc(n, len(cols), np.r_[0, np.cumsum(alen[cols])], ir[sel], val[sel])
+    R, rm, rc = oracle_spgemm(Csc(n, n, cp, ir, val), B, "plus_times", "f64")
+    assert rc == 0
+    S = C.select_columns(cols)
+    scp, sir, sval = S.to_host()
+    assert np.array_equal(scp, R.cp) and np.array_equal(sir, R.ir) and np.array_equal(sval, R.val)
+
+
+def test_gpu_col_select(gpu_ctx):
+    """cbg_col_select: arbitrary column subsets (repeats, any order) of a device CSC."""
+    rng = np.random.default_rng(3)
+    M = rand_csc(rng, 400, 300, 0.03, "i64")
+    d = upload(gpu_ctx, M)
+    cols = np.r_[rng.integers(0, 300, 200), 7, 7, 299, 0]
+    S = d.select_columns(cols)
+    cp, ir, val = S.to_host()
+    R = M.to_scipy()[:, cols].tocsc()
+    R.sort_indices()
+    assert np.array_equal(cp, R.indptr) and np.array_equal(ir, R.indices) and np.array_equal(val, R.data)
+    with pytest.raises(cb.CbgError) as ei:
+        d.select_columns([300])
+    assert ei.value.status == 3002
+
+
+def test_gpu_bpos_guard(gpu_ctx):
+    """Select2nd / BoolCopy2nd accumulate an int32 B position: nnz(B) >= 2^31 is refused (CBG_EUNSUP)
+    before any device work, instead of silently truncating."""
+    import ctypes
+    from combblas_amd import _abi
+    A = upload(gpu_ctx, rand_csc(np.random.default_rng(1), 50, 40, 0.1, "i64"))
+    va = A._view()
+    big = (1 << 31)
+    vb = _abi.DcscView(40, 10, big, 10, va.cp, None, va.ir, 4, 8, va.val, _abi.I64, 1)   # never read
+    res = _abi.CscResult()
+    m = ctypes.c_int64()
+    for sr in (_abi.SR_SELECT2ND, _abi.SR_BOOL_COPY2ND):
+        st = gpu_ctx._lib.cbg_spgemm_local(gpu_ctx._ptr, ctypes.byref(va), ctypes.byref(vb), sr, _abi.I64, 1,
+                                           ctypes.byref(res), ctypes.byref(m))
+        assert st == _abi.EUNSUP
