@@ -7,7 +7,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.environ.get("CBG_LIB_PATH") or os.path.join(_HERE, "libcbgpu.so")   # override: tuning variants
+_DEFAULT = os.path.join(_HERE, "libcbgpu.so")
+LIB_PATH = os.environ.get("CBG_LIB_PATH") or _DEFAULT   # override: tuning variants
 
 # cbg_status
 OK, EDIM, EALIAS, ENOMEM, EUNSUP, EDEVICE, EADD, EINVAL, ECOMM = 0, 3002, 3005, 10, 11, 12, 13, 14, 15
@@ -48,6 +49,29 @@ class MclStats(ctypes.Structure):
                 ("recovered_after_select", ctypes.c_int64), ("nnz_in", ctypes.c_int64), ("nnz_out", ctypes.c_int64)]
 
 
+class GridStats(ctypes.Structure):
+    _fields_ = [("multiplies", ctypes.c_int64), ("bcast_bytes", ctypes.c_int64), ("fiber_bytes", ctypes.c_int64),
+                ("bcast_ms", ctypes.c_double), ("local_ms", ctypes.c_double), ("merge_ms", ctypes.c_double),
+                ("fiber_ms", ctypes.c_double), ("total_ms", ctypes.c_double), ("stages", ctypes.c_int32)]
+
+
+# cbg_transport callbacks (include/cbgpu.h)
+BCAST_FN = ctypes.CFUNCTYPE(ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_int64,
+                            ctypes.c_int32)
+ALLTOALLV_FN = ctypes.CFUNCTYPE(ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p,
+                                ctypes.POINTER(ctypes.c_int64), ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64))
+ALLGATHER_FN = ctypes.CFUNCTYPE(ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
+                                ctypes.c_int64)
+
+
+class Transport(ctypes.Structure):
+    _fields_ = [("user", ctypes.c_void_p), ("bcast", BCAST_FN), ("alltoallv", ALLTOALLV_FN),
+                ("allgather", ALLGATHER_FN)]
+
+
+GROUP_ROW, GROUP_COL, GROUP_FIBER, GROUP_WORLD = range(4)
+HALVES, RUNNING_MERGE = 4, 8
+
 # name -> (restype, argtypes); must match include/cbgpu.h exactly
 SIGNATURES = {
     "cbg_abi_version": (ctypes.c_int32, []),
@@ -82,6 +106,21 @@ SIGNATURES = {
                                       ctypes.POINTER(CscResult)]),
     "cbg_col_select": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(CscResult), ctypes.c_void_p, ctypes.c_int64,
                                       ctypes.POINTER(CscResult)]),
+    "cbg_rccl_unique_id": (ctypes.c_int, [ctypes.c_void_p]),
+    "cbg_grid_create_rccl": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32,
+                                            ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                            ctypes.POINTER(ctypes.c_void_p)]),
+    "cbg_grid_create": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(Transport), ctypes.c_int32, ctypes.c_int32,
+                                       ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(ctypes.c_void_p)]),
+    "cbg_grid_destroy": (ctypes.c_int, [ctypes.c_void_p]),
+    "cbg_spgemm_grid": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(DcscView), ctypes.POINTER(DcscView), ctypes.c_int,
+                                       ctypes.c_int, ctypes.c_uint32, ctypes.POINTER(CscResult),
+                                       ctypes.POINTER(GridStats)]),
+    "cbg_summa_layer": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(DcscView), ctypes.POINTER(DcscView), ctypes.c_int,
+                                       ctypes.c_int, ctypes.c_uint32, ctypes.POINTER(CscResult),
+                                       ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(GridStats)]),
+    "cbg_reduce_all": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(CscResult), ctypes.c_int32, ctypes.c_int,
+                                      ctypes.c_int, ctypes.POINTER(CscResult), ctypes.POINTER(GridStats)]),
 }
 
 _lib = None
@@ -96,6 +135,8 @@ def lib():
                           "(or __graft_entry__.build()); there is no CPU fallback")
         L = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
+            if LIB_PATH != _DEFAULT and not hasattr(L, name):
+                continue   # an older tuning/diagnostic variant may lack newer entry points
             f = getattr(L, name)
             f.restype = res
             f.argtypes = args

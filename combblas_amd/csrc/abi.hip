@@ -111,7 +111,8 @@ void cbg_result_free(cbg_ctx* ctx, cbg_csc_result* C) {
 cbg_status cbg_upload(cbg_ctx* ctx, const cbg_dcsc_view* v, cbg_csc_result* out) {
   if (!ctx || !v || !out) return CBG_EINVAL;
   const int pb = v->ptr_bytes ? v->ptr_bytes : v->idx_bytes;
-  if (v->jc || (v->idx_bytes != 8 && v->idx_bytes != 4) || (pb != 8 && pb != 4)) return CBG_EINVAL;
+  if ((v->idx_bytes != 8 && v->idx_bytes != 4) || (pb != 8 && pb != 4)) return CBG_EINVAL;
+  if (v->nnz > 0 && (!v->cp || !v->ir)) return CBG_EINVAL;
   HIPCHK(hipSetDevice(ctx->device));
   std::unique_ptr<Owner> own(new Owner(ctx->pool));
   hipStream_t st = ctx->stream;
@@ -122,7 +123,31 @@ cbg_status cbg_upload(cbg_ctx* ctx, const cbg_dcsc_view* v, cbg_csc_result* out)
   HIPCHK(own->val.reserve(vs * (v->nnz + 1) + 8));
   DevBuf tmp;
   DevBuf tmp2;
-  if (pb == 8) {
+  if (v->jc) {   // reference DCSC (cp[nzc+1], jc[nzc]) -> dense colptr on device
+    const int64_t nzc = v->nzc;
+    HIPCHK(tmp2.reserve(8 * (2 * nzc + 2)));
+    int64_t* rcp = tmp2.as<int64_t>();
+    int64_t* rjc = rcp + nzc + 1;
+    DevBuf t32;
+    if (pb == 8) {
+      HIPCHK(hipMemcpyAsync(rcp, v->cp, 8 * (nzc + 1), kind, st));
+    } else {
+      HIPCHK(t32.reserve(4 * (nzc + 2)));
+      HIPCHK(hipMemcpyAsync(t32.p, v->cp, 4 * (nzc + 1), kind, st));
+      k_i32_to_i64<<<256, 256, 0, st>>>(nzc + 1, t32.as<int32_t>(), rcp);
+      HIPCHK(hipStreamSynchronize(st));
+    }
+    if (v->idx_bytes == 8) {
+      if (nzc) HIPCHK(hipMemcpyAsync(rjc, v->jc, 8 * nzc, kind, st));
+    } else if (nzc) {
+      HIPCHK(t32.reserve(4 * (nzc + 2)));
+      HIPCHK(hipMemcpyAsync(t32.p, v->jc, 4 * nzc, kind, st));
+      k_i32_to_i64<<<256, 256, 0, st>>>(nzc, t32.as<int32_t>(), rjc);
+    }
+    k_dcsc_to_csc<<<(int)grid_for(v->ncol + 1, 256, kMaxGrid), 256, 0, st>>>(v->ncol, nzc, rcp, rjc,
+                                                                             own->cp.as<int64_t>());
+    HIPCHK(hipStreamSynchronize(st));   // t32 is released at scope end
+  } else if (pb == 8) {
     HIPCHK(hipMemcpyAsync(own->cp.p, v->cp, 8 * (v->ncol + 1), kind, st));
   } else {
     HIPCHK(tmp2.reserve(4 * (v->ncol + 2)));

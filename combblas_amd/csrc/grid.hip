@@ -1,0 +1,782 @@
+// grid.hip -- distributed SpGEMM over a layers x rows x cols grid of MI355X ranks (include/cbgpu.h).
+//
+// Reference drivers (include/CombBLAS/ParFriends.h): Mult_AnXBn_Synch 1004-1108, Mult_AnXBn_DoubleBuff
+// 798-997, Mult_AnXBn_Overlap 1110-1235, Mult_AnXBn_SUMMA3D 2918-3208; 3DSpGEMM/SUMMALayer.h:24-97 and
+// Reductions.h:36-155.  One formulation covers them all: the layer SUMMA (q stages of a row-group
+// broadcast of the A piece and a column-group broadcast of the B piece, a local product, a merge)
+// followed, with L > 1 layers, by the fiber all-to-all of layer column parts and a merge.
+//
+// MI355X-first choices:
+//   * pieces, broadcast buffers and products stay in HBM (no SpTuples round trip per stage);
+//   * with RCCL the broadcasts of stage k+1 are issued on a communication stream before stage k's
+//     local product (double-buffered receive slots sized once per call), ordered by HIP events;
+//   * the three arrays of a piece go out as one RCCL group (one launch, no packing copy);
+//   * the fiber exchange is a grouped ncclSend/ncclRecv all-to-all-v of column counts, rows, values.
+// A caller-provided transport (cbg_transport: MPI on the reference side, gloo in tests) runs the same
+// schedule synchronously through host callbacks.
+#include "spgemm_host.hpp"
+#include <rccl/rccl.h>
+#include <chrono>
+
+namespace {
+
+inline double now_ms() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+#define NCCLCHK(x)                                                                                     \
+  do {                                                                                                 \
+    ncclResult_t r_ = (x);                                                                             \
+    if (r_ != ncclSuccess) {                                                                           \
+      fprintf(stderr, "cbgpu: %s failed: %s (%s:%d)\n", #x, ncclGetErrorString(r_), __FILE__, __LINE__); \
+      return CBG_ECOMM;                                                                                \
+    }                                                                                                  \
+  } while (0)
+
+#define CBGCHK(x)                      \
+  do {                                 \
+    cbg_status s_ = (x);               \
+    if (s_ != CBG_OK) return s_;       \
+  } while (0)
+
+// count[c] = cp[c+1] - cp[c]
+__global__ void k_col_counts(int64_t n, const int64_t* __restrict__ cp, int64_t* __restrict__ cnt) {
+  for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < n; c += (int64_t)gridDim.x * blockDim.x)
+    cnt[c] = cp[c + 1] - cp[c];
+}
+// rebased column range: out[c] = cp[c0 + c] - cp[c0], c in [0, n]
+__global__ void k_cp_rebase(int64_t n, const int64_t* __restrict__ cp, int64_t c0, int64_t* __restrict__ out) {
+  const int64_t base = cp[c0];
+  for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c <= n; c += (int64_t)gridDim.x * blockDim.x)
+    out[c] = cp[c0 + c] - base;
+}
+// row split of a CSC at `cut` (rows are sorted per column): per column, entries below the cut
+__global__ void k_row_cut(int64_t ncol, const int64_t* __restrict__ cp, const int32_t* __restrict__ ir, int32_t cut,
+                          int64_t* __restrict__ lo_cnt) {
+  for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < ncol; c += (int64_t)gridDim.x * blockDim.x)
+    lo_cnt[c] = lower_bound_rows(ir, cp[c], cp[c + 1], cut) - cp[c];
+}
+// copy the two row halves; hi rows are rebased by -cut
+template <typename T>
+__global__ void __launch_bounds__(256) k_row_split(int64_t ncol, const int64_t* __restrict__ cp,
+                                                   const int32_t* __restrict__ ir, const T* __restrict__ val,
+                                                   int32_t cut, const int64_t* __restrict__ lcp,
+                                                   const int64_t* __restrict__ hcp, int32_t* __restrict__ lir,
+                                                   T* __restrict__ lval, int32_t* __restrict__ hir,
+                                                   T* __restrict__ hval) {
+  const int w = threadIdx.x / kWave, l = lane_id();
+  for (int64_t c = blockIdx.x * 4 + w; c < ncol; c += (int64_t)gridDim.x * 4) {
+    const int64_t s = cp[c], e = cp[c + 1], nl = lcp[c + 1] - lcp[c];
+    for (int64_t q = s + l; q < e; q += kWave) {
+      const int64_t k = q - s;
+      if (k < nl) {
+        lir[lcp[c] + k] = ir[q];
+        if (val) lval[lcp[c] + k] = val[q];
+      } else {
+        hir[hcp[c] + k - nl] = ir[q] - cut;
+        if (val) hval[hcp[c] + k - nl] = val[q];
+      }
+    }
+  }
+}
+
+// hcp[c] = cp[c] - lcp[c]
+__global__ void k_cp_sub(int64_t n, const int64_t* __restrict__ cp, const int64_t* __restrict__ lcp,
+                         int64_t* __restrict__ hcp) {
+  for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c <= n; c += (int64_t)gridDim.x * blockDim.x)
+    hcp[c] = cp[c] - lcp[c];
+}
+
+// device CSC piece (int64 colptr, int32 rows); storage owned by `own` unless borrowed
+struct Piece {
+  int64_t nrow = 0, ncol = 0, nnz = 0;
+  const int64_t* cp = nullptr;
+  const int32_t* ir = nullptr;
+  const void* val = nullptr;
+  std::shared_ptr<Owner> own;    // storage of cp/ir/val (or of cp only, see keep)
+  std::shared_ptr<Owner> keep;   // shared storage the arrays point into (fiber receive buffers)
+  int32_t k = 0, r = 0;          // stage (inner block) and half of the product: merge order
+};
+
+}  // namespace
+
+struct cbg_grid {
+  cbg_ctx* ctx = nullptr;
+  int world = 1, rank = 0, L = 1, q = 1, layer = 0, row = 0, col = 0;
+  bool rccl = false;
+  ncclComm_t comm[4] = {nullptr, nullptr, nullptr, nullptr};
+  cbg_transport cb{};
+  hipStream_t cs = nullptr;          // communication stream
+  hipEvent_t ev_comm[2] = {}, ev_used[2] = {}, ev_t[4] = {};
+  bool used_rec[2] = {false, false};
+  DevBuf slotA[2], slotB[2], small, xsend, xrecv, xcnt;
+
+  int gsize(int g) const { return g == CBG_GROUP_ROW || g == CBG_GROUP_COL ? q : g == CBG_GROUP_FIBER ? L : world; }
+  int grank(int g) const { return g == CBG_GROUP_ROW ? col : g == CBG_GROUP_COL ? row : g == CBG_GROUP_FIBER ? layer : rank; }
+};
+
+namespace {
+
+// ------------------------------------------------------------------------------------ transport
+// n arrays broadcast from member `root` of group g (in place at the root); async on G->cs with RCCL
+cbg_status t_bcast(cbg_grid* G, int g, int n, void* const* bufs, const int64_t* bytes, int root) {
+  if (G->gsize(g) == 1) return CBG_OK;
+  if (G->rccl) {
+    NCCLCHK(ncclGroupStart());
+    for (int i = 0; i < n; ++i)
+      if (bytes[i] > 0) NCCLCHK(ncclBroadcast(bufs[i], bufs[i], (size_t)bytes[i], ncclInt8, root, G->comm[g], G->cs));
+    NCCLCHK(ncclGroupEnd());
+    return CBG_OK;
+  }
+  HIPCHK(hipStreamSynchronize(G->ctx->stream));
+  HIPCHK(hipStreamSynchronize(G->cs));
+  for (int i = 0; i < n; ++i)
+    if (bytes[i] > 0 && G->cb.bcast(G->cb.user, g, bufs[i], bytes[i], root) != 0) return CBG_ECOMM;
+  return CBG_OK;
+}
+
+// all-to-all-v of device buffers over group g: segment m of `send` (sbytes[m]) goes to member m;
+// segments land in member order in `recv`.  Synchronous on return.
+cbg_status t_alltoallv(cbg_grid* G, int g, const void* send, const int64_t* sbytes, void* recv, const int64_t* rbytes) {
+  const int P = G->gsize(g), me = G->grank(g);
+  std::vector<int64_t> so(P + 1, 0), ro(P + 1, 0);
+  for (int m = 0; m < P; ++m) { so[m + 1] = so[m] + sbytes[m]; ro[m + 1] = ro[m] + rbytes[m]; }
+  hipStream_t st = G->ctx->stream;
+  if (P == 1) {
+    if (sbytes[0]) HIPCHK(hipMemcpyAsync(recv, send, sbytes[0], hipMemcpyDeviceToDevice, st));
+    HIPCHK(hipStreamSynchronize(st));
+    return CBG_OK;
+  }
+  if (G->rccl) {
+    if (sbytes[me]) HIPCHK(hipMemcpyAsync((char*)recv + ro[me], (const char*)send + so[me], sbytes[me],
+                                          hipMemcpyDeviceToDevice, st));
+    NCCLCHK(ncclGroupStart());
+    for (int m = 0; m < P; ++m) {
+      if (m == me) continue;
+      if (sbytes[m]) NCCLCHK(ncclSend((const char*)send + so[m], (size_t)sbytes[m], ncclInt8, m, G->comm[g], st));
+      if (rbytes[m]) NCCLCHK(ncclRecv((char*)recv + ro[m], (size_t)rbytes[m], ncclInt8, m, G->comm[g], st));
+    }
+    NCCLCHK(ncclGroupEnd());
+    HIPCHK(hipStreamSynchronize(st));
+    return CBG_OK;
+  }
+  HIPCHK(hipStreamSynchronize(st));
+  return G->cb.alltoallv(G->cb.user, g, send, sbytes, recv, rbytes) == 0 ? CBG_OK : CBG_ECOMM;
+}
+
+// all-gather of `bytes` host bytes per member (GetSetSizes); synchronous
+cbg_status t_allgather(cbg_grid* G, int g, const void* mine, void* all, int64_t bytes) {
+  const int P = G->gsize(g);
+  if (P == 1) { memcpy(all, mine, bytes); return CBG_OK; }
+  if (G->rccl) {
+    HIPCHK(G->small.reserve(bytes * (P + 1)));
+    char* d = G->small.as<char>();
+    HIPCHK(hipMemcpyAsync(d, mine, bytes, hipMemcpyHostToDevice, G->cs));
+    NCCLCHK(ncclAllGather(d, d + bytes, (size_t)bytes, ncclInt8, G->comm[g], G->cs));
+    HIPCHK(hipMemcpyAsync(all, d + bytes, bytes * P, hipMemcpyDeviceToHost, G->cs));
+    HIPCHK(hipStreamSynchronize(G->cs));
+    return CBG_OK;
+  }
+  return G->cb.allgather(G->cb.user, g, mine, all, bytes) == 0 ? CBG_OK : CBG_ECOMM;
+}
+
+// every rank's flag -> true iff all are set (world all-gather of one int)
+cbg_status all_ok(cbg_grid* G, bool mine, bool* out) {
+  std::vector<int32_t> v(G->world);
+  int32_t m = mine ? 1 : 0;
+  CBGCHK(t_allgather(G, CBG_GROUP_WORLD, &m, v.data(), 4));
+  *out = true;
+  for (int32_t x : v) *out = *out && x;
+  return CBG_OK;
+}
+
+// ------------------------------------------------------------------------------------ pieces
+cbg_status make_piece(cbg_ctx* ctx, const cbg_dcsc_view* v, cbg_dtype dt, Piece* p) {
+  const int pb = v->ptr_bytes ? v->ptr_bytes : v->idx_bytes;
+  p->nrow = v->nrow; p->ncol = v->ncol; p->nnz = v->nnz;
+  // a bool-typed operand of a non-bool product is a pattern (SelectMaxSRing<bool,T>, BoolCopy*)
+  const bool pattern = !v->val || (v->val_type == CBG_BOOL && dt != CBG_BOOL);
+  if (!pattern && v->val_type != dt) return CBG_EINVAL;
+  if (v->on_device && !v->jc && pb == 8 && v->idx_bytes == 4) {   // zero copy
+    p->cp = (const int64_t*)v->cp;
+    p->ir = (const int32_t*)v->ir;
+    p->val = pattern ? nullptr : v->val;
+    return CBG_OK;
+  }
+  cbg_dcsc_view u = *v;
+  if (pattern) u.val = nullptr;
+  cbg_csc_result r;
+  CBGCHK(cbg_upload(ctx, &u, &r));
+  p->own.reset((Owner*)r._owner, [](Owner* o) { delete o; });
+  p->cp = r.colptr; p->ir = r.row; p->val = pattern ? nullptr : r.val;
+  return CBG_OK;
+}
+
+cbg_dcsc_view view_of(const Piece& p, cbg_dtype dt, bool has_val) {
+  cbg_dcsc_view v{};
+  v.nrow = p.nrow; v.ncol = p.ncol; v.nnz = p.nnz; v.nzc = p.ncol;
+  v.cp = p.cp; v.jc = nullptr; v.ir = p.ir; v.idx_bytes = 4; v.ptr_bytes = 8;
+  v.val = has_val ? p.val : nullptr; v.val_type = has_val ? dt : CBG_BOOL; v.on_device = 1;
+  return v;
+}
+
+cbg_csc_result result_of(const Piece& p, cbg_dtype dt) {
+  cbg_csc_result r{};
+  r.nrow = p.nrow; r.ncol = p.ncol; r.nnz = p.nnz;
+  r.colptr = (int64_t*)p.cp; r.row = (int32_t*)p.ir; r.val = (void*)p.val; r.val_type = dt;
+  return r;
+}
+
+// Piece owning a library result (freed with the piece)
+Piece piece_of_result(cbg_csc_result& r) {
+  Piece p;
+  p.nrow = r.nrow; p.ncol = r.ncol; p.nnz = r.nnz;
+  p.cp = r.colptr; p.ir = r.row; p.val = r.val;
+  p.own.reset((Owner*)r._owner, [](Owner* o) { delete o; });
+  r._owner = nullptr;
+  return p;
+}
+
+// columns [0, cut) and [cut, ncol) of a piece (Split by columns, SpDCCols.cpp:897)
+cbg_status col_halves(cbg_ctx* ctx, const Piece& a, size_t vs, Piece* h) {
+  const int64_t cut = a.ncol / 2;
+  hipStream_t st = ctx->stream;
+  int64_t e = 0;
+  HIPCHK(hipMemcpyAsync(&e, a.cp + cut, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  h[0] = a; h[0].ncol = cut; h[0].nnz = e;   // prefix: same arrays, shorter colptr
+  std::shared_ptr<Owner> o(new Owner(ctx->pool));
+  HIPCHK(o->cp.reserve(8 * (a.ncol - cut + 1)));
+  k_cp_rebase<<<(int)grid_for(a.ncol - cut + 1, 256, kMaxGrid), 256, 0, st>>>(a.ncol - cut, a.cp, cut, o->cp.as<int64_t>());
+  HIPCHK(hipGetLastError());
+  h[1] = a;
+  h[1].ncol = a.ncol - cut; h[1].nnz = a.nnz - e;
+  h[1].cp = o->cp.as<int64_t>(); h[1].ir = a.ir + e;
+  h[1].val = a.val ? (const void*)((const char*)a.val + vs * e) : nullptr;
+  h[1].own = o;
+  return CBG_OK;
+}
+
+// rows [0, cut) and [cut, nrow) of a piece, the second rebased (Split after transpose, ParFriends.h:823-829)
+template <typename T>
+cbg_status row_halves(cbg_ctx* ctx, const Piece& b, Piece* h) {
+  const int32_t cut = (int32_t)(b.nrow / 2);
+  hipStream_t st = ctx->stream;
+  std::shared_ptr<Owner> lo(new Owner(ctx->pool)), hi(new Owner(ctx->pool));
+  DevBuf cnt, tiles, scal;
+  const int64_t n = b.ncol;
+  HIPCHK(cnt.reserve(8 * (2 * n + 2)));
+  HIPCHK(lo->cp.reserve(8 * (n + 1)));
+  HIPCHK(hi->cp.reserve(8 * (n + 1)));
+  int64_t* lcnt = cnt.as<int64_t>();
+  int64_t* hcnt = lcnt + n + 1;
+  const int g = (int)grid_for(n, 256, kMaxGrid);
+  int64_t tot[2] = {0, 0};
+  if (n > 0) {
+    k_row_cut<<<g, 256, 0, st>>>(n, b.cp, b.ir, cut, lcnt);
+    k_col_counts<<<g, 256, 0, st>>>(n, b.cp, hcnt);
+    const int64_t ntiles = (n + kScanTile - 1) / kScanTile;
+    HIPCHK(tiles.reserve(8 * (ntiles + 1)));
+    HIPCHK(scal.reserve(16));
+    k_scan_tiles<<<(int)ntiles, 256, 0, st>>>(n, lcnt, tiles.as<int64_t>());
+    k_scan_sums<<<1, 1024, 0, st>>>(ntiles, tiles.as<int64_t>(), scal.as<int64_t>());
+    k_scan_apply<<<(int)ntiles, 256, 0, st>>>(n, lcnt, tiles.as<int64_t>(), lo->cp.as<int64_t>());
+    // hi counts = total - lo
+    HIPCHK(hipMemcpyAsync(&tot[0], scal.p, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+  } else {
+    HIPCHK(hipMemsetAsync(lo->cp.p, 0, 8, st));
+  }
+  tot[1] = b.nnz - tot[0];
+  k_cp_sub<<<(int)grid_for(n + 1, 256, kMaxGrid), 256, 0, st>>>(n, b.cp, lo->cp.as<int64_t>(), hi->cp.as<int64_t>());
+  HIPCHK(lo->ir.reserve(4 * (tot[0] + 1)));
+  HIPCHK(hi->ir.reserve(4 * (tot[1] + 1)));
+  HIPCHK(lo->val.reserve(sizeof(T) * (tot[0] + 1)));
+  HIPCHK(hi->val.reserve(sizeof(T) * (tot[1] + 1)));
+  if (n > 0 && b.nnz > 0)
+    k_row_split<T><<<(int)grid_for(n, 4, kMaxGrid * 2), 256, 0, st>>>(
+        n, b.cp, b.ir, (const T*)b.val, cut, lo->cp.as<int64_t>(), hi->cp.as<int64_t>(), lo->ir.as<int32_t>(),
+        lo->val.as<T>(), hi->ir.as<int32_t>(), hi->val.as<T>());
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(st));   // cnt/tiles/scal are released on return
+  h[0].nrow = cut; h[0].ncol = n; h[0].nnz = tot[0];
+  h[0].cp = lo->cp.as<int64_t>(); h[0].ir = lo->ir.as<int32_t>(); h[0].val = b.val ? lo->val.p : nullptr; h[0].own = lo;
+  h[1].nrow = b.nrow - cut; h[1].ncol = n; h[1].nnz = tot[1];
+  h[1].cp = hi->cp.as<int64_t>(); h[1].ir = hi->ir.as<int32_t>(); h[1].val = b.val ? hi->val.p : nullptr; h[1].own = hi;
+  return CBG_OK;
+}
+
+cbg_status row_halves_dt(cbg_ctx* ctx, cbg_dtype dt, const Piece& b, Piece* h) {
+  switch (dt_size(dt)) {
+    case 1: return row_halves<uint8_t>(ctx, b, h);
+    case 4: return row_halves<uint32_t>(ctx, b, h);
+    default: return row_halves<uint64_t>(ctx, b, h);
+  }
+}
+
+// move a pool block between owners (PoolBuf returns its block to the pool on destruction)
+void take(PoolBuf& dst, PoolBuf& src) {
+  std::swap(dst.p, src.p);
+  std::swap(dst.n, src.n);
+  std::swap(dst.pool, src.pool);
+}
+
+struct Sizes {   // GetSetSizes record of one piece
+  int64_t nrow, ncol, nnz, has_val;
+};
+
+// merge device results (cbg_merge) into one library result; parts are borrowed
+cbg_status merge_parts(cbg_ctx* ctx, const std::vector<cbg_csc_result>& parts, cbg_semiring sr, cbg_dtype dt,
+                       cbg_csc_result* out) {
+  return cbg_merge(ctx, parts.data(), (int32_t)parts.size(), sr, dt, CBG_SORTED_COLS, out);
+}
+
+// ------------------------------------------------------------------------------------ layer SUMMA
+cbg_status summa_layer_impl(cbg_grid* G, const cbg_dcsc_view* Av, const cbg_dcsc_view* Bv, cbg_semiring sr,
+                            cbg_dtype dt, uint32_t flags, std::vector<Piece>* parts, cbg_grid_stats* st) {
+  cbg_ctx* ctx = G->ctx;
+  const size_t vs = dt_size(dt);
+  Piece A0, B0;
+  CBGCHK(make_piece(ctx, Av, dt, &A0));
+  CBGCHK(make_piece(ctx, Bv, dt, &B0));
+  const bool aval = A0.val != nullptr, bval = B0.val != nullptr;
+  // rounds: one, or two halves of the inner dimension (DoubleBuff)
+  const int R = (flags & CBG_HALVES) ? 2 : 1;
+  std::vector<Piece> Ah(R), Bh(R);
+  if (R == 1) {
+    Ah[0] = A0; Bh[0] = B0;
+  } else {
+    Piece h[2];
+    CBGCHK(col_halves(ctx, A0, vs, h));
+    Ah[0] = h[0]; Ah[1] = h[1];
+    Piece g2[2];
+    CBGCHK(row_halves_dt(ctx, dt, B0, g2));
+    Bh[0] = g2[0]; Bh[1] = g2[1];
+  }
+  const int q = G->q;
+  // GetSetSizes: every member's piece sizes (per round) in the row group (A) and column group (B)
+  std::vector<Sizes> myA(R), myB(R), allA((size_t)R * q), allB((size_t)R * q);
+  for (int r = 0; r < R; ++r) {
+    myA[r] = Sizes{Ah[r].nrow, Ah[r].ncol, Ah[r].nnz, aval ? 1 : 0};
+    myB[r] = Sizes{Bh[r].nrow, Bh[r].ncol, Bh[r].nnz, bval ? 1 : 0};
+  }
+  CBGCHK(t_allgather(G, CBG_GROUP_ROW, myA.data(), allA.data(), (int64_t)sizeof(Sizes) * R));
+  CBGCHK(t_allgather(G, CBG_GROUP_COL, myB.data(), allB.data(), (int64_t)sizeof(Sizes) * R));
+  auto SA = [&](int r, int k) -> const Sizes& { return allA[(size_t)k * R + r]; };
+  auto SB = [&](int r, int k) -> const Sizes& { return allB[(size_t)k * R + r]; };
+  // CheckSpGEMMCompliance (ParFriends.h:160-181) for every stage, agreed over the world
+  bool ok = true;
+  for (int r = 0; r < R; ++r)
+    for (int k = 0; k < q; ++k) {
+      ok = ok && SA(r, k).ncol == SB(r, k).nrow && SA(r, k).nrow == SA(0, 0).nrow && SB(r, k).ncol == SB(0, 0).ncol;
+      ok = ok && SA(r, k).has_val == SA(0, 0).has_val && SB(r, k).has_val == SB(0, 0).has_val;
+    }
+  bool all = true;
+  CBGCHK(all_ok(G, ok, &all));
+  if (!all) return CBG_EDIM;
+  // receive slots sized for the largest stage
+  auto bytes_of = [&](const Sizes& s) -> int64_t { return 8 * (s.ncol + 1) + ((4 * s.nnz + 15) & ~15LL) + (int64_t)vs * s.nnz + 16; };
+  int64_t needA = 16, needB = 16;
+  for (int r = 0; r < R; ++r)
+    for (int k = 0; k < q; ++k) {
+      if (k != G->col) needA = std::max(needA, bytes_of(SA(r, k)));
+      if (k != G->row) needB = std::max(needB, bytes_of(SB(r, k)));
+    }
+  if (q > 1)
+    for (int s = 0; s < 2; ++s) { HIPCHK(G->slotA[s].reserve(needA)); HIPCHK(G->slotB[s].reserve(needB)); }
+  const int S = R * q;
+  std::vector<Piece> recvA(S), recvB(S);
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> bev;
+  // stage t = r*q + k: receive (or own) pieces, broadcasts issued on the comm stream
+  auto issue = [&](int t) -> cbg_status {
+    const int r = t / q, k = t % q, slot = t & 1;
+    Piece a, b;
+    if (k == G->col) {
+      a = Ah[r];
+    } else {
+      const Sizes& s = SA(r, k);
+      char* base = G->slotA[slot].as<char>();
+      a.nrow = s.nrow; a.ncol = s.ncol; a.nnz = s.nnz;
+      a.cp = (const int64_t*)base;
+      a.ir = (const int32_t*)(base + 8 * (s.ncol + 1));
+      a.val = s.has_val ? (const void*)(base + 8 * (s.ncol + 1) + ((4 * s.nnz + 15) & ~15LL)) : nullptr;
+    }
+    if (k == G->row) {
+      b = Bh[r];
+    } else {
+      const Sizes& s = SB(r, k);
+      char* base = G->slotB[slot].as<char>();
+      b.nrow = s.nrow; b.ncol = s.ncol; b.nnz = s.nnz;
+      b.cp = (const int64_t*)base;
+      b.ir = (const int32_t*)(base + 8 * (s.ncol + 1));
+      b.val = s.has_val ? (const void*)(base + 8 * (s.ncol + 1) + ((4 * s.nnz + 15) & ~15LL)) : nullptr;
+    }
+    if (q > 1) {
+      hipEvent_t e0, e1;
+      HIPCHK(hipEventCreate(&e0));
+      HIPCHK(hipEventCreate(&e1));
+      if (G->rccl && G->used_rec[slot]) HIPCHK(hipStreamWaitEvent(G->cs, G->ev_used[slot], 0));
+      HIPCHK(hipEventRecord(e0, G->cs));
+      void* ab[3] = {(void*)a.cp, (void*)a.ir, (void*)a.val};
+      int64_t an[3] = {8 * (a.ncol + 1), 4 * a.nnz, a.val ? (int64_t)vs * a.nnz : 0};
+      void* bb[3] = {(void*)b.cp, (void*)b.ir, (void*)b.val};
+      int64_t bn[3] = {8 * (b.ncol + 1), 4 * b.nnz, b.val ? (int64_t)vs * b.nnz : 0};
+      CBGCHK(t_bcast(G, CBG_GROUP_ROW, 3, ab, an, k));
+      CBGCHK(t_bcast(G, CBG_GROUP_COL, 3, bb, bn, k));
+      HIPCHK(hipEventRecord(e1, G->cs));
+      HIPCHK(hipEventRecord(G->ev_comm[slot], G->cs));
+      bev.emplace_back(e0, e1);
+      if (st) st->bcast_bytes += (k == G->col ? 0 : an[0] + an[1] + an[2]) + (k == G->row ? 0 : bn[0] + bn[1] + bn[2]);
+    }
+    recvA[t] = a;
+    recvB[t] = b;
+    return CBG_OK;
+  };
+  hipStream_t cst = ctx->stream;
+  const bool async = G->rccl && q > 1;
+  if (async) CBGCHK(issue(0));
+  std::vector<Piece> acc;   // running merge (Overlap)
+  for (int t = 0; t < S; ++t) {
+    if (async) {
+      if (t + 1 < S) CBGCHK(issue(t + 1));
+      HIPCHK(hipStreamWaitEvent(cst, G->ev_comm[t & 1], 0));
+    } else {
+      CBGCHK(issue(t));
+    }
+    const double t0 = now_ms();
+    cbg_dcsc_view va = view_of(recvA[t], dt, recvA[t].val != nullptr);
+    cbg_dcsc_view vb = view_of(recvB[t], dt, recvB[t].val != nullptr);
+    cbg_csc_result C;
+    int64_t m = 0;
+    CBGCHK(cbg_spgemm_local(ctx, &va, &vb, sr, dt, CBG_SORTED_COLS, &C, &m));
+    if (async) {
+      HIPCHK(hipEventRecord(G->ev_used[t & 1], cst));
+      G->used_rec[t & 1] = true;
+    }
+    if (st) { st->multiplies += m; st->local_ms += now_ms() - t0; ++st->stages; }
+    recvA[t] = Piece();   // drop references to own / received pieces
+    recvB[t] = Piece();
+    Piece P = piece_of_result(C);
+    P.k = t % q;
+    P.r = t / q;
+    if (flags & CBG_RUNNING_MERGE) {
+      if (acc.empty()) {
+        acc.push_back(P);
+      } else if (P.nnz > 0) {
+        const double t1 = now_ms();
+        std::vector<cbg_csc_result> two = {result_of(acc[0], dt), result_of(P, dt)};
+        cbg_csc_result M;
+        CBGCHK(merge_parts(ctx, two, sr, dt, &M));
+        const int32_t k0 = acc[0].k, r0 = acc[0].r;
+        acc.clear();
+        acc.push_back(piece_of_result(M));
+        acc[0].k = k0;
+        acc[0].r = r0;
+        if (st) st->merge_ms += now_ms() - t1;
+      }
+    } else if (P.nnz > 0 || parts->empty()) {
+      if (!parts->empty() && (*parts)[0].nnz == 0) (*parts)[0] = P;   // keep one (empty) part only
+      else parts->push_back(P);
+    }
+  }
+  if (flags & CBG_RUNNING_MERGE) *parts = acc;
+  HIPCHK(hipStreamSynchronize(G->cs));
+  for (auto& e : bev) {
+    float ms = 0.f;
+    (void)hipEventElapsedTime(&ms, e.first, e.second);
+    if (st) st->bcast_ms += ms;
+    (void)hipEventDestroy(e.first);
+    (void)hipEventDestroy(e.second);
+  }
+  return CBG_OK;
+}
+
+// ------------------------------------------------------------------------------------ reduction
+// Fiber all-to-all of one colsplit partial (ParFriends.h:3119-3153, Reductions.h:36-130): layer part m
+// of its columns (block_range(ncol, L, m)) goes to fiber member m; returns the L pieces of this
+// rank's own layer part, in member (layer) order.  The pieces own their receive storage.
+cbg_status fiber_exchange(cbg_grid* G, const Piece& C, size_t vs, std::vector<Piece>* pcs, cbg_grid_stats* st) {
+  cbg_ctx* ctx = G->ctx;
+  hipStream_t cst = ctx->stream;
+  const int L = G->L, me = G->layer;
+  std::vector<int64_t> cbnd(L + 1), eb(L + 1);
+  for (int m = 0; m <= L; ++m) cbnd[m] = m == L ? C.ncol : (C.ncol / L) * m;
+  for (int m = 0; m <= L; ++m) HIPCHK(hipMemcpyAsync(&eb[m], C.cp + cbnd[m], 8, hipMemcpyDeviceToHost, cst));
+  HIPCHK(hipStreamSynchronize(cst));
+  std::vector<int64_t> snnz(L), rnnz(L);
+  for (int m = 0; m < L; ++m) snnz[m] = eb[m + 1] - eb[m];
+  HIPCHK(G->small.reserve(16 * (L + 1)));
+  int64_t* dsn = G->small.as<int64_t>();
+  int64_t* drn = dsn + L;
+  HIPCHK(hipMemcpyAsync(dsn, snnz.data(), 8 * L, hipMemcpyHostToDevice, cst));
+  std::vector<int64_t> eight(L, 8);
+  CBGCHK(t_alltoallv(G, CBG_GROUP_FIBER, dsn, eight.data(), drn, eight.data()));
+  HIPCHK(hipMemcpyAsync(rnnz.data(), drn, 8 * L, hipMemcpyDeviceToHost, cst));
+  HIPCHK(hipStreamSynchronize(cst));
+  const int64_t myc = cbnd[me + 1] - cbnd[me];
+  int64_t rtot = 0;
+  for (int m = 0; m < L; ++m) rtot += rnnz[m];
+  const int64_t ir_bytes = (4 * rtot + 15) & ~15LL;
+  // one owner holds the received rows+values (ir) and counts (val), pieces share it
+  std::shared_ptr<Owner> rx(new Owner(ctx->pool));
+  HIPCHK(rx->ir.reserve(ir_bytes + vs * rtot + 16));
+  HIPCHK(rx->val.reserve(8 * ((int64_t)L * myc + C.ncol + 2)));
+  int64_t* rcnt = rx->val.as<int64_t>();
+  int64_t* scnt = rcnt + (int64_t)L * myc + 1;
+  char* rbase = rx->ir.as<char>();
+  if (C.ncol) k_col_counts<<<(int)grid_for(C.ncol, 256, kMaxGrid), 256, 0, cst>>>(C.ncol, C.cp, scnt);
+  HIPCHK(hipGetLastError());
+  std::vector<int64_t> sb(L), rb(L);
+  for (int m = 0; m < L; ++m) { sb[m] = 8 * (cbnd[m + 1] - cbnd[m]); rb[m] = 8 * myc; }
+  CBGCHK(t_alltoallv(G, CBG_GROUP_FIBER, scnt, sb.data(), rcnt, rb.data()));
+  for (int m = 0; m < L; ++m) { sb[m] = 4 * snnz[m]; rb[m] = 4 * rnnz[m]; }
+  CBGCHK(t_alltoallv(G, CBG_GROUP_FIBER, C.ir + eb[0], sb.data(), rbase, rb.data()));
+  const bool has_val = C.val != nullptr;
+  if (has_val) {
+    for (int m = 0; m < L; ++m) { sb[m] = (int64_t)vs * snnz[m]; rb[m] = (int64_t)vs * rnnz[m]; }
+    CBGCHK(t_alltoallv(G, CBG_GROUP_FIBER, (const char*)C.val + vs * eb[0], sb.data(), rbase + ir_bytes, rb.data()));
+  }
+  if (st)
+    for (int m = 0; m < L; ++m)
+      if (m != me) st->fiber_bytes += (4 + (int64_t)vs) * snnz[m] + 8 * (cbnd[m + 1] - cbnd[m]);
+  pcs->assign(L, Piece());
+  const int64_t ntiles = (myc + kScanTile - 1) / kScanTile;
+  DevBuf tiles, scal;
+  HIPCHK(tiles.reserve(8 * (ntiles + 1)));
+  HIPCHK(scal.reserve(16));
+  int64_t off = 0;
+  for (int m = 0; m < L; ++m) {
+    Piece& p = (*pcs)[m];
+    std::shared_ptr<Owner> o(new Owner(ctx->pool));
+    HIPCHK(o->cp.reserve(8 * (myc + 1)));
+    if (myc > 0) {
+      k_scan_tiles<<<(int)ntiles, 256, 0, cst>>>(myc, rcnt + m * myc, tiles.as<int64_t>());
+      k_scan_sums<<<1, 1024, 0, cst>>>(ntiles, tiles.as<int64_t>(), scal.as<int64_t>());
+      k_scan_apply<<<(int)ntiles, 256, 0, cst>>>(myc, rcnt + m * myc, tiles.as<int64_t>(), o->cp.as<int64_t>());
+    } else {
+      HIPCHK(hipMemsetAsync(o->cp.p, 0, 8, cst));
+    }
+    p.nrow = C.nrow; p.ncol = myc; p.nnz = rnnz[m];
+    p.cp = o->cp.as<int64_t>();
+    p.ir = (const int32_t*)rbase + off;
+    p.val = has_val ? (const void*)(rbase + ir_bytes + vs * off) : nullptr;
+    p.own = o;
+    p.keep = rx;
+    off += rnnz[m];
+  }
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(cst));   // tiles/scal are released on return
+  return CBG_OK;
+}
+
+// hand a piece out as a library result (move its storage when it owns it alone, else copy)
+cbg_status hand_out(cbg_ctx* ctx, Piece& C, cbg_dtype dt, cbg_csc_result* out) {
+  if (C.own && C.own.use_count() == 1 && !C.keep && C.cp == C.own->cp.as<int64_t>() &&
+      C.ir == C.own->ir.as<int32_t>()) {
+    cbg_csc_result r = result_of(C, dt);
+    Owner* o = new Owner(ctx->pool);
+    take(o->cp, C.own->cp);
+    take(o->ir, C.own->ir);
+    take(o->val, C.own->val);
+    r._owner = o;
+    *out = r;
+    C = Piece();
+    return CBG_OK;
+  }
+  cbg_csc_result src = result_of(C, dt);
+  return cbg_col_range(ctx, &src, 0, C.ncol, out);
+}
+
+// parts -> C's colsplit piece.  Duplicates combine with SR::add in the order of the inner dimension:
+// stage k, then layer l, then half r.  For every semiring but Select2nd that order is immaterial, so the
+// stage products are merged first and one partial travels the fiber; Select2nd (first contributor in
+// B's storage order wins, mtSpGEMM.h:583) sends every stage product and merges in (k, l, r) order, so
+// the product is the same on every layout.
+cbg_status reduce_all_impl(cbg_grid* G, std::vector<Piece>& parts, cbg_semiring sr, cbg_dtype dt,
+                           cbg_csc_result* out, cbg_grid_stats* st) {
+  cbg_ctx* ctx = G->ctx;
+  const size_t vs = dt_size(dt);
+  const int L = G->L;
+  const bool ordered = sr == CBG_SR_SELECT2ND;
+  std::stable_sort(parts.begin(), parts.end(),
+                   [](const Piece& a, const Piece& b) { return a.k != b.k ? a.k < b.k : a.r < b.r; });
+  auto merge_into = [&](std::vector<Piece>& ps, Piece* res) -> cbg_status {
+    if (ps.size() == 1) { *res = ps[0]; return CBG_OK; }
+    std::vector<cbg_csc_result> rs;
+    for (auto& p : ps) rs.push_back(result_of(p, dt));
+    cbg_csc_result M;
+    CBGCHK(merge_parts(ctx, rs, sr, dt, &M));
+    *res = piece_of_result(M);
+    return CBG_OK;
+  };
+  Piece C;
+  if (L == 1 || !ordered) {
+    const double t0 = now_ms();
+    CBGCHK(merge_into(parts, &C));
+    parts.clear();
+    if (st) st->merge_ms += now_ms() - t0;
+    if (L == 1) return hand_out(ctx, C, dt, out);
+    const double t1 = now_ms();
+    std::vector<Piece> pcs;
+    CBGCHK(fiber_exchange(G, C, vs, &pcs, st));
+    C = Piece();
+    if (st) st->fiber_ms += now_ms() - t1;
+    const double t2 = now_ms();
+    CBGCHK(merge_into(pcs, &C));
+    pcs.clear();
+    if (st) st->merge_ms += now_ms() - t2;
+    return hand_out(ctx, C, dt, out);
+  }
+  // Select2nd on L > 1 layers: every stage product crosses the fiber on its own
+  const double t1 = now_ms();
+  std::vector<int32_t> ks;
+  std::vector<std::vector<Piece>> got(parts.size());
+  for (size_t i = 0; i < parts.size(); ++i) {
+    ks.push_back(parts[i].k);
+    CBGCHK(fiber_exchange(G, parts[i], vs, &got[i], st));
+  }
+  parts.clear();
+  if (st) st->fiber_ms += now_ms() - t1;
+  const double t2 = now_ms();
+  std::vector<Piece> all;   // (k, l, r) order; parts (hence got) are sorted by (k, r)
+  for (size_t i = 0; i < got.size();) {
+    size_t j = i;
+    while (j < got.size() && ks[j] == ks[i]) ++j;
+    for (int l = 0; l < L; ++l)
+      for (size_t t = i; t < j; ++t) all.push_back(got[t][l]);
+    i = j;
+  }
+  got.clear();
+  CBGCHK(merge_into(all, &C));
+  all.clear();
+  if (st) st->merge_ms += now_ms() - t2;
+  return hand_out(ctx, C, dt, out);
+}
+
+cbg_status grid_common(cbg_ctx* ctx, int32_t world, int32_t rank, int32_t layers, int32_t rows, int32_t cols,
+                       cbg_grid** out) {
+  if (!ctx || !out || world <= 0 || rank < 0 || rank >= world || layers <= 0 || rows <= 0 || rows != cols ||
+      layers * rows * cols != world)
+    return CBG_EINVAL;
+  cbg_grid* G = new cbg_grid;
+  G->ctx = ctx;
+  G->world = world; G->rank = rank; G->L = layers; G->q = rows;
+  G->layer = rank / (rows * cols);
+  G->row = (rank % (rows * cols)) / cols;
+  G->col = rank % cols;
+  HIPCHK(hipSetDevice(ctx->device));
+  HIPCHK(hipStreamCreateWithFlags(&G->cs, hipStreamNonBlocking));
+  for (int i = 0; i < 2; ++i) {
+    HIPCHK(hipEventCreateWithFlags(&G->ev_comm[i], hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&G->ev_used[i], hipEventDisableTiming));
+  }
+  *out = G;
+  return CBG_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+cbg_status cbg_rccl_unique_id(char id[128]) {
+  static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId is 128 bytes");
+  if (!id) return CBG_EINVAL;
+  ncclUniqueId u;
+  NCCLCHK(ncclGetUniqueId(&u));
+  memcpy(id, &u, 128);
+  return CBG_OK;
+}
+
+cbg_status cbg_grid_create_rccl(cbg_ctx* ctx, const char id[128], int32_t world, int32_t rank, int32_t layers,
+                                int32_t rows, int32_t cols, cbg_grid** grid) {
+  if (!id) return CBG_EINVAL;
+  cbg_grid* G = nullptr;
+  CBGCHK(grid_common(ctx, world, rank, layers, rows, cols, &G));
+  G->rccl = true;
+  ncclUniqueId u;
+  memcpy(&u, id, 128);
+  ncclResult_t r = ncclCommInitRank(&G->comm[CBG_GROUP_WORLD], world, u, rank);
+  // sub-communicators: ROW = (layer, row) ordered by col; COL = (layer, col) by row; FIBER = (row, col) by layer
+  if (r == ncclSuccess) r = ncclCommSplit(G->comm[CBG_GROUP_WORLD], G->layer * rows + G->row, G->col, &G->comm[CBG_GROUP_ROW], nullptr);
+  if (r == ncclSuccess) r = ncclCommSplit(G->comm[CBG_GROUP_WORLD], G->layer * cols + G->col, G->row, &G->comm[CBG_GROUP_COL], nullptr);
+  if (r == ncclSuccess) r = ncclCommSplit(G->comm[CBG_GROUP_WORLD], G->row * cols + G->col, G->layer, &G->comm[CBG_GROUP_FIBER], nullptr);
+  if (r != ncclSuccess) {
+    fprintf(stderr, "cbgpu: RCCL grid setup failed: %s\n", ncclGetErrorString(r));
+    cbg_grid_destroy(G);
+    return CBG_ECOMM;
+  }
+  *grid = G;
+  return CBG_OK;
+}
+
+cbg_status cbg_grid_create(cbg_ctx* ctx, const cbg_transport* t, int32_t world, int32_t rank, int32_t layers,
+                           int32_t rows, int32_t cols, cbg_grid** grid) {
+  if (!t || !t->bcast || !t->alltoallv || !t->allgather) return CBG_EINVAL;
+  cbg_grid* G = nullptr;
+  CBGCHK(grid_common(ctx, world, rank, layers, rows, cols, &G));
+  G->cb = *t;
+  *grid = G;
+  return CBG_OK;
+}
+
+cbg_status cbg_grid_destroy(cbg_grid* G) {
+  if (!G) return CBG_OK;
+  (void)hipSetDevice(G->ctx->device);
+  if (G->cs) (void)hipStreamSynchronize(G->cs);
+  for (int g = 0; g < 4; ++g)
+    if (G->comm[g]) (void)ncclCommDestroy(G->comm[g]);
+  for (int i = 0; i < 2; ++i) {
+    if (G->ev_comm[i]) (void)hipEventDestroy(G->ev_comm[i]);
+    if (G->ev_used[i]) (void)hipEventDestroy(G->ev_used[i]);
+  }
+  if (G->cs) (void)hipStreamDestroy(G->cs);
+  delete G;
+  return CBG_OK;
+}
+
+cbg_status cbg_summa_layer(cbg_grid* G, const cbg_dcsc_view* A, const cbg_dcsc_view* B, cbg_semiring sr,
+                           cbg_dtype dt, uint32_t flags, cbg_csc_result* parts, int32_t* nparts,
+                           cbg_grid_stats* st) {
+  if (!G || !A || !B || !parts || !nparts) return CBG_EINVAL;
+  HIPCHK(hipSetDevice(G->ctx->device));
+  if (st) memset(st, 0, sizeof(*st));
+  const double t0 = now_ms();
+  std::vector<Piece> ps;
+  CBGCHK(summa_layer_impl(G, A, B, sr, dt, flags & ~CBG_RUNNING_MERGE, &ps, st));
+  *nparts = 0;
+  for (auto& p : ps) CBGCHK(hand_out(G->ctx, p, dt, &parts[(*nparts)++]));   // stage products, stage order
+  if (st) st->total_ms = now_ms() - t0;
+  return CBG_OK;
+}
+
+cbg_status cbg_reduce_all(cbg_grid* G, const cbg_csc_result* parts, int32_t nparts, cbg_semiring sr, cbg_dtype dt,
+                          cbg_csc_result* C, cbg_grid_stats* st) {
+  if (!G || !parts || nparts <= 0 || !C) return CBG_EINVAL;
+  HIPCHK(hipSetDevice(G->ctx->device));
+  if (st) memset(st, 0, sizeof(*st));
+  const double t0 = now_ms();
+  std::vector<Piece> ps(nparts);
+  for (int i = 0; i < nparts; ++i) {
+    ps[i].nrow = parts[i].nrow; ps[i].ncol = parts[i].ncol; ps[i].nnz = parts[i].nnz;
+    ps[i].cp = parts[i].colptr; ps[i].ir = parts[i].row; ps[i].val = parts[i].val;
+    ps[i].k = i;   // the stage products in stage order
+  }
+  CBGCHK(reduce_all_impl(G, ps, sr, dt, C, st));
+  if (st) st->total_ms = now_ms() - t0;
+  return CBG_OK;
+}
+
+cbg_status cbg_spgemm_grid(cbg_grid* G, const cbg_dcsc_view* A, const cbg_dcsc_view* B, cbg_semiring sr,
+                           cbg_dtype dt, uint32_t flags, cbg_csc_result* C, cbg_grid_stats* st) {
+  if (!G || !A || !B || !C) return CBG_EINVAL;
+  HIPCHK(hipSetDevice(G->ctx->device));
+  if (st) memset(st, 0, sizeof(*st));
+  const double t0 = now_ms();
+  std::vector<Piece> ps;
+  CBGCHK(summa_layer_impl(G, A, B, sr, dt, flags, &ps, st));
+  CBGCHK(reduce_all_impl(G, ps, sr, dt, C, st));
+  if (st) st->total_ms = now_ms() - t0;
+  return CBG_OK;
+}
+
+}  // extern "C"

@@ -259,7 +259,7 @@ def _row_slice(b, r0, r1):
     return Block(r1 - r0, b.ncol, cp, (b.ir[keep] - r0).to(torch.int32), b.val[keep])
 
 
-def _summa_partials(SR, A, B, stats, halves):
+def _summa_partials(SR, A, B, stats, halves, running_merge=False):
     """The q SUMMA stages of one layer.  halves=False: one broadcast pair per stage; halves=True
     (Mult_AnXBn_DoubleBuff, ParFriends.h:799-997): every rank Splits its A piece by columns and its
     B piece by rows at half the inner width (SpDCCols::Split, cut = n/2) and the stages run once per
@@ -308,24 +308,61 @@ def _summa_partials(SR, A, B, stats, halves):
                                   torch.zeros(0, dtype=be.val_dtype, device=be.device)))
         else:
             partials.append(be.multiply(Ak, Bk, SR, stats))
+        if running_merge and len(partials) == 2:   # Mult_AnXBn_Overlap: merge after every stage
+            partials = [be.merge(partials, SR)] if partials[1].nnz else partials[:1]
     nonempty = [p for p in partials if p.nnz]
     return nonempty or partials[:1]
 
 
-def Mult_AnXBn_SUMMA3D(SR, A, B, stats=None, halves=False):
+def _check_operands(A, B, name):
+    if A.ncol != B.nrow:
+        raise _abi.CbgError(_abi.EDIM, name)
+    if not A.colsplit or B.colsplit or B.grid is not A.grid:
+        raise ValueError("A must be colsplit and B rowsplit on the same CommGrid3D")
+
+
+def Mult_AnXBn_SUMMA3D(SR, A, B, stats=None, halves=False, running_merge=False):
     """C = A * B over the semiring on the 3D grid (ParFriends.h:2918-3208).  A must be colsplit,
     B rowsplit, on the same grid; C comes back colsplit.  Dimension checks as CheckSpGEMMCompliance
-    (ParFriends.h:160-181): a mismatch raises (the reference aborts with DIMMISMATCH 3002)."""
+    (ParFriends.h:160-181): a mismatch raises (the reference aborts with DIMMISMATCH 3002).
+
+    On the GPU backend the whole schedule runs inside libcbgpu (cbg_spgemm_grid: RCCL broadcasts on a
+    communication stream, device merges, fiber all-to-all); backends without a native grid (the CPU
+    test backend) run the same schedule here in Python."""
     g = A.grid
-    if A.ncol != B.nrow:
-        raise _abi.CbgError(_abi.EDIM, "Mult_AnXBn_SUMMA3D")
-    if not A.colsplit or B.colsplit or B.grid is not g:
-        raise ValueError("A must be colsplit and B rowsplit on the same CommGrid3D")
+    _check_operands(A, B, "Mult_AnXBn_SUMMA3D")
     be = A.backend
-    partials = _summa_partials(SR, A, B, stats, halves)
+    if hasattr(be, "spgemm_grid"):
+        flags = (_abi.HALVES if halves else 0) | (_abi.RUNNING_MERGE if running_merge else 0)
+        C = be.spgemm_grid(g, A.block, B.block, SR, flags, stats)
+        return SpParMat3D(g, A.nrow, B.ncol, C, True, be)
+    partials = _summa_partials(SR, A, B, stats, halves, running_merge)
     C = partials[0] if len(partials) == 1 else be.merge(partials, SR)
     if g.L > 1:
         C = _fiber_exchange(C, g, be, SR)
+    return SpParMat3D(g, A.nrow, B.ncol, C, True, be)
+
+
+def SUMMALayer(SR, A, B, stats=None):
+    """3DSpGEMM/SUMMALayer.h:24-97: the layer's q SUMMA stages, returning the unmerged stage products
+    (Blocks; the reference's unreducedC list).  The reference hard-codes PlusTimes; any semiring here."""
+    _check_operands(A, B, "SUMMALayer")
+    be = A.backend
+    if hasattr(be, "summa_layer"):
+        return be.summa_layer(A.grid, A.block, B.block, SR, stats)
+    return _summa_partials(SR, A, B, stats, False)
+
+
+def ReduceAll_threaded(SR, unreducedC, A, B):
+    """3DSpGEMM/Reductions.h:134-155: merge the stage products, then the fiber all-to-all of layer
+    column parts and the merge of what arrives; returns C's colsplit piece on A's grid."""
+    g, be = A.grid, A.backend
+    if hasattr(be, "reduce_all"):
+        C = be.reduce_all(g, unreducedC, SR)
+    else:
+        C = unreducedC[0] if len(unreducedC) == 1 else be.merge(unreducedC, SR)
+        if g.L > 1:
+            C = _fiber_exchange(C, g, be, SR)
     return SpParMat3D(g, A.nrow, B.ncol, C, True, be)
 
 
@@ -361,9 +398,14 @@ def Mult_AnXBn_DoubleBuff(SR, A, B, clearA=False, clearB=False, stats=None):
 
 
 def Mult_AnXBn_Overlap(SR, A, B, clearA=False, clearB=False, stats=None):
-    """ParFriends.h:1110-1235: 2D SUMMA with the next stage's non-blocking broadcasts posted before
-    the current local multiply -- what every driver here does (stage k+1 is issued async)."""
-    return Mult_AnXBn_Synch(SR, A, B, clearA, clearB, stats)
+    """ParFriends.h:1110-1235: 2D SUMMA with the next stage's broadcasts in flight during the current
+    local multiply (as in every driver here) and a running merge: the accumulated product is merged
+    with each new stage product (:1187-1189), so at most two partials are alive."""
+    a, b = _as_2d_operands(A, B, "Mult_AnXBn_Overlap")
+    C = Mult_AnXBn_SUMMA3D(SR, a, b, stats, running_merge=True)
+    _clear(A, clearA)
+    _clear(B, clearB and B is not A)
+    return C
 
 
 def _clear(M, flag):
@@ -379,8 +421,8 @@ def PSpGEMM(SR, A, B, stats=None):
 
 
 def multiply(SR, A, B, stats=None):
-    """3DSpGEMM driver entry (Multiplier.h:10-61): split-3D product on the grid A and B live on."""
-    return Mult_AnXBn_SUMMA3D(SR, A, B, stats)
+    """3DSpGEMM driver entry (Multiplier.h:10-61): SUMMALayer, then ReduceAll_threaded."""
+    return ReduceAll_threaded(SR, SUMMALayer(SR, A, B, stats), A, B)
 
 
 # --------------------------------------------------------------------------- indexing via SpGEMM
@@ -691,6 +733,112 @@ class _DevArr:
                                          "data": (int(ptr or 0), False), "version": 2, "strides": None}
 
 
+def _dev_u8(ptr, n, device):
+    """uint8 device tensor viewing n bytes at a HIP device pointer (no copy)."""
+    return torch.as_tensor(_DevArr(ptr, n, "|u1", None), device=device)
+
+
+class _NativeGrid:
+    """libcbgpu's cbg_grid for one CommGrid3D.  torch.distributed on nccl (RCCL): the library's own
+    RCCL communicators (world + ncclCommSplit row/col/fiber; the unique id travels over the default
+    group).  Otherwise (gloo): a cbg_transport whose callbacks stage device buffers through the host
+    and run the collective on the grid's torch process groups."""
+
+    def __init__(self, grid, backend):
+        self.lib = backend.ctx._lib
+        self.grid, self.backend = grid, backend
+        self.ptr = ctypes.c_void_p()
+        L, q = grid.L, grid.q
+        use_rccl = dist.get_backend() == "nccl" and os.environ.get("CBG_GRID_TRANSPORT", "rccl") == "rccl"
+        if use_rccl:
+            uid = torch.zeros(128, dtype=torch.uint8)
+            if grid.rank == 0:
+                buf = ctypes.create_string_buffer(128)
+                _abi.check(self.lib.cbg_rccl_unique_id(buf), "cbg_rccl_unique_id")
+                uid = torch.frombuffer(bytearray(buf.raw), dtype=torch.uint8).clone()
+            t = uid.to(backend.device)
+            dist.broadcast(t, src=0)
+            raw = bytes(t.cpu().numpy().tobytes())
+            idbuf = ctypes.create_string_buffer(raw, 128)
+            _abi.check(self.lib.cbg_grid_create_rccl(backend.ctx._ptr, idbuf, grid.world, grid.rank, L, q, q,
+                                                     ctypes.byref(self.ptr)), "cbg_grid_create_rccl")
+            self.kind = "rccl"
+        else:
+            l, i, j = grid.layer, grid.row, grid.col
+            self.groups = {_abi.GROUP_ROW: grid.row_group, _abi.GROUP_COL: grid.col_group,
+                           _abi.GROUP_FIBER: grid.fiber_group, _abi.GROUP_WORLD: None}
+            self.members = {_abi.GROUP_ROW: [grid.rank_of(l, i, c) for c in range(q)],
+                            _abi.GROUP_COL: [grid.rank_of(l, r, j) for r in range(q)],
+                            _abi.GROUP_FIBER: [grid.rank_of(m, i, j) for m in range(L)],
+                            _abi.GROUP_WORLD: list(range(grid.world))}
+            self._cbs = (_abi.BCAST_FN(self._bcast), _abi.ALLTOALLV_FN(self._alltoallv),
+                         _abi.ALLGATHER_FN(self._allgather))
+            self.transport = _abi.Transport(None, *self._cbs)
+            _abi.check(self.lib.cbg_grid_create(backend.ctx._ptr, ctypes.byref(self.transport), grid.world, grid.rank,
+                                                L, q, q, ctypes.byref(self.ptr)), "cbg_grid_create")
+            self.kind = "host-staged " + dist.get_backend()
+
+    # -- transport callbacks (gloo): return 0 on success, never raise into C
+    def _bcast(self, user, g, buf, nbytes, root):
+        try:
+            dev = self.backend.device
+            t = _dev_u8(buf, nbytes, dev)
+            src = self.members[g][root]
+            h = t.cpu() if src == self.grid.rank else torch.empty(nbytes, dtype=torch.uint8)
+            dist.broadcast(h, src=src, group=self.groups[g])
+            if src != self.grid.rank:
+                t.copy_(h)
+            torch.cuda.current_stream(dev).synchronize()
+            return 0
+        except Exception as e:  # pragma: no cover - reported through CBG_ECOMM
+            print(f"cbg transport bcast: {e!r}", flush=True)
+            return 1
+
+    def _alltoallv(self, user, g, send, sbytes, recv, rbytes):
+        try:
+            dev = self.backend.device
+            P = len(self.members[g])
+            sb = [int(sbytes[m]) for m in range(P)]
+            rb = [int(rbytes[m]) for m in range(P)]
+            s = _dev_u8(send, sum(sb), dev).cpu() if sum(sb) else torch.empty(0, dtype=torch.uint8)
+            r = torch.empty(sum(rb), dtype=torch.uint8)
+            dist.all_to_all_single(r, s, output_split_sizes=rb, input_split_sizes=sb, group=self.groups[g])
+            if sum(rb):
+                _dev_u8(recv, sum(rb), dev).copy_(r)
+            torch.cuda.current_stream(dev).synchronize()
+            return 0
+        except Exception as e:  # pragma: no cover
+            print(f"cbg transport alltoallv: {e!r}", flush=True)
+            return 1
+
+    def _allgather(self, user, g, send, recv, nbytes):
+        try:
+            P = len(self.members[g])
+            mine = torch.frombuffer(bytearray(ctypes.string_at(send, nbytes)), dtype=torch.uint8)
+            out = [torch.empty(nbytes, dtype=torch.uint8) for _ in range(P)]
+            dist.all_gather(out, mine, group=self.groups[g])
+            allb = torch.cat(out).numpy().tobytes()
+            ctypes.memmove(recv, allb, nbytes * P)
+            return 0
+        except Exception as e:  # pragma: no cover
+            print(f"cbg transport allgather: {e!r}", flush=True)
+            return 1
+
+    def close(self):
+        if self.ptr:
+            self.lib.cbg_grid_destroy(self.ptr)
+            self.ptr = ctypes.c_void_p()
+
+
+def _stats_update(stats, st):
+    if stats is None:
+        return
+    stats["multiplies"] = stats.get("multiplies", 0) + int(st.multiplies)
+    for k in ("bcast_bytes", "fiber_bytes", "bcast_ms", "local_ms", "merge_ms", "fiber_ms", "total_ms"):
+        stats[k] = stats.get(k, 0) + getattr(st, k)
+    stats["stages"] = stats.get("stages", 0) + int(st.stages)
+
+
 class GpuBackend:
     """Local multiply / merge on the MI355X through libcbgpu; blocks live in HBM as torch tensors.
     libcbgpu runs on torch's current stream, so RCCL waits order against it."""
@@ -776,6 +924,50 @@ class GpuBackend:
                                                ctypes.byref(st)), "cbg_mcl_prune")
         return self._take(res, "merge"), {"recovered": st.recovered, "selected": st.selected,
                                           "recovered_after_select": st.recovered_after_select}
+
+    # ------------------------------------------------------------------ native grid (cbg_grid)
+    def native_grid(self, grid):
+        key = id(grid)
+        if not hasattr(self, "_grids"):
+            self._grids = {}
+        if key not in self._grids:
+            self._grids[key] = (grid, _NativeGrid(grid, self))   # keep grid alive with its handle
+        return self._grids[key][1]
+
+    def spgemm_grid(self, grid, A, B, sr, flags=0, stats=None):
+        ng = self.native_grid(grid)
+        va, vb = self._view(A), self._view(B)
+        res, st = _abi.CscResult(), _abi.GridStats()
+        _abi.check(self.ctx._lib.cbg_spgemm_grid(ng.ptr, ctypes.byref(va), ctypes.byref(vb), sr.code, sr.dtype,
+                                                 _abi.SORTED_COLS | flags, ctypes.byref(res), ctypes.byref(st)),
+                   "cbg_spgemm_grid")
+        _stats_update(stats, st)
+        return self._take(res)
+
+    def summa_layer(self, grid, A, B, sr, stats=None):
+        ng = self.native_grid(grid)
+        va, vb = self._view(A), self._view(B)
+        parts = (_abi.CscResult * (2 * grid.q))()
+        n, st = ctypes.c_int32(0), _abi.GridStats()
+        _abi.check(self.ctx._lib.cbg_summa_layer(ng.ptr, ctypes.byref(va), ctypes.byref(vb), sr.code, sr.dtype,
+                                                 _abi.SORTED_COLS, parts, ctypes.byref(n), ctypes.byref(st)),
+                   "cbg_summa_layer")
+        _stats_update(stats, st)
+        out = []
+        for k in range(n.value):
+            r = _abi.CscResult()
+            ctypes.pointer(r)[0] = parts[k]
+            out.append(self._take(r))
+        return out
+
+    def reduce_all(self, grid, parts, sr, stats=None):
+        ng = self.native_grid(grid)
+        arr = (_abi.CscResult * len(parts))(*[self._res_view(p) for p in parts])
+        res, st = _abi.CscResult(), _abi.GridStats()
+        _abi.check(self.ctx._lib.cbg_reduce_all(ng.ptr, arr, len(parts), sr.code, sr.dtype, ctypes.byref(res),
+                                                ctypes.byref(st)), "cbg_reduce_all")
+        _stats_update(stats, st)
+        return self._take(res)
 
     def merge(self, parts, sr):
         arr = (_abi.CscResult * len(parts))(*[self._res_view(p) for p in parts])

@@ -196,6 +196,84 @@ cbg_status cbg_col_select(cbg_ctx* ctx, const cbg_csc_result* in, const int64_t*
 /* Horizontal concatenation of nparts device CSCs with equal nrow/val_type. */
 cbg_status cbg_col_concat(cbg_ctx* ctx, const cbg_csc_result* parts, int32_t nparts, cbg_csc_result* out);
 
+/*
+ * ---------------------------------------------------------------------------------------------
+ * Distributed SpGEMM on a layers x rows x cols process grid, one process (rank) per GPU.
+ *
+ *   cbg_grid_create_rccl / cbg_grid_create   CommGrid3D(world, nlayers, rows, cols)
+ *                                            include/CombBLAS/CommGrid3D.h:21-80 (CommGrid, src/CommGrid.cpp:37-76)
+ *   cbg_spgemm_grid    Mult_AnXBn_SUMMA3D(A3D, B3D)              include/CombBLAS/ParFriends.h:2918-3208
+ *                      Mult_AnXBn_Synch / PSpGEMM (one layer)     ParFriends.h:1004-1108, SpParMat.h:451-464
+ *                      Mult_AnXBn_DoubleBuff (CBG_HALVES)         ParFriends.h:798-997
+ *                      Mult_AnXBn_Overlap (CBG_RUNNING_MERGE)     ParFriends.h:1110-1235
+ *   cbg_summa_layer    SUMMALayer(splitA, splitB, unreducedC, CMG) 3DSpGEMM/SUMMALayer.h:24-97
+ *   cbg_reduce_all     ReduceAll_threaded(unreducedC, CMG)        3DSpGEMM/Reductions.h:134-155
+ *                      (multiply() = SUMMALayer + ReduceAll_threaded, 3DSpGEMM/Multiplier.h:10-61)
+ *
+ * Rank r = (l, i, j) with r = l*rows*cols + i*cols + j (CommGrid3D::GetRank, CommGrid3D.h:90-91);
+ * rows == cols = q (SUMMA needs a square layer grid, CommGrid.cpp:44-50).  Groups, members in
+ * increasing rank order: ROW = {(l,i,*)} (member index j), COL = {(l,*,j)} (member i), FIBER =
+ * {(*,i,j)} (member l), WORLD (member r).  Layout (SpParMat3D, non-special, SpParMat3D.cpp:337-444):
+ * the inner dimension's block k is cut into L layer parts; rank (l,i,j) holds the A piece
+ * A[row block i, layer-l part of column block j] ("colsplit") and the B piece B[layer-l part of row
+ * block i, column block j] ("rowsplit"); the product's piece comes back colsplit.  Layer l runs q SUMMA stages (stage k: A piece (l,i,k) broadcast along ROW, B piece
+ * (l,k,j) along COL: BCastMatrix, SpParHelper.cpp:583-600, sizes exchanged first as GetSetSizes,
+ * :798-809), multiplies locally (cbg_spgemm_local) and merges the q partials (cbg_merge); with L > 1
+ * the fiber exchanges layer column parts (all-to-all-v, ParFriends.h:3119-3153) and merges them in
+ * layer order.  Everything stays in HBM; with RCCL the next stage's broadcasts run on a
+ * communication stream while the current stage multiplies.
+ *
+ * Every call is collective over the grid.  Pieces are views (host or device, CSC or DCSC); results
+ * are library-owned device CSCs (cbg_result_free).
+ */
+typedef enum { CBG_GROUP_ROW = 0, CBG_GROUP_COL = 1, CBG_GROUP_FIBER = 2, CBG_GROUP_WORLD = 3 } cbg_group;
+
+/* Caller-provided transport (e.g. MPI on the reference side, gloo in tests).  bcast / alltoallv get
+ * DEVICE buffers of the grid's device (the library has synchronised its streams before the call);
+ * allgather gets HOST buffers.  root / segment order = member index in the group.  Return 0 on
+ * success; anything else makes the library return CBG_ECOMM. */
+typedef struct {
+  void* user;
+  int32_t (*bcast)(void* user, int32_t group, void* buf, int64_t bytes, int32_t root);
+  int32_t (*alltoallv)(void* user, int32_t group, const void* send, const int64_t* send_bytes, void* recv,
+                       const int64_t* recv_bytes);
+  int32_t (*allgather)(void* user, int32_t group, const void* send, void* recv, int64_t bytes);
+} cbg_transport;
+
+typedef struct cbg_grid cbg_grid;
+
+/* flags of cbg_spgemm_grid / cbg_summa_layer (besides CBG_SORTED_COLS) */
+#define CBG_HALVES 4u          /* Mult_AnXBn_DoubleBuff: operands split in two along the inner dim, 2q stages */
+#define CBG_RUNNING_MERGE 8u   /* Mult_AnXBn_Overlap: merge the accumulated product after every stage */
+
+typedef struct {
+  int64_t multiplies;          /* this rank's local multiplies */
+  int64_t bcast_bytes, fiber_bytes;
+  double bcast_ms, local_ms, merge_ms, fiber_ms, total_ms;
+  int32_t stages;
+} cbg_grid_stats;
+
+/* RCCL unique id (128 bytes) made on one rank and handed to all (any out-of-band channel). */
+cbg_status cbg_rccl_unique_id(char id[128]);
+/* Grid over RCCL communicators (world + ncclCommSplit row/col/fiber), on ctx's device and stream. */
+cbg_status cbg_grid_create_rccl(cbg_ctx* ctx, const char id[128], int32_t world, int32_t rank, int32_t layers,
+                                int32_t rows, int32_t cols, cbg_grid** grid);
+/* Grid over a caller-provided transport (copied; `user` must outlive the grid). */
+cbg_status cbg_grid_create(cbg_ctx* ctx, const cbg_transport* t, int32_t world, int32_t rank, int32_t layers,
+                           int32_t rows, int32_t cols, cbg_grid** grid);
+cbg_status cbg_grid_destroy(cbg_grid* grid);
+
+/* C piece = A (x) B over the grid.  Dimension mismatch on any rank -> CBG_EDIM on every rank. */
+cbg_status cbg_spgemm_grid(cbg_grid* grid, const cbg_dcsc_view* A, const cbg_dcsc_view* B, cbg_semiring sr,
+                           cbg_dtype out_type, uint32_t flags, cbg_csc_result* C, cbg_grid_stats* stats);
+/* The layer SUMMA alone: the unmerged stage products (at most 2*rows entries of `parts`; *nparts set). */
+cbg_status cbg_summa_layer(cbg_grid* grid, const cbg_dcsc_view* A, const cbg_dcsc_view* B, cbg_semiring sr,
+                           cbg_dtype out_type, uint32_t flags, cbg_csc_result* parts, int32_t* nparts,
+                           cbg_grid_stats* stats);
+/* Merge the stage products, then (L > 1) the fiber exchange + merge: the rank's colsplit C piece. */
+cbg_status cbg_reduce_all(cbg_grid* grid, const cbg_csc_result* parts, int32_t nparts, cbg_semiring sr,
+                          cbg_dtype out_type, cbg_csc_result* C, cbg_grid_stats* stats);
+
 #ifdef __cplusplus
 }
 #endif

@@ -22,7 +22,8 @@
  *                    followed by a CORRECT row sort (the reference's PBBS integerSort
  *                    mis-sorts when the column's max row is a power of two,
  *                    include/CombBLAS/PBBS/radixSort.h:116-120).
- *   orc_merge        MultiwayMerge              include/CombBLAS/MultiwayMerge.h:411-526
+ *   orc_merge        MultiwayMergeHash order    include/CombBLAS/MultiwayMerge.h:536-684 (SerialMergeHash 320-405);
+ *                    = MultiwayMerge (411-526) except Select2nd ties, pinned by tests/golden/merge.npz
  *                    (duplicates combined with SR::add in list order).
  *   orc_mcl_prune    MCLPruneRecoverySelect     include/CombBLAS/ParFriends.h:185-353 on one
  *                    rank (column statistics of Prune(less_equal thr) in storage order,
@@ -206,8 +207,12 @@ int orc_symbolic(const orc_csc* A, const orc_csc* B, int64_t* nnz_per_col, int64
     if (adderr) return ORC_EADD;                                                           \
     return bad ? ORC_ENOMEM : ORC_OK;                                                      \
   }                                                                                        \
-  /* MultiwayMerge: lists are column-sorted CSCs of equal shape; duplicates combined  */   \
-  /* in list order: acc = add(next, acc) keeps the same argument order as the hash.   */   \
+  /* Multi-list merge in MultiwayMergeHash order (SerialMergeHash, MultiwayMerge.h:320-405):  */ \
+  /* lists are column-sorted CSCs of equal shape; duplicates combined in list order,           */ \
+  /* acc = add(next, acc) = SR::add(curval, existing) (:357): for Select2nd the first list     */ \
+  /* wins.  The heap MultiwayMerge (SerialMerge, :184-231) calls SR::add(existing, new) in     */ \
+  /* heap-pop order instead, which differs for Select2nd only; tests/golden/merge.npz holds    */ \
+  /* both reference outputs, and this order is the one equal to the 1-rank product (min-k).    */ \
   static int merge_##SUF(int sr, int nl, const orc_csc* L, int64_t* cp_out, int32_t* ir_out, \
                          T* val_out, int count_only) {                                     \
     int64_t ncol = L[0].ncol, nrow = L[0].nrow;                                            \

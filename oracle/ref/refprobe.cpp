@@ -14,6 +14,7 @@
 //   SpParMat::ParallelReadMM include/CombBLAS/SpParMat.cpp:3922
 //   MCLPruneRecoverySelect include/CombBLAS/ParFriends.h:185-353 (kselectVersion 1)
 //   MemEfficientSpGEMM include/CombBLAS/ParFriends.h:449-730 (hash kernel, phases)
+//   MultiwayMerge / MultiwayMergeHash include/CombBLAS/MultiwayMerge.h:411-526, 536-684 (k lists)
 // Because of the reference's integerSort off-by-one every product is
 // re-sorted column-major with SpTuples::SortColBased before it is written, so
 // fixtures hold the mathematically defined product (rows ascending per column).
@@ -202,6 +203,42 @@ static int run_memeff(const char* fa, int phases, double thr, long sel, long rec
   return 0;
 }
 
+// k column-sorted lists merged by the reference's heap MultiwayMerge (MultiwayMerge.h:411-526) and hash
+// MultiwayMergeHash (:536-684), both written out (outputs re-sorted column-major, as everywhere here).
+template <class SR, class NT>
+static int run_merge_t(int k, char** files, const char* out_heap, const char* out_hash) {
+  std::vector<RawCsc> raw;
+  for (int i = 0; i < k; ++i) raw.push_back(read_bin(files[i]));
+  const I m = raw[0].nrow, n = raw[0].ncol;
+  auto lists = [&]() {
+    std::vector<SpTuples<I, NT>*> L;
+    for (auto& R : raw) {
+      SpDCCols<I, NT>* D = to_dcc<NT>(R);
+      SpTuples<I, NT>* T = new SpTuples<I, NT>(*D);
+      T->SortColBased();
+      delete D;
+      L.push_back(T);
+    }
+    return L;
+  };
+  std::vector<SpTuples<I, NT>*> l1 = lists(), l2 = lists();
+  SpTuples<I, NT>* h = MultiwayMerge<SR>(l1, m, n, true);
+  SpTuples<I, NT>* g = MultiwayMergeHash<SR>(l2, m, n, true, true);
+  write_tuples<NT>(out_heap, *h, m, n);
+  write_tuples<NT>(out_hash, *g, m, n);
+  printf("{\"merge\":%d,\"nnz_heap\":%ld,\"nnz_hash\":%ld}\n", k, (long)h->getnnz(), (long)g->getnnz());
+  delete h; delete g;
+  return 0;
+}
+
+static int run_merge(const char* sr, int k, char** files, const char* oh, const char* og) {
+  std::string s(sr);
+  if (s == "select2nd_i64") return run_merge_t<Select2ndSRing<int64_t, int64_t, int64_t>, int64_t>(k, files, oh, og);
+  if (s == "plus_times_i64") return run_merge_t<PlusTimesSRing<int64_t, int64_t>, int64_t>(k, files, oh, og);
+  if (s == "min_plus_i64") return run_merge_t<MinPlusSRing<int64_t, int64_t>, int64_t>(k, files, oh, og);
+  fprintf(stderr, "unknown semiring %s\n", sr); return 2;
+}
+
 int main(int argc, char** argv) {
   int prov; MPI_Init_thread(&argc, &argv, MPI_THREAD_SERIALIZED, &prov);
   int rc = 2;
@@ -213,11 +250,13 @@ int main(int argc, char** argv) {
     else if (cmd == "readmm" && argc == 4) rc = run_readmm(argv[2], argv[3]);
     else if (cmd == "mcl" && argc == 8)
       rc = run_mcl(argv[2], atof(argv[3]), atol(argv[4]), atol(argv[5]), atof(argv[6]), argv[7]);
+    else if (cmd == "merge" && argc >= 6 && argc == 6 + atoi(argv[3]))
+      rc = run_merge(argv[2], atoi(argv[3]), argv + 4, argv[4 + atoi(argv[3])], argv[5 + atoi(argv[3])]);
     else if (cmd == "memeff" && argc == 9)
       rc = run_memeff(argv[2], atoi(argv[3]), atof(argv[4]), atol(argv[5]), atol(argv[6]), atof(argv[7]), argv[8]);
   }
   if (rc == 2 && argc < 3)
-    fprintf(stderr, "usage: refprobe mult <sr> <hash|hash_unsorted|heap|hybrid> A.bin B.bin C.bin | synch A B C | gen scale ef out | readmm in.mtx out | mcl A thr sel rec pct out | memeff A phases thr sel rec pct out\n");
+    fprintf(stderr, "usage: refprobe mult <sr> <hash|hash_unsorted|heap|hybrid> A.bin B.bin C.bin | synch A B C | gen scale ef out | readmm in.mtx out | mcl A thr sel rec pct out | memeff A phases thr sel rec pct out | merge <sr> k L1..Lk heap.out hash.out\n");
   MPI_Finalize();
   return rc;
 }

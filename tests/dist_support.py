@@ -273,3 +273,80 @@ def run_index_case(rank, world, port, backend_kind, cases, errq):
         import traceback
         errq.put(f"rank {rank}: {e!r}\n{traceback.format_exc()}")
         raise
+
+
+def _sr_obj(sr, dt):
+    import combblas_amd as cb
+    return {"plus_times": cb.PlusTimesSRing, "min_plus": cb.MinPlusSRing, "select2nd": cb.Select2ndSRing,
+            "select_max": cb.SelectMaxSRing, "select_max_bool": cb.SelectMaxBoolSRing}[sr](dt)
+
+
+def check_piece_exact_or_f64(M, R, rank, what, scale=None, rtol=1e-12):
+    """M's local piece against the same block of the global CSC R (helpers.Csc or scipy): structure
+    exact; values bit-exact, or |c - r| <= rtol * max(|r|, scale) when `scale` (a global scipy
+    matrix of sum|a*b|) is given."""
+    R = sp.csc_matrix(R)
+    (r0, r1), (c0, c1) = M.local_range()
+    Rl = R[r0:r1, c0:c1].tocsc()
+    Rl.sort_indices()
+    blk = M.block
+    assert (blk.nrow, blk.ncol) == (r1 - r0, c1 - c0), (what, blk.nrow, blk.ncol)
+    cp, ir, val = blk.cp.cpu().numpy(), blk.ir.cpu().numpy(), blk.val.cpu().numpy()
+    assert np.array_equal(cp, Rl.indptr), f"rank {rank} {what}: colptr differs ({cp[-1]} vs {Rl.indptr[-1]})"
+    assert np.array_equal(ir, Rl.indices), f"rank {rank} {what}: rows differ"
+    if scale is None:
+        assert np.array_equal(val.astype(np.float64), Rl.data.astype(np.float64)), f"rank {rank} {what}: values differ"
+    else:
+        S = sp.csc_matrix(scale)[r0:r1, c0:c1].tocsc()
+        cols = np.repeat(np.arange(c1 - c0), np.diff(Rl.indptr))
+        s = np.maximum(np.abs(Rl.data), np.asarray(S[Rl.indices, cols]).ravel())
+        bad = np.abs(val - Rl.data) > rtol * s
+        assert not bad.any(), f"rank {rank} {what}: {int(bad.sum())} values off"
+
+
+def run_fixture_case(rank, world, port, backend_kind, cases, errq):
+    """Per-rank body: the reference's own golden products (tests/golden, made by the reference-built
+    refprobe) through the mandated layout for `world` (1x1x2, 2x2, 2x2x2), every semiring of the
+    fixture, with Mult_AnXBn_SUMMA3D and -- on one-layer grids -- Synch / DoubleBuff / Overlap, and
+    the 3DSpGEMM multiply (SUMMALayer + ReduceAll_threaded).  Each rank checks its own piece."""
+    try:
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        L, q, _ = cbd.grid_for(world)
+        grid = cbd.CommGrid3D(L, q, q)
+        import combblas_amd as cb
+        be = cbd.GpuBackend(cb.Context(0)) if backend_kind == "gpu" else ScipyBackend()
+        from helpers import abs_product_sums, fixture_inputs, fixture_product, load_fixture
+        for (name, tag, golden) in cases:
+            z = load_fixture(name)
+            A, B, sr, dt = fixture_inputs(z, tag)
+            aval = A.val if A.val is not None else np.ones(A.nnz, np.uint8)
+            Ad = cbd.SpParMat3D.from_global_csc(grid, A.nrow, A.ncol, A.cp, A.ir, aval, True, be)
+            Bd = cbd.SpParMat3D.from_global_csc(grid, B.nrow, B.ncol, B.cp, B.ir, B.val, False, be)
+            R = fixture_product(z, tag)
+            Rs = sp.csc_matrix((R.val, R.ir, R.cp), shape=(A.nrow, B.ncol))
+            scale = abs_product_sums(A, B) if dt == "f64" and sr == "plus_times" else None
+            SR = _sr_obj(sr, dt)
+            stats = {}
+            drivers = [("SUMMA3D", lambda: cbd.Mult_AnXBn_SUMMA3D(SR, Ad, Bd, stats)),
+                       ("multiply", lambda: cbd.multiply(SR, Ad, Bd))]
+            if L == 1:
+                drivers += [(f.__name__, (lambda f=f: f(SR, Ad, Bd)))
+                            for f in (cbd.Mult_AnXBn_Synch, cbd.Mult_AnXBn_DoubleBuff, cbd.Mult_AnXBn_Overlap)]
+            for dname, run in drivers:
+                C = run()
+                check_piece_exact_or_f64(C, Rs, rank, f"{name}/{tag}/{dname}", scale)
+                if golden is not None:   # MATLAB's bcsstk01^2 (3DSpGEMM/matlab/C.mtx), as test_mpipspgemm
+                    G = sp.csc_matrix((z[golden + "_val"], z[golden + "_ir"], z[golden + "_cp"]),
+                                      shape=(A.nrow, B.ncol))
+                    check_piece_exact_or_f64(C, G, rank, f"{name}/matlab/{dname}", scale)
+            t = torch.tensor([stats.get("multiplies", 0)], dtype=torch.int64)
+            dist.all_reduce(t)
+            assert int(t.item()) == int(z[f"C_{tag}_flops"]), (int(t.item()), int(z[f"C_{tag}_flops"]))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:
+        import traceback
+        errq.put(f"rank {rank}: {e!r}\n{traceback.format_exc()}")
+        raise

@@ -69,6 +69,18 @@ def canonical_sha256(cp, ir, val):
 
 
 # ---------------------------------------------------------------------------------- oracle
+_CT = {np.dtype(np.uint8): ctypes.c_uint8, np.dtype(np.int32): ctypes.c_int32, np.dtype(np.int64): ctypes.c_int64,
+       np.dtype(np.float32): ctypes.c_float, np.dtype(np.float64): ctypes.c_double}
+
+
+def _copy_out(ptr, n, dtype):
+    """n elements of `dtype` at a C pointer, copied (no 2/4 GiB limit, unlike ctypes.string_at)."""
+    dtype = np.dtype(dtype)
+    if n == 0:
+        return np.zeros(0, dtype)
+    return np.ctypeslib.as_array(ctypes.cast(ptr, ctypes.POINTER(_CT[dtype])), (n,)).copy()
+
+
 class _OrcCsc(ctypes.Structure):
     _fields_ = [("nrow", ctypes.c_int64), ("ncol", ctypes.c_int64), ("nnz", ctypes.c_int64),
                 ("cp", ctypes.c_void_p), ("ir", ctypes.c_void_p), ("val", ctypes.c_void_p)]
@@ -115,9 +127,8 @@ def oracle_spgemm(A, B, sr, dt, sort=True):
         return None, fl.value, rc
     n = nnz.value
     dtype = NP_DT[DT[dt]]
-    ir = np.ctypeslib.as_array(ctypes.cast(ir_p, ctypes.POINTER(ctypes.c_int32)), (max(n, 1),))[:n].copy()
-    raw = ctypes.string_at(val_p, n * np.dtype(dtype).itemsize)
-    val = np.frombuffer(raw, dtype).copy()
+    ir = _copy_out(ir_p, n, np.int32)
+    val = _copy_out(val_p, n, dtype)
     lib.orc_free(ir_p)
     lib.orc_free(val_p)
     return Csc(A.nrow, B.ncol, cp, ir, val), fl.value, 0
@@ -136,8 +147,8 @@ def oracle_merge(parts, sr, dt):
         return None, rc
     n = nnz.value
     dtype = NP_DT[DT[dt]]
-    ir = np.ctypeslib.as_array(ctypes.cast(ir_p, ctypes.POINTER(ctypes.c_int32)), (max(n, 1),))[:n].copy()
-    val = np.frombuffer(ctypes.string_at(val_p, n * np.dtype(dtype).itemsize), dtype).copy()
+    ir = _copy_out(ir_p, n, np.int32)
+    val = _copy_out(val_p, n, dtype)
     lib.orc_free(ir_p)
     lib.orc_free(val_p)
     return Csc(parts[0].nrow, ncol, cp, ir, val), 0
@@ -196,8 +207,8 @@ def oracle_mcl_prune(A, thr, select, recover, pct):
                            ctypes.byref(ir_p), ctypes.byref(val_p), st.ctypes.data)
     assert rc == 0
     n = int(cp[-1])
-    ir = np.ctypeslib.as_array(ctypes.cast(ir_p, ctypes.POINTER(ctypes.c_int32)), (max(n, 1),))[:n].copy()
-    val = np.frombuffer(ctypes.string_at(val_p, n * 8), np.float64).copy()
+    ir = _copy_out(ir_p, n, np.int32)
+    val = _copy_out(val_p, n, np.float64)
     lib.orc_free(ir_p)
     lib.orc_free(val_p)
     return Csc(A.nrow, A.ncol, cp, ir, val), tuple(int(x) for x in st)

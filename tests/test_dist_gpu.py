@@ -33,3 +33,18 @@ def test_2d_drivers_and_indexing_gloo_gpu(world, port):
     PlusTimes for SubsRef_SR / SpAsgn) through libcbgpu, exact against scipy."""
     from dist_support import run_index_case
     spawn_case(world, "gpu", INDEX_CASES, port, body=run_index_case)
+
+
+FIXTURE_CASES = [("bcsstk01", "pt_f64_hash", "M_matlab")] + \
+    [("g500_s10", t, None) for t in ("pt_f64_hash", "pt_i64_hash", "mp_i64_hash", "s2_i64_hash", "sm_i64_hash",
+                                     "smb_i64_hash")]
+
+
+@pytest.mark.parametrize("world,port", [(2, 29631), (4, 29632), (8, 29633)])
+def test_reference_fixtures_through_layouts_gloo_gpu(world, port):
+    """The reference's golden products (bcsstk01^2 + MATLAB C.mtx as test_mpipspgemm.cpp:101-153 does,
+    G500 s10 under PlusTimes f64/i64, MinPlus, Select2nd, SelectMax, SelectMax<bool>) through the
+    1x1x2 / 2x2 / 2x2x2 layouts on libcbgpu's native grid (cbg_spgemm_grid), every rank's piece
+    checked; Select2nd included (merges follow the inner dimension's order on every layout)."""
+    from dist_support import run_fixture_case
+    spawn_case(world, "gpu", FIXTURE_CASES, port, body=run_fixture_case)

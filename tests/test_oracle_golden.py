@@ -112,3 +112,40 @@ def test_oracle_boolcopy_add_is_error():
     B1 = Csc(2, 1, [0, 1], [1], np.array([4], np.int64))
     C, _, rc = oracle_spgemm(A, B1, "bool_copy2nd", "i64")
     assert rc == 0 and C.val.tolist() == [4]
+
+
+MERGE_SETS = [("split", "select2nd_i64"), ("split", "plus_times_i64"), ("rand", "select2nd_i64"),
+              ("rand", "plus_times_i64"), ("rand", "min_plus_i64")]
+
+
+def merge_lists(z, which):
+    m, n = (int(x) for x in z[f"{which}_shape"])
+    return [Csc(m, n, z[f"{which}_L{l}_cp"], z[f"{which}_L{l}_ir"], z[f"{which}_L{l}_val"])
+            for l in range(int(z[f"{which}_k"]))]
+
+
+@pytest.mark.parametrize("which,sr", MERGE_SETS)
+def test_oracle_merge_matches_reference_multiwaymergehash(which, sr):
+    """The oracle's multi-list merge equals the reference's MultiwayMergeHash (first list wins for
+    Select2nd, MultiwayMerge.h:357) on reference-made partials; the heap MultiwayMerge agrees on every
+    semiring except Select2nd, whose heap-pop order keeps a later list's value."""
+    z = load_fixture("merge")
+    lists = merge_lists(z, which)
+    s, dt = sr.rsplit("_", 1)
+    R, rc = oracle_merge(lists, s, dt)
+    assert rc == 0
+    H = Csc(0, len(z[f"{which}_{sr}_hash_cp"]) - 1, z[f"{which}_{sr}_hash_cp"], z[f"{which}_{sr}_hash_ir"],
+            z[f"{which}_{sr}_hash_val"])
+    assert np.array_equal(R.cp, H.cp) and np.array_equal(R.ir, H.ir) and np.array_equal(R.val, H.val)
+    heap_same = np.array_equal(z[f"{which}_{sr}_heap_val"], H.val)
+    assert heap_same == (s != "select2nd")
+
+
+def test_merged_split_products_equal_the_product_select2nd():
+    """Merging the inner-dimension split products in part order reproduces the 1-rank Select2nd
+    product (min-k rule): the reference's MultiwayMergeHash output equals LocalSpGEMMHash's."""
+    z = load_fixture("merge")
+    f = load_fixture("g500_s10")
+    assert np.array_equal(z["split_select2nd_i64_hash_cp"], f["C_s2_i64_hash_cp"])
+    assert np.array_equal(z["split_select2nd_i64_hash_ir"], f["C_s2_i64_hash_ir"])
+    assert np.array_equal(z["split_select2nd_i64_hash_val"], f["C_s2_i64_hash_val"])

@@ -411,3 +411,20 @@ def test_gpu_bpos_guard(gpu_ctx):
         st = gpu_ctx._lib.cbg_spgemm_local(gpu_ctx._ptr, ctypes.byref(va), ctypes.byref(vb), sr, _abi.I64, 1,
                                            ctypes.byref(res), ctypes.byref(m))
         assert st == _abi.EUNSUP
+
+
+@pytest.mark.parametrize("which,sr", [("split", "select2nd_i64"), ("split", "plus_times_i64"),
+                                      ("rand", "select2nd_i64"), ("rand", "plus_times_i64"),
+                                      ("rand", "min_plus_i64")])
+def test_gpu_merge_matches_reference_multiwaymergehash(gpu_ctx, which, sr):
+    """cbg_merge equals the reference's MultiwayMergeHash on reference-made lists (tests/golden/merge.npz,
+    refprobe `merge`): duplicates combined in list order, Select2nd keeping the first list's value."""
+    z = load_fixture("merge")
+    m, n = (int(x) for x in z[f"{which}_shape"])
+    lists = [upload(gpu_ctx, Csc(m, n, z[f"{which}_L{l}_cp"], z[f"{which}_L{l}_ir"], z[f"{which}_L{l}_val"]))
+             for l in range(int(z[f"{which}_k"]))]
+    s, dt = sr.rsplit("_", 1)
+    M = cb.MultiwayMerge(SRCLS[s](dt), lists)
+    cp, ir, val = M.to_host()
+    assert np.array_equal(cp, z[f"{which}_{sr}_hash_cp"]) and np.array_equal(ir, z[f"{which}_{sr}_hash_ir"])
+    assert np.array_equal(val, z[f"{which}_{sr}_hash_val"])
