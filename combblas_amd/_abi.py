@@ -66,7 +66,7 @@ ALLGATHER_FN = ctypes.CFUNCTYPE(ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32,
 
 class Transport(ctypes.Structure):
     _fields_ = [("user", ctypes.c_void_p), ("bcast", BCAST_FN), ("alltoallv", ALLTOALLV_FN),
-                ("allgather", ALLGATHER_FN)]
+                ("allgather", ALLGATHER_FN), ("host_buffers", ctypes.c_int32)]
 
 
 GROUP_ROW, GROUP_COL, GROUP_FIBER, GROUP_WORLD = range(4)

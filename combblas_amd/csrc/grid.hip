@@ -130,8 +130,18 @@ cbg_status t_bcast(cbg_grid* G, int g, int n, void* const* bufs, const int64_t* 
   }
   HIPCHK(hipStreamSynchronize(G->ctx->stream));
   HIPCHK(hipStreamSynchronize(G->cs));
-  for (int i = 0; i < n; ++i)
-    if (bytes[i] > 0 && G->cb.bcast(G->cb.user, g, bufs[i], bytes[i], root) != 0) return CBG_ECOMM;
+  const bool me_root = G->grank(g) == root;
+  for (int i = 0; i < n; ++i) {
+    if (bytes[i] <= 0) continue;
+    if (!G->cb.host_buffers) {
+      if (G->cb.bcast(G->cb.user, g, bufs[i], bytes[i], root) != 0) return CBG_ECOMM;
+      continue;
+    }
+    std::vector<char> h((size_t)bytes[i]);
+    if (me_root) HIPCHK(hipMemcpy(h.data(), bufs[i], bytes[i], hipMemcpyDeviceToHost));
+    if (G->cb.bcast(G->cb.user, g, h.data(), bytes[i], root) != 0) return CBG_ECOMM;
+    if (!me_root) HIPCHK(hipMemcpy(bufs[i], h.data(), bytes[i], hipMemcpyHostToDevice));
+  }
   return CBG_OK;
 }
 
@@ -161,7 +171,12 @@ cbg_status t_alltoallv(cbg_grid* G, int g, const void* send, const int64_t* sbyt
     return CBG_OK;
   }
   HIPCHK(hipStreamSynchronize(st));
-  return G->cb.alltoallv(G->cb.user, g, send, sbytes, recv, rbytes) == 0 ? CBG_OK : CBG_ECOMM;
+  if (!G->cb.host_buffers) return G->cb.alltoallv(G->cb.user, g, send, sbytes, recv, rbytes) == 0 ? CBG_OK : CBG_ECOMM;
+  std::vector<char> hs((size_t)so[P] + 1), hr((size_t)ro[P] + 1);
+  if (so[P]) HIPCHK(hipMemcpy(hs.data(), send, so[P], hipMemcpyDeviceToHost));
+  if (G->cb.alltoallv(G->cb.user, g, hs.data(), sbytes, hr.data(), rbytes) != 0) return CBG_ECOMM;
+  if (ro[P]) HIPCHK(hipMemcpy(recv, hr.data(), ro[P], hipMemcpyHostToDevice));
+  return CBG_OK;
 }
 
 // all-gather of `bytes` host bytes per member (GetSetSizes); synchronous
@@ -357,8 +372,9 @@ cbg_status summa_layer_impl(cbg_grid* G, const cbg_dcsc_view* Av, const cbg_dcsc
   // GetSetSizes: every member's piece sizes (per round) in the row group (A) and column group (B)
   std::vector<Sizes> myA(R), myB(R), allA((size_t)R * q), allB((size_t)R * q);
   for (int r = 0; r < R; ++r) {
-    myA[r] = Sizes{Ah[r].nrow, Ah[r].ncol, Ah[r].nnz, aval ? 1 : 0};
-    myB[r] = Sizes{Bh[r].nrow, Bh[r].ncol, Bh[r].nnz, bval ? 1 : 0};
+    // has_val: 1 values, 0 pattern, -1 empty (an empty piece's value pointer says nothing)
+    myA[r] = Sizes{Ah[r].nrow, Ah[r].ncol, Ah[r].nnz, Ah[r].nnz ? (aval ? 1 : 0) : -1};
+    myB[r] = Sizes{Bh[r].nrow, Bh[r].ncol, Bh[r].nnz, Bh[r].nnz ? (bval ? 1 : 0) : -1};
   }
   CBGCHK(t_allgather(G, CBG_GROUP_ROW, myA.data(), allA.data(), (int64_t)sizeof(Sizes) * R));
   CBGCHK(t_allgather(G, CBG_GROUP_COL, myB.data(), allB.data(), (int64_t)sizeof(Sizes) * R));
@@ -366,10 +382,13 @@ cbg_status summa_layer_impl(cbg_grid* G, const cbg_dcsc_view* Av, const cbg_dcsc
   auto SB = [&](int r, int k) -> const Sizes& { return allB[(size_t)k * R + r]; };
   // CheckSpGEMMCompliance (ParFriends.h:160-181) for every stage, agreed over the world
   bool ok = true;
+  int64_t ha = -1, hb = -1;   // value/pattern status of the non-empty pieces: must agree
   for (int r = 0; r < R; ++r)
     for (int k = 0; k < q; ++k) {
       ok = ok && SA(r, k).ncol == SB(r, k).nrow && SA(r, k).nrow == SA(0, 0).nrow && SB(r, k).ncol == SB(0, 0).ncol;
-      ok = ok && SA(r, k).has_val == SA(0, 0).has_val && SB(r, k).has_val == SB(0, 0).has_val;
+      const int64_t a = SA(r, k).has_val, b = SB(r, k).has_val;
+      if (a >= 0) { ok = ok && (ha < 0 || ha == a); ha = a; }
+      if (b >= 0) { ok = ok && (hb < 0 || hb == b); hb = b; }
     }
   bool all = true;
   CBGCHK(all_ok(G, ok, &all));
@@ -399,7 +418,7 @@ cbg_status summa_layer_impl(cbg_grid* G, const cbg_dcsc_view* Av, const cbg_dcsc
       a.nrow = s.nrow; a.ncol = s.ncol; a.nnz = s.nnz;
       a.cp = (const int64_t*)base;
       a.ir = (const int32_t*)(base + 8 * (s.ncol + 1));
-      a.val = s.has_val ? (const void*)(base + 8 * (s.ncol + 1) + ((4 * s.nnz + 15) & ~15LL)) : nullptr;
+      a.val = s.has_val > 0 ? (const void*)(base + 8 * (s.ncol + 1) + ((4 * s.nnz + 15) & ~15LL)) : nullptr;
     }
     if (k == G->row) {
       b = Bh[r];
@@ -409,7 +428,7 @@ cbg_status summa_layer_impl(cbg_grid* G, const cbg_dcsc_view* Av, const cbg_dcsc
       b.nrow = s.nrow; b.ncol = s.ncol; b.nnz = s.nnz;
       b.cp = (const int64_t*)base;
       b.ir = (const int32_t*)(base + 8 * (s.ncol + 1));
-      b.val = s.has_val ? (const void*)(base + 8 * (s.ncol + 1) + ((4 * s.nnz + 15) & ~15LL)) : nullptr;
+      b.val = s.has_val > 0 ? (const void*)(base + 8 * (s.ncol + 1) + ((4 * s.nnz + 15) & ~15LL)) : nullptr;
     }
     if (q > 1) {
       hipEvent_t e0, e1;

@@ -708,6 +708,7 @@ def MemEfficientSpGEMM(SR, A, B, phases, hardThreshold, selectNum, recoverNum, r
 
 # -------------------------------------------------------------------------------------- backends
 _TYPESTR = {torch.float64: "<f8", torch.float32: "<f4", torch.int64: "<i8", torch.int32: "<i4", torch.uint8: "|u1"}
+_FROM_ABI = {v: k for k, v in _ABI_DT.items()}
 
 
 class _ResultOwner:
@@ -771,12 +772,14 @@ class _NativeGrid:
                             _abi.GROUP_COL: [grid.rank_of(l, r, j) for r in range(q)],
                             _abi.GROUP_FIBER: [grid.rank_of(m, i, j) for m in range(L)],
                             _abi.GROUP_WORLD: list(range(grid.world))}
+            # nccl process groups move device tensors directly; gloo moves host tensors
+            self.direct = dist.get_backend() == "nccl"
             self._cbs = (_abi.BCAST_FN(self._bcast), _abi.ALLTOALLV_FN(self._alltoallv),
                          _abi.ALLGATHER_FN(self._allgather))
-            self.transport = _abi.Transport(None, *self._cbs)
+            self.transport = _abi.Transport(None, *self._cbs, 0)
             _abi.check(self.lib.cbg_grid_create(backend.ctx._ptr, ctypes.byref(self.transport), grid.world, grid.rank,
                                                 L, q, q, ctypes.byref(self.ptr)), "cbg_grid_create")
-            self.kind = "host-staged " + dist.get_backend()
+            self.kind = ("torch-nccl" if self.direct else "host-staged ") + ("" if self.direct else dist.get_backend())
 
     # -- transport callbacks (gloo): return 0 on success, never raise into C
     def _bcast(self, user, g, buf, nbytes, root):
@@ -784,10 +787,13 @@ class _NativeGrid:
             dev = self.backend.device
             t = _dev_u8(buf, nbytes, dev)
             src = self.members[g][root]
-            h = t.cpu() if src == self.grid.rank else torch.empty(nbytes, dtype=torch.uint8)
-            dist.broadcast(h, src=src, group=self.groups[g])
-            if src != self.grid.rank:
-                t.copy_(h)
+            if self.direct:
+                dist.broadcast(t, src=src, group=self.groups[g])
+            else:
+                h = t.cpu() if src == self.grid.rank else torch.empty(nbytes, dtype=torch.uint8)
+                dist.broadcast(h, src=src, group=self.groups[g])
+                if src != self.grid.rank:
+                    t.copy_(h)
             torch.cuda.current_stream(dev).synchronize()
             return 0
         except Exception as e:  # pragma: no cover - reported through CBG_ECOMM
@@ -800,8 +806,10 @@ class _NativeGrid:
             P = len(self.members[g])
             sb = [int(sbytes[m]) for m in range(P)]
             rb = [int(rbytes[m]) for m in range(P)]
-            s = _dev_u8(send, sum(sb), dev).cpu() if sum(sb) else torch.empty(0, dtype=torch.uint8)
-            r = torch.empty(sum(rb), dtype=torch.uint8)
+            where = dev if self.direct else torch.device("cpu")
+            s = _dev_u8(send, sum(sb), dev) if sum(sb) else torch.empty(0, dtype=torch.uint8, device=dev)
+            s = s.to(where)
+            r = torch.empty(sum(rb), dtype=torch.uint8, device=where)
             dist.all_to_all_single(r, s, output_split_sizes=rb, input_split_sizes=sb, group=self.groups[g])
             if sum(rb):
                 _dev_u8(recv, sum(rb), dev).copy_(r)
@@ -814,10 +822,11 @@ class _NativeGrid:
     def _allgather(self, user, g, send, recv, nbytes):
         try:
             P = len(self.members[g])
-            mine = torch.frombuffer(bytearray(ctypes.string_at(send, nbytes)), dtype=torch.uint8)
-            out = [torch.empty(nbytes, dtype=torch.uint8) for _ in range(P)]
+            where = self.backend.device if self.direct else torch.device("cpu")
+            mine = torch.frombuffer(bytearray(ctypes.string_at(send, nbytes)), dtype=torch.uint8).to(where)
+            out = [torch.empty(nbytes, dtype=torch.uint8, device=where) for _ in range(P)]
             dist.all_gather(out, mine, group=self.groups[g])
-            allb = torch.cat(out).numpy().tobytes()
+            allb = torch.cat(out).cpu().numpy().tobytes()
             ctypes.memmove(recv, allb, nbytes * P)
             return 0
         except Exception as e:  # pragma: no cover
@@ -879,9 +888,10 @@ class GpuBackend:
         try:
             owner = _ResultOwner(self.ctx, res)
             n, nc = int(res.nnz), int(res.ncol)
+            vdt = _FROM_ABI.get(int(res.val_type), self.val_dtype)   # the result's own value type
             cp = torch.as_tensor(_DevArr(res.colptr, nc + 1, "<i8", owner), device=self.device)
             ir = torch.as_tensor(_DevArr(res.row, n, "<i4", owner), device=self.device)
-            val = torch.as_tensor(_DevArr(res.val, n, _TYPESTR[self.val_dtype], owner), device=self.device)
+            val = torch.as_tensor(_DevArr(res.val, n, _TYPESTR[vdt], owner), device=self.device)
             if cp.data_ptr() == res.colptr and (n == 0 or ir.data_ptr() == res.row):
                 return Block(int(res.nrow), nc, cp, ir, val)
         except (TypeError, RuntimeError, ValueError):
@@ -897,7 +907,7 @@ class GpuBackend:
             n, nc = int(res.nnz), int(res.ncol)
             cp = torch.empty(nc + 1, dtype=torch.int64, device=self.device)
             ir = torch.empty(n, dtype=torch.int32, device=self.device)
-            val = torch.empty(n, dtype=self.val_dtype, device=self.device)
+            val = torch.empty(n, dtype=_FROM_ABI.get(int(res.val_type), self.val_dtype), device=self.device)
             _abi.check(lib.cbg_result_to_host(self.ctx._ptr, ctypes.byref(res), cp.data_ptr(),
                                               ir.data_ptr() if n else None, val.data_ptr() if n else None),
                        "cbg_result_to_host")

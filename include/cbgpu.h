@@ -18,6 +18,12 @@
  *                      (Kselect1 SpParMat.cpp:1413-1700, PruneColumn SpParMat.cpp:2567-2720)
  *   cbg_col_range      SpDCCols::ColSplit (one piece)                    include/CombBLAS/SpDCCols.cpp:927-1086
  *   cbg_col_concat     SpDCCols::ColConcatenate                          include/CombBLAS/SpDCCols.cpp:1087-1185
+ *   cbg_col_select     SubsRef_SR column form on one block               include/CombBLAS/SpParMat.cpp:2251-2422
+ *   cbg_spgemm_grid    Mult_AnXBn_Synch / PSpGEMM / DoubleBuff / Overlap include/CombBLAS/ParFriends.h:798-1235
+ *                      Mult_AnXBn_SUMMA3D                                include/CombBLAS/ParFriends.h:2918-3208
+ *   cbg_summa_layer    SUMMALayer                                        3DSpGEMM/SUMMALayer.h:24-97
+ *   cbg_reduce_all     ReduceAll_threaded                                3DSpGEMM/Reductions.h:134-155
+ *   cbg_grid_create*   CommGrid / CommGrid3D / CCGrid                    src/CommGrid.cpp:37-76, CommGrid3D.h:21-80
  *
  * Semantics (SURVEY §8a parity rules):
  *   - Output columns are row-sorted and duplicate-free when CBG_SORTED_COLS is set (the reference
@@ -129,7 +135,9 @@ cbg_status cbg_estimate(cbg_ctx* ctx, const cbg_dcsc_view* A, const cbg_dcsc_vie
                         int64_t* multiplies, int64_t* nnz_c);
 
 /* Merge nparts column-sorted partial products of identical shape; duplicates combined with
- * SR::add in part order (MultiwayMerge.h:184-231 / 320-405). */
+ * SR::add in part order, MultiwayMergeHash's order (SerialMergeHash, MultiwayMerge.h:320-405:
+ * for Select2nd the first part holding an entry wins; the heap MultiwayMerge differs only there,
+ * tests/golden/merge.npz pins both). */
 cbg_status cbg_merge(cbg_ctx* ctx, const cbg_csc_result* parts, int32_t nparts, cbg_semiring sr,
                      cbg_dtype val_type, uint32_t flags, cbg_csc_result* C);
 
@@ -229,15 +237,17 @@ cbg_status cbg_col_concat(cbg_ctx* ctx, const cbg_csc_result* parts, int32_t npa
 typedef enum { CBG_GROUP_ROW = 0, CBG_GROUP_COL = 1, CBG_GROUP_FIBER = 2, CBG_GROUP_WORLD = 3 } cbg_group;
 
 /* Caller-provided transport (e.g. MPI on the reference side, gloo in tests).  bcast / alltoallv get
- * DEVICE buffers of the grid's device (the library has synchronised its streams before the call);
- * allgather gets HOST buffers.  root / segment order = member index in the group.  Return 0 on
- * success; anything else makes the library return CBG_ECOMM. */
+ * DEVICE buffers of the grid's device (the library has synchronised its streams before the call),
+ * or HOST buffers when host_buffers is set (the library stages through host memory: a plain MPI
+ * transport); allgather always gets HOST buffers.  root / segment order = member index in the
+ * group.  Return 0 on success; anything else makes the library return CBG_ECOMM. */
 typedef struct {
   void* user;
   int32_t (*bcast)(void* user, int32_t group, void* buf, int64_t bytes, int32_t root);
   int32_t (*alltoallv)(void* user, int32_t group, const void* send, const int64_t* send_bytes, void* recv,
                        const int64_t* recv_bytes);
   int32_t (*allgather)(void* user, int32_t group, const void* send, void* recv, int64_t bytes);
+  int32_t host_buffers;
 } cbg_transport;
 
 typedef struct cbg_grid cbg_grid;

@@ -8,6 +8,15 @@
  *   combblas::gpu::MultiwayMerge<SR>(lists, mdim, ndim, delarrs)          MultiwayMerge.h:411-412
  *   combblas::gpu::EstimateLocalFLOP<SR>(A, B)                             mtSpGEMM.h:667-694
  *   combblas::gpu::MCLPruneRecoverySelect(A, thr, select, recover, pct, v) ParFriends.h:185-353
+ *   combblas::gpu::Mult_AnXBn_Synch<SR, NUO, UDERO>(A, B, clearA, clearB) ParFriends.h:1004-1108
+ *   combblas::gpu::Mult_AnXBn_DoubleBuff / Mult_AnXBn_Overlap           ParFriends.h:798-997, 1110-1235
+ *   combblas::gpu::PSpGEMM<SR>(A, B)                                      SpParMat.h:451-464
+ *   combblas::gpu::Mult_AnXBn_SUMMA3D<SR, NUO, UDERO>(A3D, B3D)          ParFriends.h:2918-3208
+ *
+ * The distributed ones run the whole SUMMA (stage broadcasts, local products, merges, fiber
+ * exchange) inside libcbgpu on the device (cbg_spgemm_grid) over the SpParMat's own MPI
+ * communicators (a host-staged cbg_transport built on MPI_Bcast / MPI_Alltoallv / MPI_Allgather);
+ * the local block goes down once and the product comes back once (no SpTuples per stage).
  *
  * MemEfficientSpGEMM (ParFriends.h:449-730) gets the device path by calling the first and the last
  * of these in place of the reference's LocalSpGEMMHash / MCLPruneRecoverySelect.
@@ -25,7 +34,9 @@
 #ifndef COMBBLAS_GPU_H
 #define COMBBLAS_GPU_H
 
+#include <algorithm>
 #include <cstdint>
+#include <memory>
 #include <stdexcept>
 #include <string>
 #include <tuple>
@@ -245,6 +256,153 @@ void MCLPruneRecoverySelect(SpParMat<IT, NT, DER>& A, NT hardThreshold, IT selec
     L = DER(*pt, false);
     delete pt;
     (void)kselectVersion;   // Kselect1 / Kselect2 pick the same k-th value
+  }
+}
+
+// --------------------------------------------------------------------- distributed drivers
+// MPI transport for cbg_grid: host buffers (host_buffers = 1), the grid's four communicators.
+struct MpiTransport {
+  MPI_Comm comm[4];   // CBG_GROUP_ROW, COL, FIBER, WORLD
+  static constexpr int64_t kChunk = 1 << 30;
+  static int32_t bcast(void* u, int32_t g, void* buf, int64_t bytes, int32_t root) {
+    MPI_Comm c = ((MpiTransport*)u)->comm[g];
+    for (int64_t o = 0; o < bytes; o += kChunk) {
+      const int n = (int)std::min<int64_t>(kChunk, bytes - o);
+      if (MPI_Bcast((char*)buf + o, n, MPI_BYTE, root, c) != MPI_SUCCESS) return 1;
+    }
+    return 0;
+  }
+  static int32_t alltoallv(void* u, int32_t g, const void* send, const int64_t* sb, void* recv, const int64_t* rb) {
+    MPI_Comm c = ((MpiTransport*)u)->comm[g];
+    int P = 0;
+    MPI_Comm_size(c, &P);
+    std::vector<int> sc(P), rc(P), sd(P), rd(P);
+    int64_t so = 0, ro = 0;
+    for (int m = 0; m < P; ++m) {
+      if (sb[m] > INT32_MAX || rb[m] > INT32_MAX || so > INT32_MAX || ro > INT32_MAX) return 2;   // MPI int counts
+      sc[m] = (int)sb[m]; rc[m] = (int)rb[m]; sd[m] = (int)so; rd[m] = (int)ro;
+      so += sb[m]; ro += rb[m];
+    }
+    return MPI_Alltoallv(send, sc.data(), sd.data(), MPI_BYTE, recv, rc.data(), rd.data(), MPI_BYTE, c) == MPI_SUCCESS ? 0 : 1;
+  }
+  static int32_t allgather(void* u, int32_t g, const void* send, void* recv, int64_t bytes) {
+    MPI_Comm c = ((MpiTransport*)u)->comm[g];
+    return MPI_Allgather(send, (int)bytes, MPI_BYTE, recv, (int)bytes, MPI_BYTE, c) == MPI_SUCCESS ? 0 : 1;
+  }
+};
+
+struct GridHandle {
+  MpiTransport mt;
+  cbg_grid* grid = nullptr;
+  ~GridHandle() { if (grid) cbg_grid_destroy(grid); }
+};
+
+inline cbg_grid* make_grid(GridHandle& h, MPI_Comm world, MPI_Comm row, MPI_Comm col, MPI_Comm fiber, int layers,
+                           int rows, int cols) {
+  h.mt.comm[CBG_GROUP_ROW] = row; h.mt.comm[CBG_GROUP_COL] = col;
+  h.mt.comm[CBG_GROUP_FIBER] = fiber; h.mt.comm[CBG_GROUP_WORLD] = world;
+  cbg_transport t{};
+  t.user = &h.mt; t.bcast = &MpiTransport::bcast; t.alltoallv = &MpiTransport::alltoallv;
+  t.allgather = &MpiTransport::allgather; t.host_buffers = 1;
+  int wsize = 0, wrank = 0;
+  MPI_Comm_size(world, &wsize);
+  MPI_Comm_rank(world, &wrank);
+  check(cbg_grid_create(context(), &t, wsize, wrank, layers, rows, cols, &h.grid), "cbg_grid_create");
+  return h.grid;
+}
+
+// the rank's product piece (device CSC) -> UDERO via column-sorted SpTuples
+template <class IU, class NUO, class UDERO>
+UDERO* to_local(cbg_csc_result& C) {
+  typedef typename UDERO::LocalIT LIT;
+  SpTuples<LIT, NUO>* t = to_tuples<LIT, NUO>(context(), C);
+  UDERO* D = new UDERO(*t, false);
+  delete t;
+  return D;
+}
+
+template <class SR, class NUO, class UDERO, class IU, class NU1, class NU2, class UDERA, class UDERB>
+SpParMat<IU, NUO, UDERO> summa2d(SpParMat<IU, NU1, UDERA>& A, SpParMat<IU, NU2, UDERB>& B, bool clearA, bool clearB,
+                                 uint32_t flags) {
+  std::shared_ptr<CommGrid> GA = A.getcommgrid(), GB = B.getcommgrid();
+  if (A.getncol() != B.getnrow() || !(*GA == *GB)) throw std::runtime_error("Mult_AnXBn: DIMMISMATCH (3002)");
+  GridHandle h;
+  make_grid(h, GA->GetWorld(), GA->GetRowWorld(), GA->GetColWorld(), MPI_COMM_SELF, 1, GA->GetGridRows(),
+            GA->GetGridCols());
+  cbg_dcsc_view va = view_of(*A.seqptr()), vb = view_of(*B.seqptr());
+  cbg_csc_result C{};
+  cbg_grid_stats st{};
+  check(cbg_spgemm_grid(h.grid, &va, &vb, DeviceSemiring<SR>::code, DeviceType<NUO>::code,
+                        CBG_SORTED_COLS | flags, &C, &st), "cbg_spgemm_grid");
+  UDERO* D = to_local<IU, NUO, UDERO>(C);
+  if (clearA) A.FreeMemory();
+  if (clearB) B.FreeMemory();
+  return SpParMat<IU, NUO, UDERO>(D, GA);
+}
+
+template <class SR, class NUO, class UDERO, class IU, class NU1, class NU2, class UDERA, class UDERB>
+SpParMat<IU, NUO, UDERO> Mult_AnXBn_Synch(SpParMat<IU, NU1, UDERA>& A, SpParMat<IU, NU2, UDERB>& B,
+                                          bool clearA = false, bool clearB = false) {
+  constexpr bool dev = DeviceSemiring<SR>::ok && DeviceType<NUO>::ok &&
+                       (std::is_same<NU1, NUO>::value || std::is_same<NU1, bool>::value) &&
+                       (std::is_same<NU2, NUO>::value || std::is_same<NU2, bool>::value);
+  if constexpr (!dev) return combblas::Mult_AnXBn_Synch<SR, NUO, UDERO>(A, B, clearA, clearB);
+  else return summa2d<SR, NUO, UDERO>(A, B, clearA, clearB, 0u);
+}
+
+template <class SR, class NUO, class UDERO, class IU, class NU1, class NU2, class UDERA, class UDERB>
+SpParMat<IU, NUO, UDERO> Mult_AnXBn_DoubleBuff(SpParMat<IU, NU1, UDERA>& A, SpParMat<IU, NU2, UDERB>& B,
+                                               bool clearA = false, bool clearB = false) {
+  constexpr bool dev = DeviceSemiring<SR>::ok && DeviceType<NUO>::ok &&
+                       (std::is_same<NU1, NUO>::value || std::is_same<NU1, bool>::value) &&
+                       (std::is_same<NU2, NUO>::value || std::is_same<NU2, bool>::value);
+  if constexpr (!dev) return combblas::Mult_AnXBn_DoubleBuff<SR, NUO, UDERO>(A, B, clearA, clearB);
+  else return summa2d<SR, NUO, UDERO>(A, B, clearA, clearB, CBG_HALVES);
+}
+
+template <class SR, class NUO, class UDERO, class IU, class NU1, class NU2, class UDERA, class UDERB>
+SpParMat<IU, NUO, UDERO> Mult_AnXBn_Overlap(SpParMat<IU, NU1, UDERA>& A, SpParMat<IU, NU2, UDERB>& B,
+                                            bool clearA = false, bool clearB = false) {
+  constexpr bool dev = DeviceSemiring<SR>::ok && DeviceType<NUO>::ok &&
+                       (std::is_same<NU1, NUO>::value || std::is_same<NU1, bool>::value) &&
+                       (std::is_same<NU2, NUO>::value || std::is_same<NU2, bool>::value);
+  if constexpr (!dev) return combblas::Mult_AnXBn_Overlap<SR, NUO, UDERO>(A, B, clearA, clearB);
+  else return summa2d<SR, NUO, UDERO>(A, B, clearA, clearB, CBG_RUNNING_MERGE);
+}
+
+// PSpGEMM (SpParMat.h:451-464): the default distributed product, Mult_AnXBn_Synch
+template <typename SR, typename IU, typename NU1, typename NU2, typename UDERA, typename UDERB>
+SpParMat<IU, typename promote_trait<NU1, NU2>::T_promote,
+         typename promote_trait<UDERA, UDERB>::T_promote>
+PSpGEMM(SpParMat<IU, NU1, UDERA>& A, SpParMat<IU, NU2, UDERB>& B, bool clearA = false, bool clearB = false) {
+  typedef typename promote_trait<NU1, NU2>::T_promote N_promote;
+  typedef typename promote_trait<UDERA, UDERB>::T_promote DER_promote;
+  return gpu::Mult_AnXBn_Synch<SR, N_promote, DER_promote>(A, B, clearA, clearB);
+}
+
+// Mult_AnXBn_SUMMA3D on the reference's (non-special) SpParMat3D layout: A colsplit, B rowsplit
+template <class SR, class NUO, class UDERO, class IU, class NU1, class NU2, class UDER1, class UDER2>
+SpParMat3D<IU, NUO, UDERO> Mult_AnXBn_SUMMA3D(SpParMat3D<IU, NU1, UDER1>& A, SpParMat3D<IU, NU2, UDER2>& B) {
+  constexpr bool dev = DeviceSemiring<SR>::ok && DeviceType<NUO>::ok &&
+                       (std::is_same<NU1, NUO>::value || std::is_same<NU1, bool>::value) &&
+                       (std::is_same<NU2, NUO>::value || std::is_same<NU2, bool>::value);
+  if constexpr (!dev) {
+    return combblas::Mult_AnXBn_SUMMA3D<SR, NUO, UDERO>(A, B);
+  } else {
+    std::shared_ptr<CommGrid3D> G = A.getcommgrid3D();
+    if (A.getncol() != B.getnrow() || !A.isColSplit() || B.isColSplit() || A.isSpecial() || B.isSpecial())
+      throw std::runtime_error("Mult_AnXBn_SUMMA3D: needs colsplit A, rowsplit B, non-special layout (3002)");
+    std::shared_ptr<CommGrid> layer = G->GetCommGridLayer();
+    GridHandle h;
+    make_grid(h, G->GetWorld(), layer->GetRowWorld(), layer->GetColWorld(), G->GetFiberWorld(), G->GetGridLayers(),
+              G->GetGridRows(), G->GetGridCols());
+    cbg_dcsc_view va = view_of(*A.seqptr()), vb = view_of(*B.seqptr());
+    cbg_csc_result C{};
+    cbg_grid_stats st{};
+    check(cbg_spgemm_grid(h.grid, &va, &vb, DeviceSemiring<SR>::code, DeviceType<NUO>::code, CBG_SORTED_COLS, &C, &st),
+          "cbg_spgemm_grid");
+    UDERO* D = to_local<IU, NUO, UDERO>(C);
+    return SpParMat3D<IU, NUO, UDERO>(D, G, true, false);
   }
 }
 

@@ -312,11 +312,15 @@ def run_fixture_case(rank, world, port, backend_kind, cases, errq):
     try:
         os.environ["MASTER_ADDR"] = "127.0.0.1"
         os.environ["MASTER_PORT"] = str(port)
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        if backend_kind == "gpu-rccl":   # libcbgpu's own RCCL communicators (one rank per GPU)
+            torch.cuda.set_device(0)
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", 0))
+        else:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
         L, q, _ = cbd.grid_for(world)
         grid = cbd.CommGrid3D(L, q, q)
         import combblas_amd as cb
-        be = cbd.GpuBackend(cb.Context(0)) if backend_kind == "gpu" else ScipyBackend()
+        be = cbd.GpuBackend(cb.Context(0)) if backend_kind.startswith("gpu") else ScipyBackend()
         from helpers import abs_product_sums, fixture_inputs, fixture_product, load_fixture
         for (name, tag, golden) in cases:
             z = load_fixture(name)
@@ -341,9 +345,11 @@ def run_fixture_case(rank, world, port, backend_kind, cases, errq):
                     G = sp.csc_matrix((z[golden + "_val"], z[golden + "_ir"], z[golden + "_cp"]),
                                       shape=(A.nrow, B.ncol))
                     check_piece_exact_or_f64(C, G, rank, f"{name}/matlab/{dname}", scale)
-            t = torch.tensor([stats.get("multiplies", 0)], dtype=torch.int64)
+            t = torch.tensor([stats.get("multiplies", 0)], dtype=torch.int64, device=be.comm_device)
             dist.all_reduce(t)
             assert int(t.item()) == int(z[f"C_{tag}_flops"]), (int(t.item()), int(z[f"C_{tag}_flops"]))
+            if backend_kind == "gpu-rccl":
+                assert be.native_grid(grid).kind == "rccl"
         dist.barrier()
         dist.destroy_process_group()
     except Exception as e:

@@ -5,7 +5,10 @@
 // combblas::gpu::LocalSpGEMMHash (libcbgpu) and the reference's combblas::LocalSpGEMMHash (CPU), and
 // compares the column-sorted products entry by entry (the reference output is re-sorted with
 // SortColBased: its integerSort mis-sorts power-of-two rows).  Also MultiwayMerge and a
-// semiring without a device functor (must take the reference CPU path).
+// semiring without a device functor (must take the reference CPU path).  The distributed drivers
+// (gpu::Mult_AnXBn_Synch / DoubleBuff / Overlap / PSpGEMM, libcbgpu's grid over the SpParMat's MPI
+// communicators) are compared block by block with the reference's Mult_AnXBn_Synch on the same
+// SpParMat operands; run it under mpirun -np 1 or 4 (square grids, CommGrid.cpp:44-50).
 //   usage: dropin_test [--expect-no-gpu]
 // Exit 0 = all equal (or, with --expect-no-gpu, the device path threw a device error).
 #include <mpi.h>
@@ -46,6 +49,45 @@ bool same(SpTuples<I, T>* a, SpTuples<I, T>* b, const char* what) {
     }
   printf("%s: %lld entries equal\n", what, (long long)a->getnnz());
   return true;
+}
+
+// the rank's block of a deterministic global random M x N matrix (same stream on every rank)
+template <class T>
+SpDCCols<I, T>* random_block(std::shared_ptr<CommGrid> grid, I M, I N, double density, unsigned seed) {
+  const int q = grid->GetGridRows(), i = grid->GetRankInProcCol(), j = grid->GetRankInProcRow();
+  const I r0 = i * (M / q), r1 = (i == q - 1) ? M : r0 + M / q;
+  const I c0 = j * (N / q), c1 = (j == q - 1) ? N : c0 + N / q;
+  std::mt19937_64 g(seed);
+  std::uniform_real_distribution<double> u(0.0, 1.0);
+  std::vector<std::tuple<I, I, T>> tv;
+  for (I c = 0; c < N; ++c)
+    for (I r = 0; r < M; ++r) {
+      const bool on = u(g) < density;
+      const T v = (T)(1 + (g() % 9));
+      if (on && r >= r0 && r < r1 && c >= c0 && c < c1) tv.emplace_back(r - r0, c - c0, v);
+    }
+  std::tuple<I, I, T>* t = new std::tuple<I, I, T>[tv.size() > 0 ? tv.size() : 1];
+  for (size_t k = 0; k < tv.size(); ++k) t[k] = tv[k];
+  SpTuples<I, T> tup((int64_t)tv.size(), r1 - r0, c1 - c0, t, true);
+  return new SpDCCols<I, T>(tup, false);
+}
+
+// duplicates combined by + (the reference's multi-rank Synch leaves duplicates: SURVEY §0.5)
+template <class T>
+SpTuples<I, T>* dedup_sum(SpTuples<I, T>* a) {
+  a->SortColBased();
+  std::vector<std::tuple<I, I, T>> v;
+  for (I k = 0; k < a->getnnz(); ++k) {
+    if (!v.empty() && std::get<0>(v.back()) == a->rowindex(k) && std::get<1>(v.back()) == a->colindex(k))
+      std::get<2>(v.back()) += a->numvalue(k);
+    else
+      v.emplace_back(a->rowindex(k), a->colindex(k), a->numvalue(k));
+  }
+  std::tuple<I, I, T>* t = new std::tuple<I, I, T>[v.size() > 0 ? v.size() : 1];
+  for (size_t k = 0; k < v.size(); ++k) t[k] = v[k];
+  SpTuples<I, T>* r = new SpTuples<I, T>((int64_t)v.size(), a->getnrow(), a->getncol(), t, true);
+  delete a;
+  return r;
 }
 
 template <class T1, class T2>
@@ -140,6 +182,33 @@ int main(int argc, char** argv) {
         delete a; delete b;
       }
       delete sq; delete P;
+    }
+    // distributed drivers on the SpParMat's grid, block by block against the reference's Synch
+    {
+      typedef SpDCCols<I, int64_t> DI;
+      typedef SpParMat<I, int64_t, DI> PMI;
+      typedef PlusTimesSRing<int64_t, int64_t> PTI;
+      std::shared_ptr<CommGrid> grid(new CommGrid(MPI_COMM_WORLD, 0, 0));
+      PMI A(random_block<int64_t>(grid, 420, 380, 0.05, 11), grid);
+      PMI B(random_block<int64_t>(grid, 380, 350, 0.05, 12), grid);
+      PMI R = combblas::Mult_AnXBn_Synch<PTI, int64_t, DI>(A, B);
+      SpTuples<I, int64_t>* rt = dedup_sum(new SpTuples<I, int64_t>(R.seq()));
+      const char* names[4] = {"gpu::Mult_AnXBn_Synch", "gpu::Mult_AnXBn_DoubleBuff", "gpu::Mult_AnXBn_Overlap",
+                              "gpu::PSpGEMM"};
+      for (int d = 0; d < 4; ++d) {
+        PMI D = d == 0 ? gpu::Mult_AnXBn_Synch<PTI, int64_t, DI>(A, B)
+              : d == 1 ? gpu::Mult_AnXBn_DoubleBuff<PTI, int64_t, DI>(A, B)
+              : d == 2 ? gpu::Mult_AnXBn_Overlap<PTI, int64_t, DI>(A, B)
+                       : gpu::PSpGEMM<PTI>(A, B);
+        SpTuples<I, int64_t>* dt = new SpTuples<I, int64_t>(D.seq());
+        SpTuples<I, int64_t>* rc2 = new SpTuples<I, int64_t>(*rt);
+        if (!same(dt, rc2, names[d])) rc = 1;
+        delete dt; delete rc2;
+      }
+      delete rt;
+      int bad = rc, any = 0;
+      MPI_Allreduce(&bad, &any, 1, MPI_INT, MPI_MAX, MPI_COMM_WORLD);
+      rc = any;
     }
   }
   MPI_Finalize();

@@ -48,3 +48,11 @@ def test_reference_fixtures_through_layouts_gloo_gpu(world, port):
     checked; Select2nd included (merges follow the inner dimension's order on every layout)."""
     from dist_support import run_fixture_case
     spawn_case(world, "gpu", FIXTURE_CASES, port, body=run_fixture_case)
+
+
+def test_rccl_native_grid_single_rank():
+    """libcbgpu's RCCL path (cbg_rccl_unique_id, ncclCommInitRank, ncclCommSplit of row/col/fiber
+    communicators) on a one-rank nccl process group: the only RCCL shape one GPU can host (RCCL refuses
+    two ranks on one device); the reference fixtures must come out unchanged."""
+    from dist_support import run_fixture_case
+    spawn_case(1, "gpu-rccl", FIXTURE_CASES[:3], 29634, body=run_fixture_case)

@@ -3,7 +3,8 @@
 tests/dropin/dropin_test.cpp is compiled against the reference headers (build container only, by
 __graft_entry__.build() or here) and links libcbgpu.so; on a GPU it compares gpu::LocalSpGEMMHash,
 gpu::MultiwayMerge and gpu::EstimateLocalFLOP with the reference's LocalSpGEMMHash / MultiwayMerge /
-EstimateLocalFLOP in one process, plus a semiring without a device functor (reference CPU template)."""
+EstimateLocalFLOP in one process, plus a semiring without a device functor (reference CPU template),
+and the distributed drivers (gpu::Mult_AnXBn_Synch etc.) against the reference's Mult_AnXBn_Synch."""
 import os
 import subprocess
 
@@ -34,3 +35,15 @@ def test_dropin_matches_reference_on_gpu():
         pytest.skip("dropin_test not built (needs the reference headers in the build container)")
     r = subprocess.run([BIN], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and "DROPIN OK" in r.stdout, r.stdout + r.stderr
+
+
+@pytest.mark.gpu
+def test_dropin_distributed_drivers_4_ranks_on_gpu():
+    """gpu::Mult_AnXBn_Synch / DoubleBuff / Overlap / PSpGEMM at 4 MPI ranks (2x2 CommGrid, ranks sharing
+    cuda:0, libcbgpu's grid over the SpParMat's MPI communicators) against the reference's own
+    Mult_AnXBn_Synch on the same operands, block by block (the reference's duplicates summed)."""
+    mpirun = "/opt/conda/bin/mpirun"
+    if not os.path.exists(BIN) or not os.path.exists(mpirun):
+        pytest.skip("dropin_test or MPICH's mpirun not available")
+    r = subprocess.run([mpirun, "-np", "4", BIN], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and r.stdout.count("DROPIN OK") == 4, r.stdout + r.stderr
