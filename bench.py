@@ -182,6 +182,7 @@ def bench_local(args):
         "phases_ms": {k: round(float(np.mean([p[k] for p in profs])), 3)
                       for k in ("flops_ms", "bin_ms", "symbolic_ms", "scan_ms", "numeric_ms", "heavy_ms",
                                 "total_ms")},
+        "heavy_items": {"total": int(profs[-1]["bins"][13]), "rows_known": int(profs[-1]["known_items"])},
         "roofline": {"bound": "hbm", "kernel": "k_num_heavy", "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "traffic_source": tsrc, "algorithmic_bytes_per_launch": hb, "avg_launch_ms": heavy_ms,
@@ -224,15 +225,29 @@ def bench_dist(args, world, rank, local_rank):
     del cp, ir, val
     SR = cb.PlusTimesSRing("f64")
 
+    phases = {}
+
     def step():
         st = {}
         C = cbd.Mult_AnXBn_SUMMA3D(SR, A, B, st)
         nz = C.block.nnz
         del C
+        for k in ("bcast_ms", "local_ms", "merge_ms", "fiber_ms", "total_ms", "bcast_bytes", "fiber_bytes"):
+            phases[k] = phases.get(k, 0) + st.get(k, 0)
         return st.get("multiplies", 0), nz
 
-    for _ in range(max(args.warmup, 1)):
+    try:
+        step()   # first product also sets up libcbgpu's grid (RCCL communicators)
+    except Exception as e:   # RCCL grid unavailable: the same schedule over torch's own process groups
+        if os.environ.get("CBG_GRID_TRANSPORT", "rccl") != "rccl":
+            raise
+        print(f"bench: native RCCL grid failed ({e!r}); retrying over torch.distributed", file=sys.stderr)
+        os.environ["CBG_GRID_TRANSPORT"] = "torch"
+        be._grids = {}
         step()
+    for _ in range(max(args.warmup - 1, 0)):
+        step()
+    phases.clear()
     torch.cuda.synchronize()
     dist.barrier()
     torch.cuda.synchronize()
@@ -252,16 +267,18 @@ def bench_dist(args, world, rank, local_rank):
     dist.all_reduce(s)
     elapsed, mults, nnzc = float(t.item()), float(s[0].item()), float(s[1].item())
     if rank == 0:
+        ng = be.native_grid(grid)
         cfg = workload(args.scale, args.edgefactor,
                        f"{L}x{q}x{q} ({'3D split SUMMA' if L > 1 else '2D SUMMA'}), "
-                       f"{'RCCL' if backend == 'nccl' else backend}")
+                       f"libcbgpu grid over {ng.kind}")
         cfg.update({"nnz_A": nnzb, "multiplies": int(mults / args.steps), "nnz_C": int(nnzc / args.steps)})
         out = {"metric": METRIC, "value": mults / elapsed, "unit": "multiplies/s", "n_gpus": world,
                "steps": args.steps, "warmup": args.warmup, "ms_per_step": 1000.0 * elapsed / args.steps,
                "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
                "data": "synthetic", "config": cfg,
                "effective_GBps": balg_bytes(mults / args.steps, nnzc / args.steps, nnzb, n)
-               / (elapsed / args.steps) / 1e9}
+               / (elapsed / args.steps) / 1e9,
+               "rank0_phases_per_step": {k: round(v / args.steps, 3) for k, v in phases.items()}}
         print(json.dumps(out), flush=True)
     dist.destroy_process_group()
 

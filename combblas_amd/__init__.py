@@ -111,7 +111,7 @@ class Context:
         _abi.check(self._lib.cbg_last_profile(self._ptr, ctypes.byref(p)), "cbg_last_profile")
         return {"flops_ms": p.flops_ms, "bin_ms": p.bin_ms, "symbolic_ms": p.symbolic_ms, "scan_ms": p.scan_ms,
                 "numeric_ms": p.numeric_ms, "total_ms": p.total_ms, "multiplies": p.multiplies,
-                "nnz_out": p.nnz_out, "bins": list(p.bins), "heavy_ms": p.heavy_ms}
+                "nnz_out": p.nnz_out, "bins": list(p.bins), "heavy_ms": p.heavy_ms, "known_items": p.known_items}
 
     # raw ABI-level product (views in, device result out)
     def spgemm(self, A, B, sr, sort=True):

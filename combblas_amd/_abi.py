@@ -36,7 +36,7 @@ class Profile(ctypes.Structure):
     _fields_ = [("flops_ms", ctypes.c_double), ("bin_ms", ctypes.c_double), ("symbolic_ms", ctypes.c_double),
                 ("scan_ms", ctypes.c_double), ("numeric_ms", ctypes.c_double), ("total_ms", ctypes.c_double),
                 ("multiplies", ctypes.c_int64), ("nnz_out", ctypes.c_int64), ("bins", ctypes.c_int64 * 16),
-                ("heavy_ms", ctypes.c_double)]
+                ("heavy_ms", ctypes.c_double), ("known_items", ctypes.c_int64)]
 
 
 class HostCsc(ctypes.Structure):

@@ -127,6 +127,9 @@ struct cbg_ctx {
   DevBuf flop, span, cnt, list, hist, cursor, scan_tiles, scalars, cur, nxt, ovf_list, stageA[5], stageB[5];
   DevBuf split_idx, long_cols, split_tab, heavy_cols, sub, units, ucnt, uspan, ulist, fb_units, fb_list, uovf_list;
   DevBuf nunits, segsz, segoff, useg, icnt, itemoff, items, parts, wide_win;
+  DevBuf hrows, hmode, hpoff, urows;   // symbolic -> numeric row handoff of heavy columns
+  DevBuf oitems;                       // heavy items the rows-known kernel does not take
+  int row_handoff = -1;                // -1: read CBG_ROW_HANDOFF once (default on)
 };
 
 inline hipError_t launch_cfg_lds(const void* fn, size_t lds) {
@@ -298,6 +301,23 @@ hipError_t launch_num_heavy(hipStream_t st, int64_t nitems, const HeavyItem* ite
   k_num_heavy<SRT, V, LOGT, NT><<<(int)nitems, NT, lds, st>>>(items, hcols, units, nsub, A, B, span, spl, o);
   return hipGetLastError();
 }
+template <int LOGT, int NT, class SRT, typename V>
+hipError_t launch_num_heavy_known(hipStream_t st, int64_t nitems, const HeavyItem* items, const int32_t* hcols,
+                                  const Unit* units, int32_t nsub, const DevCsc<V>& A, const DevCsc<V>& B,
+                                  const int2* span, const Split& spl, const NumOut<V>& o) {
+  if (nitems <= 0) return hipSuccess;
+  const size_t lds = num_heavy_known_lds<SRT, V, LOGT, NT>();
+  if (A.val) {
+    hipError_t e = launch_cfg_lds((const void*)k_num_heavy_known<SRT, V, LOGT, NT, true>, lds);
+    if (e != hipSuccess) return e;
+    k_num_heavy_known<SRT, V, LOGT, NT, true><<<(int)nitems, NT, lds, st>>>(items, hcols, units, nsub, A, B, span, spl, o);
+  } else {
+    hipError_t e = launch_cfg_lds((const void*)k_num_heavy_known<SRT, V, LOGT, NT, false>, lds);
+    if (e != hipSuccess) return e;
+    k_num_heavy_known<SRT, V, LOGT, NT, false><<<(int)nitems, NT, lds, st>>>(items, hcols, units, nsub, A, B, span, spl, o);
+  }
+  return hipGetLastError();
+}
 template <int MODE, class SRT, typename V, int W>
 hipError_t launch_window(hipStream_t st, const int32_t* l, const int* count_dev, int64_t count_host, int64_t grid,
                          const DevCsc<V>& A, const DevCsc<V>& B, const int2* span, const int64_t* colptr,
@@ -416,16 +436,40 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
   HIPCHK(hipMemsetAsync(hist, 0, sizeof(unsigned long long) * 64, st));
   bin_count(st, N, flop, span, sbp, hist, list);
   HIPCHK(hipMemcpyAsync(hh, hist, sizeof(unsigned long long) * 32, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipMemcpyAsync(hh + 32, sc, 32, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(hh + 32, sc, 96, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
   const int NL = ((int*)&hh[34])[1];
   if ((s = bin_fill(st, N, flop, span, sbp, hist, hh, list, &cs)) != CBG_OK) return s;
   const int64_t hcap = (int64_t)cs.hist[31];
   HIPCHK(ctx->heavy_cols.reserve(sizeof(int32_t) * (hcap + 1)));
   HIPCHK(ctx->sub.reserve(sizeof(int32_t) * (hcap * nsub + 1)));
-  HeavyOut ho{heavy_n, ctx->heavy_cols.as<int32_t>(), ctx->sub.as<int32_t>(), nsub, slog};
+  HeavyOut ho{heavy_n, ctx->heavy_cols.as<int32_t>(), ctx->sub.as<int32_t>(), nsub, slog,
+              nullptr, nullptr, 0, nullptr, nullptr};
+  // row handoff: scratch for the heavy columns' sorted rows, sized by the bound sum(min(flop, span))
+  // over flop-heavy columns (k_col_stats); off if that does not fit comfortably in free memory
+  if (ctx->row_handoff < 0) {
+    const char* e = getenv("CBG_ROW_HANDOFF");
+    ctx->row_handoff = (e && e[0] == '0') ? 0 : 1;
+  }
+  const unsigned long long hbound = hh[42];
+  if (ctx->row_handoff && hcap > 0 && hbound > 0 && !SRT::kAddIsError) {
+    size_t fr = 0, tot = 0;
+    HIPCHK(hipMemGetInfo(&fr, &tot));
+    const size_t need = sizeof(int32_t) * (hbound + 1);
+    if (need <= ctx->hrows.n || need < fr / 3) {
+      HIPCHK(ctx->hrows.reserve(need));
+      HIPCHK(ctx->hmode.reserve(sizeof(int32_t) * (hcap + 1)));
+      HIPCHK(ctx->hpoff.reserve(sizeof(int64_t) * (hcap * kMaxParts + 1)));
+      HIPCHK(hipMemsetAsync(ctx->hmode.p, 0, sizeof(int32_t) * (hcap + 1), st));
+      ho.rows = ctx->hrows.as<int32_t>();
+      ho.cursor = sc + 11;
+      ho.cap = hbound;
+      ho.poff = ctx->hpoff.as<int64_t>();
+      ho.mode = ctx->hmode.as<int32_t>();
+    }
+  }
   // split table (unit segments, wide-column parts): needed whenever a column can be heavy
-  Split spl{ctx->split_idx.as<int32_t>(), nullptr, nsub, slog};
+  Split spl{ctx->split_idx.as<int32_t>(), nullptr, nsub, slog, nullptr, nullptr, nullptr};
   if (hcap > 0) {
     HIPCHK(ctx->split_tab.reserve(sizeof(int32_t) * ((int64_t)NL * (nsub + 1) + 1)));
     spl.tab = ctx->split_tab.as<int32_t>();
@@ -512,11 +556,16 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
     HIPCHK(ctx->segoff.reserve(sizeof(int64_t) * (H + 1)));
     HIPCHK(ctx->icnt.reserve(sizeof(int64_t) * (H + 1)));
     HIPCHK(ctx->itemoff.reserve(sizeof(int64_t) * (H + 1)));
+    if (ho.rows) HIPCHK(ctx->urows.reserve(sizeof(UnitRows) * (nunit_cap + 1)));
     k_build_units<<<(H + 255) / 256, 256, 0, st>>>(H, ctx->heavy_cols.as<int32_t>(), ctx->sub.as<int32_t>(), nsub,
                                                    slog, heavy_unit_cap<SRT>(), heavy_span_cap<SRT>(), span,
                                                    colptr, B.cp, units, ctx->ucnt.as<int64_t>(),
                                                    ctx->uspan.as<int2>(), nnz, ctx->nunits.as<int32_t>(),
-                                                   ctx->segsz.as<int64_t>(), ctx->icnt.as<int64_t>());
+                                                   ctx->segsz.as<int64_t>(), ctx->icnt.as<int64_t>(),
+                                                   ho.mode, ho.poff,
+                                                   ho.rows ? ctx->urows.as<UnitRows>() : nullptr);
+    spl.hrows = ho.rows;
+    spl.urows = ho.rows ? ctx->urows.as<UnitRows>() : nullptr;
     // offsets of every heavy column's block of (unit, B nonzero) segments; total -> sc[8]
     const int64_t ht = (H + kScanTile - 1) / kScanTile;
     k_scan_tiles<<<(int)ht, 256, 0, st>>>(H, ctx->segsz.as<int64_t>(), ctx->scan_tiles.as<int64_t>());
@@ -531,25 +580,33 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
     HIPCHK(hipGetLastError());
   }
 
-  // 5. numeric binning (columns and units, one host sync) + kernels
+  // 5. numeric binning (columns and units, one host sync) + kernels; heavy items split into the
+  //    rows-known list (k_num_heavy_known) and the rest (k_num_heavy), counts -> sc[12], sc[13]
   Classes cn;
   BinParams nbp{kNumWave, kNumBlock, 64, 0};
   HIPCHK(hipMemsetAsync(hist, 0, sizeof(unsigned long long) * 128, st));
   bin_count(st, N, nnz, span, nbp, hist, list);
-  unsigned long long hn[128], tots[2] = {0, 0};
+  if (H > 0) {
+    const int64_t icap = nunit_cap / kItemUnits + H + 1;   // >= sum of ceil(nunits / kItemUnits)
+    HIPCHK(ctx->items.reserve(sizeof(HeavyItem) * (icap + 1)));
+    HIPCHK(ctx->oitems.reserve(sizeof(HeavyItem) * (icap + 1)));
+    k_heavy_items_split<SRT, CBG_HEAVY_LOGT, CBG_HEAVY_NT><<<(H + 255) / 256, 256, 0, st>>>(
+        H, ctx->nunits.as<int32_t>(), units, nsub, ctx->uspan.as<int2>(), spl.urows, ctx->items.as<HeavyItem>(),
+        ctx->oitems.as<HeavyItem>(), sc + 12);
+    HIPCHK(hipGetLastError());
+  }
+  unsigned long long hn[128], tots[6] = {0, 0, 0, 0, 0, 0};
   HIPCHK(hipMemcpyAsync(hn, hist, sizeof(unsigned long long) * 128, hipMemcpyDeviceToHost, st));
   if (H > 0) HIPCHK(hipMemcpyAsync(tots, sc + 8, sizeof(tots), hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
   const int64_t segtot = (int64_t)tots[0], nitems = (int64_t)tots[1];
+  const int64_t nknown = (int64_t)tots[4], nother = (int64_t)tots[5];
   if (H > 0) {
     HIPCHK(ctx->useg.reserve(sizeof(UnitSeg) * (segtot + 1)));
-    HIPCHK(ctx->items.reserve(sizeof(HeavyItem) * (nitems + 1)));
     spl.useg = ctx->useg.as<UnitSeg>();
     k_unit_segs<<<H, 256, 0, st>>>(ctx->heavy_cols.as<int32_t>(), ctx->nunits.as<int32_t>(),
                                    ctx->segoff.as<int64_t>(), units, nsub, A.cp, A.ir, B.cp, B.ir, spl,
                                    ctx->useg.as<UnitSeg>());
-    k_heavy_items<<<(H + 255) / 256, 256, 0, st>>>(H, ctx->nunits.as<int32_t>(), ctx->itemoff.as<int64_t>(),
-                                                   ctx->items.as<HeavyItem>());
     HIPCHK(hipGetLastError());
   }
   if ((s = bin_fill(st, N, nnz, span, nbp, hist, hn, list, &cn)) != CBG_OK) return s;
@@ -560,14 +617,20 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
   for (int c = 0; c < 12; ++c) pf.bins[c] = (int64_t)cn.hist[c];
   pf.bins[12] = H;
   pf.bins[13] = nitems;
+  pf.known_items = nknown;
   NumOut<V> oc{own->ir.as<int32_t>(), own->val.as<V>(), adderr, ovf_n, ctx->ovf_list.as<int32_t>()};
   {
     hipError_t e = launch_numeric_classes<SRT, V, false>(st, cn, list, nullptr, A, B, span, colptr, spl, oc);
     if (e == hipSuccess && H > 0) {
       NumOut<V> ou{own->ir.as<int32_t>(), own->val.as<V>(), adderr, uovf_n, ctx->uovf_list.as<int32_t>()};
       HIPCHK(hipEventRecord(ctx->ev[6], st));
-      e = launch_num_heavy<CBG_HEAVY_LOGT, CBG_HEAVY_NT, SRT, V>(st, nitems, ctx->items.as<HeavyItem>(), ctx->heavy_cols.as<int32_t>(),
-                                             units, nsub, A, B, span, spl, ou);
+      e = launch_num_heavy_known<CBG_HEAVY_LOGT, CBG_HEAVY_NT, SRT, V>(st, nknown, ctx->items.as<HeavyItem>(),
+                                                                     ctx->heavy_cols.as<int32_t>(), units, nsub, A, B,
+                                                                     span, spl, ou);
+      if (e == hipSuccess)
+        e = launch_num_heavy<CBG_HEAVY_LOGT, CBG_HEAVY_NT, SRT, V>(st, nother, ctx->oitems.as<HeavyItem>(),
+                                                                 ctx->heavy_cols.as<int32_t>(), units, nsub, A, B, span,
+                                                                 spl, ou);
       HIPCHK(hipEventRecord(ctx->ev[7], st));
       // overflowed hash units -> single-subwindow (dense) units
       if (e == hipSuccess) {

@@ -82,6 +82,7 @@ constexpr int64_t kUnitCap = CBG_UNIT_CAP;   // max outputs of a multi-subwindow
 constexpr int kSplitMin = 16;      // A columns at least this long get split-table rows
 constexpr int kMaxSub = 2048;      // max subwindows per column (SUBW chosen so nrow/SUBW <= kMaxSub)
 constexpr int kItemUnits = CBG_ITEM_UNITS; // units of one heavy column per workgroup item (k_num_heavy)
+constexpr int kMaxParts = 32;      // symbolic parts per wide column (wider, hypersparse columns: windowed path)
 
 template <typename V>
 struct DevCsc {
@@ -93,12 +94,15 @@ struct DevCsc {
 
 // split table: for long A columns, tab[idx[k]*(nsub+1) + s] = (first entry with row >= s*SUBW) - cp[k]
 struct UnitSeg;
+struct UnitRows;
 struct Split {
   const int32_t* idx;   // per A column: row of tab, or -1
   const int32_t* tab;
   int32_t nsub;         // subwindows in the row space
   int32_t log;          // log2(SUBW)
   const UnitSeg* useg;  // precomputed unit segments (k_unit_segs)
+  const int32_t* hrows; // sorted output rows of heavy columns written by the symbolic pass (or null)
+  const UnitRows* urows;// per unit: where its rows lie in hrows (k_build_units)
 };
 
 struct Unit {
@@ -111,6 +115,14 @@ struct Unit {
 
 struct UnitSeg {        // A segment [a0, a1) of one (unit, B nonzero) pair
   int64_t a0, a1;
+};
+
+// A unit's output rows inside the symbolic pass's row scratch: up to 3 contiguous pieces (a unit's
+// span crosses at most two 2^kPartLog-row part boundaries); np = 0: rows unknown (old rank path).
+struct UnitRows {
+  int64_t off[3];
+  int32_t n[3];
+  int32_t np;
 };
 
 // per-item description shared by all numeric/symbolic kernels
@@ -252,15 +264,20 @@ __global__ void __launch_bounds__(256) k_col_stats(int64_t ncol, const int64_t* 
     flop[j] = f;
     span[j] = make_int2(lo, hi);
   }
-  // block-level total of multiplies
-  __shared__ unsigned long long s_tot;
-  if (threadIdx.x == 0) s_tot = 0;
+  // block-level totals: multiplies -> total[0]; an upper bound of the heavy columns' outputs,
+  // sum of min(flop, span) over columns with flop > kHeavy -> total[10] (row handoff scratch)
+  __shared__ unsigned long long s_tot, s_hb;
+  if (threadIdx.x == 0) { s_tot = 0; s_hb = 0; }
   __syncthreads();
   int64_t wf = (sub == 0) ? f : 0;
+  int64_t hb = (sub == 0 && f > 4096 && hi >= lo) ? min(f, (int64_t)hi - lo + 1) : 0;
   wf = wave_sum64(wf);
+  hb = wave_sum64(hb);
   if (lane_id() == 0 && wf) atomicAdd(&s_tot, (unsigned long long)wf);
+  if (lane_id() == 0 && hb) atomicAdd(&s_hb, (unsigned long long)hb);
   __syncthreads();
   if (threadIdx.x == 0 && s_tot) atomicAdd(total, s_tot);
+  if (threadIdx.x == 0 && s_hb) atomicAdd(total + 10, s_hb);
 }
 
 // ============================================================================ 2. binning
@@ -421,20 +438,22 @@ __device__ __forceinline__ void expand_staged(const SegBuf<V>& sb, int tid, int6
     int ss[U];
     int64_t qq[U];
     int nv[U];
+    // every load is issued unconditionally (index clamped into the group, or 0 for an idle lane, a
+    // valid entry of any non-empty A): divergent conditional loads make the compiler drain the load
+    // counter before each one, serialising the gathers
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int64_t g = g0 + (int64_t)u * NT + tid;
-      nv[u] = 0;
-      if (g < F) {
-        const int sg = seg_search<NT>(sb.off, g, P);
-        const int64_t k0 = (g - sb.off[sg]) * G;
-        ss[u] = sg;
-        qq[u] = sb.qb[sg] + k0;
-        nv[u] = (int)min<int64_t>(G, sb.len[sg] - k0);
+      const bool valid = g < F;
+      const int sg = seg_search<NT>(sb.off, valid ? g : 0, P);
+      const int64_t k0 = ((valid ? g : 0) - sb.off[sg]) * G;
+      ss[u] = sg;
+      qq[u] = sb.qb[sg] + k0;
+      nv[u] = valid ? (int)min<int64_t>(G, sb.len[sg] - k0) : 0;
+      const int64_t qs = nv[u] > 0 ? qq[u] : 0;
+      const int last = nv[u] > 0 ? nv[u] - 1 : 0;
 #pragma unroll
-        for (int i = 0; i < G; ++i)
-          if (i < nv[u]) it[u][i] = ld(qq[u] + i);
-      }
+      for (int i = 0; i < G; ++i) it[u][i] = ld(qs + min(i, last));
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -581,7 +600,21 @@ struct HeavyOut {       // columns with nnz > kHeavy: list + nnz per subwindow
   int32_t* cols;
   int32_t* sub;         // [h * nsub + s]
   int32_t nsub, log;
+  // Row handoff to the numeric pass (rows == nullptr: off).  A heavy column's bitmap is compacted
+  // into its sorted output rows, written to `rows` at an offset reserved from `cursor` (capacity `cap`,
+  // an upper bound of the heavy outputs); poff[h * kMaxParts + p] = offset of relative part p (or of
+  // the whole column, p = 0); mode[h] = 1 whole column in one run, 2 per part, other = unavailable.
+  int32_t* rows;
+  unsigned long long* cursor;
+  unsigned long long cap;
+  int64_t* poff;
+  int32_t* mode;
 };
+
+__device__ __forceinline__ int64_t reserve_rows(const HeavyOut& ho, int64_t n) {
+  const unsigned long long o = atomicAdd(ho.cursor, (unsigned long long)n);
+  return (o + (unsigned long long)n <= ho.cap) ? (int64_t)o : -1;
+}
 
 // symbolic insert of row r into a presence bitmap (base = 32-aligned first row) or a keys-only hash;
 // returns 1 if r is new
@@ -648,6 +681,31 @@ __global__ void __launch_bounds__(256) k_sym_wave(const int32_t* __restrict__ li
           if (((base + 32 * w2) >> ho.log) == s) c += __popc((uint32_t)tab[w2]);
         const int64_t cs = wave_sum64(c);
         if (l == 0) dst[s] = (int32_t)cs;
+      }
+      if (ho.rows) {   // sorted rows for the numeric pass: words in order, 64 at a time
+        int64_t off = 0;
+        if (l == 0) off = reserve_rows(ho, tot);
+        off = __shfl(off, 0, kWave);
+        if (off >= 0) {
+          int64_t run = off;
+          for (int w0 = 0; w0 < nw; w0 += kWave) {
+            const int w2 = w0 + l;
+            uint32_t wd = w2 < nw ? (uint32_t)tab[w2] : 0u;
+            const int pc = __popc(wd);
+            const int inc = wave_incl_scan(pc);
+            int64_t pos = run + inc - pc;
+            while (wd) {
+              const int b = __ffs(wd) - 1;
+              wd &= wd - 1;
+              ho.rows[pos++] = base + 32 * w2 + b;
+            }
+            run += __shfl(inc, kWave - 1, kWave);
+          }
+        }
+        if (l == 0) {
+          ho.poff[(int64_t)h * kMaxParts] = off;
+          ho.mode[h] = off >= 0 ? 1 : 0;
+        }
       }
     }
     wave_sync();
@@ -724,6 +782,35 @@ __global__ void __launch_bounds__(NT) k_sym_block(const int32_t* __restrict__ li
       __syncthreads();
       int32_t* dst = ho.sub + (int64_t)misc[2] * ho.nsub;
       for (int s = threadIdx.x; s <= sl - sf; s += NT) dst[sf + s] = scnt[s];
+      if (ho.rows && bitmap) {   // sorted rows for the numeric pass: contiguous words per thread
+        const int nw = ((sp.y - base) >> 5) + 1;
+        const int WPT = (nw + NT - 1) / NT;
+        const int w0 = min(nw, (int)threadIdx.x * WPT), w1 = min(nw, w0 + WPT);
+        int c = 0;
+        for (int w = w0; w < w1; ++w) c += __popc((uint32_t)tab[w]);
+        int tot2;
+        const int ex = block_excl_scan<NT>(c, lens, &tot2);   // lens is idle after the expansion
+        if (threadIdx.x == 0) {
+          const int64_t off = reserve_rows(ho, tot2);
+          misc[4] = (int)(off & 0xffffffff);
+          misc[5] = (int)(off >> 32);
+          ho.poff[(int64_t)misc[2] * kMaxParts] = off;
+          ho.mode[misc[2]] = off >= 0 ? 1 : 0;
+        }
+        __syncthreads();
+        const int64_t off = (int64_t)(uint32_t)misc[4] | ((int64_t)misc[5] << 32);
+        if (off >= 0) {
+          int64_t pos = off + ex;
+          for (int w = w0; w < w1; ++w) {
+            uint32_t wd = (uint32_t)tab[w];
+            while (wd) {
+              const int b = __ffs(wd) - 1;
+              wd &= wd - 1;
+              ho.rows[pos++] = base + 32 * w + b;
+            }
+          }
+        }
+      }
     }
     __syncthreads();
   }
@@ -747,7 +834,6 @@ constexpr int kPartNT = CBG_PART_NT;
 // column has flop > kHeavy (2*flop > 2^(class+4) words), so the heavy lists can hold it
 constexpr int kWideClass = kPartLog - 9 > 9 ? kPartLog - 9 : 9;
 static_assert(kPartLog >= 17 && kPartLog <= 19, "part bitmap 16..64 KB");
-constexpr int kMaxParts = 32;   // wider columns (hypersparse, > 8M-row spans) take the windowed path
 struct PartItem {
   int32_t j, p, h;
 };
@@ -830,12 +916,40 @@ __global__ void __launch_bounds__(NT) k_sym_part(const PartItem* __restrict__ it
         });
     __syncthreads();
     int c = 0;
-#pragma unroll 8
-    for (int w = 0; w < WPT; ++w) c += __popc(tab[threadIdx.x * WPT + w]);
+    uint32_t wds[WPT];
+#pragma unroll
+    for (int w = 0; w < WPT; ++w) {
+      wds[w] = tab[threadIdx.x * WPT + w];
+      c += __popc(wds[w]);
+    }
     if (c) atomicAdd(&scnt[((r0 + threadIdx.x * WPT * 32) >> spl.log) - s0], c);
-    const int64_t wc = wave_sum64(c);
-    if (lane_id() == 0 && wc) atomicAdd(&misc[0], (int)wc);
+    int ptot;
+    const int ex = block_excl_scan<NT>(c, lens, &ptot);   // lens is idle after the expansion
+    if (threadIdx.x == 0) {
+      misc[0] = ptot;
+      int64_t off = -1;
+      if (ho.rows && ptot > 0) {
+        off = reserve_rows(ho, ptot);
+        ho.poff[(int64_t)it.h * kMaxParts + it.p] = off;
+        atomicOr(&ho.mode[it.h], off >= 0 ? 2 : 16);
+      }
+      misc[4] = (int)(off & 0xffffffff);
+      misc[5] = (int)(off >> 32);
+    }
     __syncthreads();
+    const int64_t off = (int64_t)(uint32_t)misc[4] | ((int64_t)misc[5] << 32);
+    if (off >= 0) {   // this part's sorted rows for the numeric pass (each thread: its words' rows)
+      int64_t pos = off + ex;
+#pragma unroll
+      for (int w = 0; w < WPT; ++w) {
+        uint32_t wd = wds[w];
+        while (wd) {
+          const int b = __ffs(wd) - 1;
+          wd &= wd - 1;
+          ho.rows[pos++] = r0 + 32 * (threadIdx.x * WPT + w) + b;
+        }
+      }
+    }
     if (threadIdx.x == 0 && misc[0]) atomicAdd((unsigned long long*)&nnz[it.j], (unsigned long long)misc[0]);
     const int32_t sf = max(s0, sp.x >> spl.log), sl = min(s1 - 1, sp.y >> spl.log);
     int32_t* dst = ho.sub + (int64_t)it.h * ho.nsub;
@@ -980,7 +1094,9 @@ __global__ void k_build_units(int H, const int32_t* __restrict__ cols, const int
                               const int2* __restrict__ span, const int64_t* __restrict__ colptr,
                               const int64_t* __restrict__ Bcp, Unit* __restrict__ units, int64_t* __restrict__ ucnt,
                               int2* __restrict__ uspan, int64_t* __restrict__ nnz, int32_t* __restrict__ nunits,
-                              int64_t* __restrict__ segsz, int64_t* __restrict__ icnt) {
+                              int64_t* __restrict__ segsz, int64_t* __restrict__ icnt,
+                              const int32_t* __restrict__ hmode, const int64_t* __restrict__ hpoff,
+                              UnitRows* __restrict__ urows) {
   const int h = blockIdx.x * blockDim.x + threadIdx.x;
   if (h >= H) return;
   const int32_t j = cols[h];
@@ -997,12 +1113,34 @@ __global__ void k_build_units(int H, const int32_t* __restrict__ cols, const int
   int64_t out = colptr[j];
   int u = 0, st = sf;
   int64_t acc = 0;
+  // where each subwindow's rows lie in the symbolic row scratch (mode 1: one run for the column,
+  // mode 2: one run per 2^kPartLog-row part, parts relative to the column's first part)
+  const int32_t mode = hmode ? hmode[h] : 0;
+  const int pshift = kPartLog - log;   // subwindows -> parts
+  const int32_t P0 = sp.x >> kPartLog;
+  int64_t pfx_col = 0, pfx_part = 0;
+  int32_t curP = -1;
+  UnitRows ur{};
+  int64_t poff_cur = -1, pn_cur = 0;
+  auto close_piece = [&]() {
+    if (pn_cur > 0) {
+      if (ur.np < 3) { ur.off[ur.np] = poff_cur; ur.n[ur.np] = (int32_t)pn_cur; ++ur.np; }
+      else ur.np = 4;   // cannot happen (span cap < 2 parts): rows unknown for this unit
+    }
+    pn_cur = 0;
+    poff_cur = -1;
+  };
   auto emit = [&](int32_t s0, int32_t s1, int64_t n) {
     units[slot + u] = Unit{j, s0, s1, (int32_t)n, out, -1};
     ucnt[slot + u] = n;
     const int64_t lo = max((int64_t)sp.x, (int64_t)s0 << log);
     const int64_t hi = min((int64_t)sp.y, ((int64_t)s1 << log) - 1);
     uspan[slot + u] = make_int2((int32_t)lo, (int32_t)hi);
+    close_piece();
+    if (mode != 1 && mode != 2) ur.np = 0;
+    if (ur.np > 3) ur.np = 0;
+    if (urows) urows[slot + u] = ur;
+    ur = UnitRows{};
     ++u;
     out += n;
   };
@@ -1015,7 +1153,23 @@ __global__ void k_build_units(int H, const int32_t* __restrict__ cols, const int
       st = s;
       acc = 0;
     }
+    // this subwindow's rows in the scratch
+    int64_t ro = -1;
+    if (mode == 1) {
+      ro = hpoff[(int64_t)h * kMaxParts] + pfx_col;
+    } else if (mode == 2) {
+      const int32_t P = s >> pshift;
+      if (P != curP) { curP = P; pfx_part = 0; }
+      const int32_t pr = P - P0;
+      ro = (pr >= 0 && pr < kMaxParts) ? hpoff[(int64_t)h * kMaxParts + pr] + pfx_part : -1;
+    }
+    if (n > 0) {
+      if (pn_cur > 0 && ro == poff_cur + pn_cur) pn_cur += n;
+      else { close_piece(); poff_cur = ro; pn_cur = n; }
+    }
     acc += n;
+    pfx_col += n;
+    pfx_part += n;
   }
   if (acc > 0) emit(st, sl + 1, acc);
   nnz[j] = 0;   // the whole column is now covered by units
@@ -1477,7 +1631,7 @@ struct HeavyItem {
 
 template <class SRT, typename V, int LOGT, int NT>
 constexpr size_t num_heavy_lds() {
-  return num_block_lds<SRT, V, LOGT, NT>() + kItemUnits * sizeof(Unit) + (size_t)(1 << LOGT) * 2;
+  return num_block_lds<SRT, V, LOGT, NT>() + kItemUnits * (sizeof(Unit) + sizeof(UnitRows)) + (size_t)(1 << LOGT) * 2;
 }
 
 template <class SRT, typename V, int LOGT, int NT>
@@ -1499,7 +1653,8 @@ __global__ void __launch_bounds__(NT) k_num_heavy(const HeavyItem* __restrict__ 
   Acc* vals = (Acc*)(s_units + kItemUnits);      // T + NT
   int32_t* keys = (int32_t*)(vals + T + NT);     // T + NT
   uint32_t* hc = (uint32_t*)(keys + T + NT);     // T/2 packed home counters (compaction) / rank directory
-  static_assert(sizeof(Unit) % 8 == 0 && (NT % 2) == 0, "LDS carve-up must keep 8-byte alignment");
+  static_assert(sizeof(Unit) % 8 == 0 && sizeof(UnitRows) % 8 == 0 && (NT % 2) == 0,
+                "LDS carve-up must keep 8-byte alignment");
   constexpr int64_t kRankBytes = (int64_t)(T + NT) * (int64_t)(sizeof(Acc) + 4);
   const SegBuf<V> sb{qb, off, bvs, scr, lens};
   STAMP_DECL
@@ -1634,7 +1789,13 @@ __global__ void __launch_bounds__(NT) k_num_heavy(const HeavyItem* __restrict__ 
                 const int o = r - wk.lo;
                 atomicOr(&bm[o >> 5], 1u << (o & 31));
               },
-              [&]() { __syncthreads(); return directory(); },
+              [&]() {
+                __syncthreads();
+                STAMP(24);
+                const bool d = directory();
+                STAMP(25);
+                return d;
+              },
               [&](int32_t r, V a, V bv2, int64_t q, int64_t b) {
                 if (r < wk.lo || r > wk.hi) return;
                 const int o = r - wk.lo, w = o >> 5;
@@ -1708,6 +1869,204 @@ __global__ void __launch_bounds__(NT) k_num_heavy(const HeavyItem* __restrict__ 
     if (threadIdx.x == 0 && misc[2]) atomicOr(out.adderr, 1);
     __syncthreads();
     STAMP(5);
+  }
+}
+
+// ---- heavy numeric with the rows known (symbolic row handoff): one workgroup per item of up to
+// kItemUnits units, every unit of it eligible (heavy_unit_known).  Per unit:
+//   a. its sorted output rows come from the symbolic pass's scratch (UnitRows pieces): written to
+//      C.row (coalesced) and staged in LDS;
+//   b. the rank structure over the unit's span -- for every 64-row pair holding rows: two bitmap words
+//      and the index of its first row -- is built from the rows alone (words of empty pairs are never
+//      read, so nothing span-sized is cleared or scanned);
+//   c. ONE sweep over the multiplies: gather (row, value), slot = pre[pair] + popcounts below the row,
+//      SR::acc at that slot (exact: every gathered row of the unit's range is an output row);
+//   d. the values, already in row order, are written out.
+template <class SRT, int LOGT, int NT>
+__device__ __forceinline__ bool heavy_unit_known(const Unit& un, int2 usp, const UnitRows& ur) {
+  using Acc = typename SRT::Acc;
+  constexpr int T = 1 << LOGT;
+  constexpr int64_t kRankBytes = (int64_t)(T + NT) * (int64_t)(sizeof(Acc) + 4);
+  const int64_t spn = (int64_t)usp.y - usp.x + 1;
+  const int64_t nw = (spn + 31) >> 5;
+  const int64_t cpad = (un.cnt + 1) & ~1;
+  return !SRT::kAddIsError && CBG_RANK_MODE && ur.np >= 1 && ur.np <= 3 && spn > T && un.cnt <= T &&
+         nw <= 2 * (int64_t)T && cpad * (int64_t)sizeof(Acc) + 4 * (nw + 1) <= kRankBytes;
+}
+
+#ifndef CBG_UNROLL_KNOWN
+#define CBG_UNROLL_KNOWN 3
+#endif
+
+template <class SRT, typename V, int LOGT, int NT, bool AV>
+__global__ void __launch_bounds__(NT) k_num_heavy_known(const HeavyItem* __restrict__ items,
+                                                        const int32_t* __restrict__ hcols,
+                                                        const Unit* __restrict__ units, int32_t nsub, DevCsc<V> A,
+                                                        DevCsc<V> B, const int2* __restrict__ span, Split spl,
+                                                        NumOut<V> out) {
+  using Acc = typename SRT::Acc;
+  constexpr int T = 1 << LOGT;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  int64_t* qb = (int64_t*)smem;                  // NT
+  int64_t* off = qb + NT;                        // NT
+  int64_t* scr = off + NT;                       // NT/64 + 1
+  V* bvs = (V*)(scr + NT / kWave + 1);           // NT
+  int32_t* lens = (int32_t*)(bvs + NT);          // NT
+  int* misc = lens + NT;                         // 64 ints
+  Unit* s_units = (Unit*)(misc + 64);            // kItemUnits
+  UnitRows* s_urows = (UnitRows*)(s_units + kItemUnits);   // kItemUnits
+  Acc* vals = (Acc*)(s_urows + kItemUnits);      // (T + NT) * (sizeof(Acc) + 4) bytes: values, then the bitmap
+  uint16_t* pre = (uint16_t*)((char*)vals + (size_t)(T + NT) * (sizeof(Acc) + 4));   // T entries
+  const SegBuf<V> sb{qb, off, bvs, scr, lens};
+  STAMP_DECL
+  STAMP(0);
+  const HeavyItem item = items[blockIdx.x];
+  const int32_t j = hcols[item.h];
+  const int2 sp = span[j];
+  const int64_t bs = B.cp[j], nb = B.cp[j + 1] - bs;
+  const int nu = item.u1 - item.u0;
+  if ((int)threadIdx.x < nu) {
+    const int64_t slot = (int64_t)item.h * nsub + item.u0 + threadIdx.x;
+    s_units[threadIdx.x] = units[slot];
+    s_urows[threadIdx.x] = spl.urows[slot];
+  }
+  __syncthreads();
+  auto fetch = [&](int u, int64_t c, int64_t& a0, int64_t& a1, V& bv) {
+    const int64_t i = c + threadIdx.x;
+    a0 = a1 = 0;
+    bv = V(0);
+    if (u < nu && i < nb) {
+      const UnitSeg g = spl.useg[s_units[u].segbase + i];
+      a0 = g.a0;
+      a1 = g.a1;
+      bv = load_val(B.val, bs + i);
+    }
+  };
+  int64_t pa0, pa1;
+  V pbv;
+  fetch(0, 0, pa0, pa1, pbv);
+  for (int u = 0; u < nu; ++u) {
+    const Unit un = s_units[u];
+    const UnitRows ur = s_urows[u];
+    const int32_t lo = (int32_t)max((int64_t)sp.x, (int64_t)un.s0 << spl.log);
+    const int32_t hi = (int32_t)min((int64_t)sp.y, ((int64_t)un.s1 << spl.log) - 1);
+    const int cnt = un.cnt;
+    const int cpad = (cnt + 1) & ~1;
+    uint32_t* bm = (uint32_t*)(vals + cpad);
+    STAMP(1);
+    // a. rows: scratch -> C.row and LDS (staged in the values region); all of a thread's loads are
+    //    issued before any is used (cnt <= T, so at most T/NT per thread)
+    int32_t* urow = (int32_t*)vals;
+    const int64_t o1 = ur.n[0], o2 = o1 + (ur.np > 1 ? ur.n[1] : 0);
+    {
+      constexpr int RPT = (T + NT - 1) / NT;
+      int32_t rr[RPT];
+#pragma unroll
+      for (int k = 0; k < RPT; ++k) {
+        const int i = threadIdx.x + k * NT;
+        const int ic = i < cnt ? i : 0;
+        const int64_t src = ic < o1 ? ur.off[0] + ic : ic < o2 ? ur.off[1] + (ic - o1) : ur.off[2] + (ic - o2);
+        rr[k] = spl.hrows[src];
+      }
+#pragma unroll
+      for (int k = 0; k < RPT; ++k) {
+        const int i = threadIdx.x + k * NT;
+        if (i < cnt) {
+          out.row[un.outoff + i] = rr[k];
+          urow[i] = rr[k];
+        }
+      }
+    }
+    __syncthreads();
+    // b. pair words and directory: the first row of a pair clears its two words and records its index,
+    //    then every row sets its bit
+    for (int i = threadIdx.x; i < cnt; i += NT) {
+      const int pr = (urow[i] - lo) >> 6;
+      if (i == 0 || ((urow[i - 1] - lo) >> 6) != pr) {
+        bm[2 * pr] = 0u;
+        bm[2 * pr + 1] = 0u;
+        pre[pr] = (uint16_t)i;
+      }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < cnt; i += NT) {
+      const int o = urow[i] - lo;
+      atomicOr(&bm[o >> 5], 1u << (o & 31));
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < cnt; i += NT) vals[i] = SRT::identity();
+    __syncthreads();
+    STAMP(2);
+    // c. one sweep over the unit's multiplies
+    for (int64_t c = 0; c < nb; c += NT) {
+      const int64_t a0 = pa0, a1 = pa1;
+      const V bv = pbv;
+      if (c + NT < nb) fetch(u, c + NT, pa0, pa1, pbv);
+      else fetch(u + 1, 0, pa0, pa1, pbv);
+      const int64_t F = stage_segments<NT, false, kGroupHeavy, V>(sb, a0, a1, bv);
+      STAMP(3);
+      expand_staged<NT, CBG_UNROLL_KNOWN, kGroupHeavy, V>(
+          sb, threadIdx.x, F, bs + c, (int)min<int64_t>(NT, nb - c),
+          [&](int64_t q) { return NumItem<V>{A.ir[q], AV ? A.val[q] : V(1)}; },   // AV: no pointer test per load
+          [&](const NumItem<V>& it, V bv2, int64_t q, int64_t b) {
+            if (it.r < lo || it.r > hi) return;
+            const int o = it.r - lo, w = o >> 5;
+            const int slot = (int)pre[w >> 1] + ((w & 1) ? __popc(bm[w - 1]) : 0) +
+                             __popc(bm[w] & ((1u << (o & 31)) - 1u));
+            SRT::acc(&vals[slot], SRT::mul(it.a, bv2, q, b));
+          });
+      __syncthreads();
+      STAMP(4);
+    }
+    // d. values out, row order
+    for (int i = threadIdx.x; i < cnt; i += NT) out.val[un.outoff + i] = SRT::out(vals[i], A.val, B.val);
+    __syncthreads();
+    STAMP(5);
+  }
+}
+
+template <class SRT, typename V, int LOGT, int NT>
+constexpr size_t num_heavy_known_lds() {
+  return (size_t)NT * (8 + 8 + sizeof(V) + 4) + (size_t)(NT / kWave + 1) * 8 + 64 * 4 +
+         kItemUnits * (sizeof(Unit) + sizeof(UnitRows)) + (size_t)((1 << LOGT) + NT) * (sizeof(typename SRT::Acc) + 4) +
+         (size_t)(1 << LOGT) * 2;
+}
+
+// Items of every heavy column: ceil(nunits / kItemUnits) consecutive unit groups, split into the
+// rows-known list (every unit eligible for k_num_heavy_known) and the rest (k_num_heavy); the two
+// counts go to counts[0], counts[1].
+template <class SRT, int LOGT, int NT>
+__global__ void k_heavy_items_split(int H, const int32_t* __restrict__ nunits, const Unit* __restrict__ units,
+                                    int32_t nsub, const int2* __restrict__ uspan, const UnitRows* __restrict__ urows,
+                                    HeavyItem* __restrict__ kitems, HeavyItem* __restrict__ oitems,
+                                    unsigned long long* __restrict__ counts) {
+  const int h = blockIdx.x * blockDim.x + threadIdx.x;
+  const int nu = h < H ? nunits[h] : 0;
+  // pass 1: this column's item kinds (bit i of kmask: item i is rows-known); pass 2: write
+  uint64_t kmask = 0;
+  int nk = 0, no = 0;
+  for (int u = 0, i = 0; u < nu; u += kItemUnits, ++i) {
+    const int u1 = min(nu, u + kItemUnits);
+    bool known = urows != nullptr && i < 64;
+    for (int k = u; k < u1 && known; ++k) {
+      const int64_t slot = (int64_t)h * nsub + k;
+      known = heavy_unit_known<SRT, LOGT, NT>(units[slot], uspan[slot], urows[slot]);
+    }
+    if (known) { kmask |= 1ull << i; ++nk; } else ++no;
+  }
+  // one atomic per wave and list (a single counter hit by every column serialises at the L2)
+  const int ik = wave_incl_scan(nk), io = wave_incl_scan(no);
+  unsigned long long bk = 0, bo = 0;
+  if (lane_id() == kWave - 1) {
+    bk = ik ? atomicAdd(&counts[0], (unsigned long long)ik) : 0;
+    bo = io ? atomicAdd(&counts[1], (unsigned long long)io) : 0;
+  }
+  bk = __shfl(bk, kWave - 1, kWave) + (ik - nk);
+  bo = __shfl(bo, kWave - 1, kWave) + (io - no);
+  for (int u = 0, i = 0; u < nu; u += kItemUnits, ++i) {
+    const HeavyItem it{h, u, min(nu, u + kItemUnits), 0};
+    if (i < 64 && ((kmask >> i) & 1)) kitems[bk++] = it;
+    else oitems[bo++] = it;
   }
 }
 

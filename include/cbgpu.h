@@ -112,7 +112,8 @@ typedef struct cbg_ctx cbg_ctx;
 typedef struct {
   double flops_ms, bin_ms, symbolic_ms, scan_ms, numeric_ms, total_ms;
   int64_t multiplies, nnz_out, bins[16];
-  double heavy_ms;      /* k_num_heavy alone (heavy-column units), HIP events on the context stream */
+  double heavy_ms;      /* k_num_heavy_known + k_num_heavy (heavy-column units), HIP events on the context stream */
+  int64_t known_items;  /* heavy items whose rows came from the symbolic pass (k_num_heavy_known) */
 } cbg_profile;
 
 int32_t     cbg_abi_version(void);

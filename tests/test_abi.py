@@ -56,7 +56,7 @@ def test_struct_layouts_match_header():
     # cbg_dcsc_view: 4 int64, 3 pointers, 2 int32, pointer, enum, int32 -> 80 bytes on LP64
     assert ctypes.sizeof(_abi.DcscView) == 80
     assert ctypes.sizeof(_abi.CscResult) == 72
-    assert ctypes.sizeof(_abi.Profile) == 6 * 8 + 2 * 8 + 16 * 8 + 8   # + heavy_ms
+    assert ctypes.sizeof(_abi.Profile) == 6 * 8 + 2 * 8 + 16 * 8 + 8 + 8   # + heavy_ms, known_items
 
 
 def test_init_without_gpu_fails_loudly():
