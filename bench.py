@@ -182,7 +182,7 @@ def bench_local(args):
         "phases_ms": {k: round(float(np.mean([p[k] for p in profs])), 3)
                       for k in ("flops_ms", "bin_ms", "symbolic_ms", "scan_ms", "numeric_ms", "heavy_ms",
                                 "total_ms")},
-        "heavy_items": {"total": int(profs[-1]["bins"][13]), "rows_known": int(profs[-1]["known_items"])},
+        "heavy_items": {"items": int(profs[-1]["bins"][13]), "rows_known_units": int(profs[-1]["known_items"])},
         "roofline": {"bound": "hbm", "kernel": "k_num_heavy", "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "traffic_source": tsrc, "algorithmic_bytes_per_launch": hb, "avg_launch_ms": heavy_ms,

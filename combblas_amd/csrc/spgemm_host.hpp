@@ -129,6 +129,7 @@ struct cbg_ctx {
   DevBuf nunits, segsz, segoff, useg, icnt, itemoff, items, parts, wide_win;
   DevBuf hrows, hmode, hpoff, urows;   // symbolic -> numeric row handoff of heavy columns
   DevBuf oitems;                       // heavy items the rows-known kernel does not take
+  int ncu = 0;                         // compute units (persistent grids)
   int row_handoff = -1;                // -1: read CBG_ROW_HANDOFF once (default on)
 };
 
@@ -290,31 +291,31 @@ hipError_t launch_num_block(hipStream_t st, const int32_t* l, const int* n_dev, 
   k_num_block<SRT, V, LOGT, NT, UNIT><<<(int)grid, NT, lds, st>>>(l, n_dev, n, units, A, B, span, colptr, spl, o);
   return hipGetLastError();
 }
+// persistent launches over device-counted lists: `grid` workgroups (one per CU; the LDS allows one)
 template <int LOGT, int NT, class SRT, typename V>
-hipError_t launch_num_heavy(hipStream_t st, int64_t nitems, const HeavyItem* items, const int32_t* hcols,
-                            const Unit* units, int32_t nsub, const DevCsc<V>& A, const DevCsc<V>& B, const int2* span,
-                            const Split& spl, const NumOut<V>& o) {
-  if (nitems <= 0) return hipSuccess;
+hipError_t launch_num_heavy(hipStream_t st, int grid, const HeavyItem* items, const unsigned long long* nitems,
+                            const int32_t* hcols, const Unit* units, int32_t nsub, const DevCsc<V>& A,
+                            const DevCsc<V>& B, const int2* span, const Split& spl, const NumOut<V>& o) {
+  if (grid <= 0) return hipSuccess;
   const size_t lds = num_heavy_lds<SRT, V, LOGT, NT>();
   hipError_t e = launch_cfg_lds((const void*)k_num_heavy<SRT, V, LOGT, NT>, lds);
   if (e != hipSuccess) return e;
-  k_num_heavy<SRT, V, LOGT, NT><<<(int)nitems, NT, lds, st>>>(items, hcols, units, nsub, A, B, span, spl, o);
+  k_num_heavy<SRT, V, LOGT, NT><<<grid, NT, lds, st>>>(items, nitems, hcols, units, nsub, A, B, span, spl, o);
   return hipGetLastError();
 }
 template <int LOGT, int NT, class SRT, typename V>
-hipError_t launch_num_heavy_known(hipStream_t st, int64_t nitems, const HeavyItem* items, const int32_t* hcols,
-                                  const Unit* units, int32_t nsub, const DevCsc<V>& A, const DevCsc<V>& B,
-                                  const int2* span, const Split& spl, const NumOut<V>& o) {
-  if (nitems <= 0) return hipSuccess;
+hipError_t launch_num_heavy_known(hipStream_t st, int grid, const KnownUnit* ku, const unsigned long long* nku,
+                                  const DevCsc<V>& A, const DevCsc<V>& B, const Split& spl, const NumOut<V>& o) {
+  if (grid <= 0) return hipSuccess;
   const size_t lds = num_heavy_known_lds<SRT, V, LOGT, NT>();
   if (A.val) {
     hipError_t e = launch_cfg_lds((const void*)k_num_heavy_known<SRT, V, LOGT, NT, true>, lds);
     if (e != hipSuccess) return e;
-    k_num_heavy_known<SRT, V, LOGT, NT, true><<<(int)nitems, NT, lds, st>>>(items, hcols, units, nsub, A, B, span, spl, o);
+    k_num_heavy_known<SRT, V, LOGT, NT, true><<<grid, NT, lds, st>>>(ku, nku, A, B, spl, o);
   } else {
     hipError_t e = launch_cfg_lds((const void*)k_num_heavy_known<SRT, V, LOGT, NT, false>, lds);
     if (e != hipSuccess) return e;
-    k_num_heavy_known<SRT, V, LOGT, NT, false><<<(int)nitems, NT, lds, st>>>(items, hcols, units, nsub, A, B, span, spl, o);
+    k_num_heavy_known<SRT, V, LOGT, NT, false><<<grid, NT, lds, st>>>(ku, nku, A, B, spl, o);
   }
   return hipGetLastError();
 }
@@ -586,27 +587,24 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
   BinParams nbp{kNumWave, kNumBlock, 64, 0};
   HIPCHK(hipMemsetAsync(hist, 0, sizeof(unsigned long long) * 128, st));
   bin_count(st, N, nnz, span, nbp, hist, list);
-  if (H > 0) {
-    const int64_t icap = nunit_cap / kItemUnits + H + 1;   // >= sum of ceil(nunits / kItemUnits)
-    HIPCHK(ctx->items.reserve(sizeof(HeavyItem) * (icap + 1)));
-    HIPCHK(ctx->oitems.reserve(sizeof(HeavyItem) * (icap + 1)));
-    k_heavy_items_split<SRT, CBG_HEAVY_LOGT, CBG_HEAVY_NT><<<(H + 255) / 256, 256, 0, st>>>(
-        H, ctx->nunits.as<int32_t>(), units, nsub, ctx->uspan.as<int2>(), spl.urows, ctx->items.as<HeavyItem>(),
-        ctx->oitems.as<HeavyItem>(), sc + 12);
-    HIPCHK(hipGetLastError());
-  }
-  unsigned long long hn[128], tots[6] = {0, 0, 0, 0, 0, 0};
+  unsigned long long hn[128], tots[2] = {0, 0};
   HIPCHK(hipMemcpyAsync(hn, hist, sizeof(unsigned long long) * 128, hipMemcpyDeviceToHost, st));
   if (H > 0) HIPCHK(hipMemcpyAsync(tots, sc + 8, sizeof(tots), hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
   const int64_t segtot = (int64_t)tots[0], nitems = (int64_t)tots[1];
-  const int64_t nknown = (int64_t)tots[4], nother = (int64_t)tots[5];
   if (H > 0) {
     HIPCHK(ctx->useg.reserve(sizeof(UnitSeg) * (segtot + 1)));
     spl.useg = ctx->useg.as<UnitSeg>();
     k_unit_segs<<<H, 256, 0, st>>>(ctx->heavy_cols.as<int32_t>(), ctx->nunits.as<int32_t>(),
                                    ctx->segoff.as<int64_t>(), units, nsub, A.cp, A.ir, B.cp, B.ir, spl,
                                    ctx->useg.as<UnitSeg>());
+    // units -> rows-known list + other items (device counts sc[12], sc[13]; units <= items * kItemUnits)
+    const int64_t ucap = nitems * kItemUnits + 1;
+    HIPCHK(ctx->items.reserve(sizeof(KnownUnit) * ucap));
+    HIPCHK(ctx->oitems.reserve(sizeof(HeavyItem) * ucap));
+    k_heavy_items_split<SRT, CBG_KNOWN_LOGT, CBG_KNOWN_NT><<<(H + 255) / 256, 256, 0, st>>>(
+        H, ctx->heavy_cols.as<int32_t>(), ctx->nunits.as<int32_t>(), units, nsub, ctx->uspan.as<int2>(), spl.urows,
+        B.cp, ctx->items.as<KnownUnit>(), ctx->oitems.as<HeavyItem>(), sc + 12);
     HIPCHK(hipGetLastError());
   }
   if ((s = bin_fill(st, N, nnz, span, nbp, hist, hn, list, &cn)) != CBG_OK) return s;
@@ -617,18 +615,22 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
   for (int c = 0; c < 12; ++c) pf.bins[c] = (int64_t)cn.hist[c];
   pf.bins[12] = H;
   pf.bins[13] = nitems;
-  pf.known_items = nknown;
   NumOut<V> oc{own->ir.as<int32_t>(), own->val.as<V>(), adderr, ovf_n, ctx->ovf_list.as<int32_t>()};
   {
     hipError_t e = launch_numeric_classes<SRT, V, false>(st, cn, list, nullptr, A, B, span, colptr, spl, oc);
     if (e == hipSuccess && H > 0) {
       NumOut<V> ou{own->ir.as<int32_t>(), own->val.as<V>(), adderr, uovf_n, ctx->uovf_list.as<int32_t>()};
       HIPCHK(hipEventRecord(ctx->ev[6], st));
-      e = launch_num_heavy_known<CBG_HEAVY_LOGT, CBG_HEAVY_NT, SRT, V>(st, nknown, ctx->items.as<HeavyItem>(),
-                                                                     ctx->heavy_cols.as<int32_t>(), units, nsub, A, B,
-                                                                     span, spl, ou);
+      if (ctx->ncu <= 0) {
+        int ncu = 0;
+        HIPCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device));
+        ctx->ncu = ncu > 0 ? ncu : 256;
+      }
+      const int grid = (int)std::min<int64_t>(ctx->ncu, nitems * kItemUnits);
+      e = launch_num_heavy_known<CBG_KNOWN_LOGT, CBG_KNOWN_NT, SRT, V>(st, grid, ctx->items.as<KnownUnit>(), sc + 12,
+                                                                     A, B, spl, ou);
       if (e == hipSuccess)
-        e = launch_num_heavy<CBG_HEAVY_LOGT, CBG_HEAVY_NT, SRT, V>(st, nother, ctx->oitems.as<HeavyItem>(),
+        e = launch_num_heavy<CBG_HEAVY_LOGT, CBG_HEAVY_NT, SRT, V>(st, grid, ctx->oitems.as<HeavyItem>(), sc + 13,
                                                                  ctx->heavy_cols.as<int32_t>(), units, nsub, A, B, span,
                                                                  spl, ou);
       HIPCHK(hipEventRecord(ctx->ev[7], st));
@@ -654,7 +656,9 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
   }
   HIPCHK(hipEventRecord(ctx->ev[5], st));
   int herr[8];
+  unsigned long long hknown = 0;
   HIPCHK(hipMemcpyAsync(herr, si, sizeof(herr), hipMemcpyDeviceToHost, st));
+  if (H > 0) HIPCHK(hipMemcpyAsync(&hknown, sc + 12, sizeof(hknown), hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
   float t;
   (void)hipEventElapsedTime(&t, ctx->ev[0], ctx->ev[1]); pf.flops_ms = t;
@@ -664,6 +668,7 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
   (void)hipEventElapsedTime(&t, ctx->ev[4], ctx->ev[5]); pf.numeric_ms = t;
   (void)hipEventElapsedTime(&t, ctx->ev[0], ctx->ev[5]); pf.total_ms = t;
   if (H > 0) { (void)hipEventElapsedTime(&t, ctx->ev[6], ctx->ev[7]); pf.heavy_ms = t; }
+  pf.known_items = (int64_t)hknown;
   pf.bins[14] = herr[4];   // overflowed units (re-run dense per subwindow)
   pf.bins[15] = herr[3];   // overflowed columns (windowed fallback)
   C->nnz = nnzc;

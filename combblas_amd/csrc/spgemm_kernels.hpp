@@ -60,6 +60,13 @@ constexpr int64_t kHeavy = 4096;   // nnz(C(:,j)) above which a column is split 
 #ifndef CBG_HEAVY_NT
 #define CBG_HEAVY_NT 1024
 #endif
+// k_num_heavy_known geometry (rows-known units; default: the k_num_heavy geometry)
+#ifndef CBG_KNOWN_LOGT
+#define CBG_KNOWN_LOGT CBG_HEAVY_LOGT
+#endif
+#ifndef CBG_KNOWN_NT
+#define CBG_KNOWN_NT CBG_HEAVY_NT
+#endif
 #ifndef CBG_ITEM_UNITS
 #define CBG_ITEM_UNITS 4
 #endif
@@ -398,6 +405,24 @@ __device__ __forceinline__ int seg_search(const int64_t* off, int64_t m, int P) 
   return s;
 }
 
+// U searches in lockstep: each step issues the U independent LDS reads together (one latency per
+// step instead of U); steps >= P are skipped by a uniform branch.
+template <int NT, int U>
+__device__ __forceinline__ void seg_search_n(const int64_t* off, const int64_t (&m)[U], int P, int (&s)[U]) {
+#pragma unroll
+  for (int u = 0; u < U; ++u) s[u] = 0;
+#pragma unroll
+  for (int step = NT >> 1; step > 0; step >>= 1) {
+    if (step < P) {
+      int64_t o[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) o[u] = off[s[u] + step];
+#pragma unroll
+      for (int u = 0; u < U; ++u) s[u] = o[u] <= m[u] ? s[u] + step : s[u];
+    }
+  }
+}
+
 // Stage one chunk of NT segments (this lane's a0, a1, bv) into LDS; returns the chunk's number of
 // GROUPS: a segment of len multiplies is cut into ceil(len/G) groups of G consecutive A
 // entries, and the groups (not the multiplies) are what lanes are dealt.  The LDS arrays are valid
@@ -436,20 +461,23 @@ __device__ __forceinline__ void expand_staged(const SegBuf<V>& sb, int tid, int6
   for (int64_t g0 = 0; g0 < F; g0 += (int64_t)NT * U) {
     Item it[U][G];
     int ss[U];
-    int64_t qq[U];
+    int64_t qq[U], m[U];
     int nv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t g = g0 + (int64_t)u * NT + tid;
+      m[u] = g < F ? g : 0;
+    }
+    seg_search_n<NT, U>(sb.off, m, P, ss);
     // every load is issued unconditionally (index clamped into the group, or 0 for an idle lane, a
     // valid entry of any non-empty A): divergent conditional loads make the compiler drain the load
     // counter before each one, serialising the gathers
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int64_t g = g0 + (int64_t)u * NT + tid;
-      const bool valid = g < F;
-      const int sg = seg_search<NT>(sb.off, valid ? g : 0, P);
-      const int64_t k0 = ((valid ? g : 0) - sb.off[sg]) * G;
-      ss[u] = sg;
+      const int sg = ss[u];
+      const int64_t k0 = (m[u] - sb.off[sg]) * G;
       qq[u] = sb.qb[sg] + k0;
-      nv[u] = valid ? (int)min<int64_t>(G, sb.len[sg] - k0) : 0;
+      nv[u] = g0 + (int64_t)u * NT + tid < F ? (int)min<int64_t>(G, sb.len[sg] - k0) : 0;
       const int64_t qs = nv[u] > 0 ? qq[u] : 0;
       const int last = nv[u] > 0 ? nv[u] - 1 : 0;
 #pragma unroll
@@ -462,6 +490,56 @@ __device__ __forceinline__ void expand_staged(const SegBuf<V>& sb, int tid, int6
 #pragma unroll
         for (int i = 0; i < G; ++i)
           if (i < nv[u]) ins(it[u][i], bv, qq[u] + i, base + ss[u]);
+      }
+    }
+  }
+}
+
+// expand_staged for an accumulator whose slot lookup only READS LDS (the rank directory): all U*G
+// slots are looked up first (slotf, branch-free on the clamped items; < 0 = drop), so their LDS reads
+// issue together, then the U*G accumulations run.
+template <int NT, int U, int G, typename V, class LdF, class SlotF, class AccF>
+__device__ __forceinline__ void expand_staged_slots(const SegBuf<V>& sb, int tid, int64_t F, int64_t base, int nseg,
+                                                    LdF ld, SlotF slotf, AccF acc) {
+  using Item = decltype(ld(int64_t(0)));
+  int P = 1;
+  while (P < nseg) P <<= 1;
+  for (int64_t g0 = 0; g0 < F; g0 += (int64_t)NT * U) {
+    Item it[U][G];
+    int ss[U], sl[U][G];
+    int64_t qq[U], m[U];
+    int nv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t g = g0 + (int64_t)u * NT + tid;
+      m[u] = g < F ? g : 0;
+    }
+    seg_search_n<NT, U>(sb.off, m, P, ss);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int sg = ss[u];
+      const int64_t k0 = (m[u] - sb.off[sg]) * G;
+      qq[u] = sb.qb[sg] + k0;
+      nv[u] = g0 + (int64_t)u * NT + tid < F ? (int)min<int64_t>(G, sb.len[sg] - k0) : 0;
+      const int64_t qs = nv[u] > 0 ? qq[u] : 0;
+      const int last = nv[u] > 0 ? nv[u] - 1 : 0;
+#pragma unroll
+      for (int i = 0; i < G; ++i) it[u][i] = ld(qs + min(i, last));
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int i = 0; i < G; ++i) {
+        const int v = slotf(it[u][i]);
+        sl[u][i] = i < nv[u] ? v : -1;
+      }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (nv[u] > 0) {
+        const V bv = sb.bv[ss[u]];
+#pragma unroll
+        for (int i = 0; i < G; ++i)
+          if (sl[u][i] >= 0) acc(sl[u][i], it[u][i], bv, qq[u] + i, base + ss[u]);
       }
     }
   }
@@ -1636,6 +1714,7 @@ constexpr size_t num_heavy_lds() {
 
 template <class SRT, typename V, int LOGT, int NT>
 __global__ void __launch_bounds__(NT) k_num_heavy(const HeavyItem* __restrict__ items,
+                                                  const unsigned long long* __restrict__ nitems,
                                                   const int32_t* __restrict__ hcols, const Unit* __restrict__ units,
                                                   int32_t nsub, DevCsc<V> A, DevCsc<V> B,
                                                   const int2* __restrict__ span, Split spl, NumOut<V> out) {
@@ -1659,7 +1738,9 @@ __global__ void __launch_bounds__(NT) k_num_heavy(const HeavyItem* __restrict__ 
   const SegBuf<V> sb{qb, off, bvs, scr, lens};
   STAMP_DECL
   STAMP(0);
-  const HeavyItem item = items[blockIdx.x];
+  const int64_t nit = (int64_t)*nitems;   // persistent: workgroup b takes items b, b+G, ...
+  for (int64_t ii = blockIdx.x; ii < nit; ii += gridDim.x) {
+  const HeavyItem item = items[ii];
   const int32_t j = hcols[item.h];
   const int2 sp = span[j];
   const int64_t bs = B.cp[j], nb = B.cp[j + 1] - bs;
@@ -1870,18 +1951,25 @@ __global__ void __launch_bounds__(NT) k_num_heavy(const HeavyItem* __restrict__ 
     __syncthreads();
     STAMP(5);
   }
+  }
 }
 
-// ---- heavy numeric with the rows known (symbolic row handoff): one workgroup per item of up to
-// kItemUnits units, every unit of it eligible (heavy_unit_known).  Per unit:
-//   a. its sorted output rows come from the symbolic pass's scratch (UnitRows pieces): written to
-//      C.row (coalesced) and staged in LDS;
-//   b. the rank structure over the unit's span -- for every 64-row pair holding rows: two bitmap words
-//      and the index of its first row -- is built from the rows alone (words of empty pairs are never
-//      read, so nothing span-sized is cleared or scanned);
-//   c. ONE sweep over the multiplies: gather (row, value), slot = pre[pair] + popcounts below the row,
-//      SR::acc at that slot (exact: every gathered row of the unit's range is an output row);
+// ---- heavy numeric with the rows known (symbolic row handoff).  A persistent kernel: workgroup b
+// takes the rows-known units b, b+G, b+2G, ... of one flat list (KnownUnit, built by
+// k_heavy_items_split), keeping the next unit's header and sorted rows in flight while it sweeps the
+// current one.  Per unit:
+//   a. its sorted output rows (symbolic scratch pieces, prefetched into registers) go to C.row; for every 64-row pair holding rows the pair's first row clears the two
+//      bitmap words and records its rank (pre[pair]); the value slots are cleared;
+//   b. every row sets its bit -- words of empty pairs are never read, so nothing span-sized is cleared
+//      or scanned;
+//   c. ONE sweep over the multiplies: gather (row, value), slot = pre[pair] + popcount of the pair word
+//      below the row, SR::acc at that slot (exact: every gathered row of the unit's range is an output
+//      row);
 //   d. the values, already in row order, are written out.
+// rows per thread of k_num_heavy_known (a multi-subwindow unit has at most kUnitCap outputs)
+template <int NT>
+constexpr int known_rpt() { return (int)((kUnitCap + NT - 1) / NT); }
+
 template <class SRT, int LOGT, int NT>
 __device__ __forceinline__ bool heavy_unit_known(const Unit& un, int2 usp, const UnitRows& ur) {
   using Acc = typename SRT::Acc;
@@ -1891,135 +1979,173 @@ __device__ __forceinline__ bool heavy_unit_known(const Unit& un, int2 usp, const
   const int64_t nw = (spn + 31) >> 5;
   const int64_t cpad = (un.cnt + 1) & ~1;
   return !SRT::kAddIsError && CBG_RANK_MODE && ur.np >= 1 && ur.np <= 3 && spn > T && un.cnt <= T &&
-         nw <= 2 * (int64_t)T && cpad * (int64_t)sizeof(Acc) + 4 * (nw + 1) <= kRankBytes;
+         un.cnt <= known_rpt<NT>() * NT && nw <= 2 * (int64_t)T &&
+         cpad * (int64_t)sizeof(Acc) + 4 * (nw + 1) <= kRankBytes;
+}
+
+// everything k_num_heavy_known needs about one unit, in one 80-byte record
+struct KnownUnit {
+  int64_t outoff;       // first output in C
+  int64_t segbase;      // the unit's (unit, B nonzero) segments in Split::useg
+  int64_t bs;           // B.cp[j]
+  int64_t roff[3];      // row pieces in the symbolic row scratch (Split::hrows)
+  int32_t o1, o2;       // ranks where pieces 1 and 2 start (o1 = o2 = cnt: one piece)
+  int32_t cnt, nb;      // outputs; B nonzeros of the column
+  int32_t lo, hi;       // the unit's row range [lo, hi]
+  int32_t pad[2];
+};
+static_assert(sizeof(KnownUnit) == 80, "KnownUnit is 20 words");
+constexpr int kKnownWords = (int)(sizeof(KnownUnit) / 4);
+
+__device__ __forceinline__ int64_t known_row_src(const KnownUnit& H, int i) {
+  return i < H.o1 ? H.roff[0] + i : i < H.o2 ? H.roff[1] + (i - H.o1) : H.roff[2] + (i - H.o2);
 }
 
 #ifndef CBG_UNROLL_KNOWN
-#define CBG_UNROLL_KNOWN 3
+#define CBG_UNROLL_KNOWN 2   // 3 spills at 1024 threads (128 VGPRs)
 #endif
 
 template <class SRT, typename V, int LOGT, int NT, bool AV>
-__global__ void __launch_bounds__(NT) k_num_heavy_known(const HeavyItem* __restrict__ items,
-                                                        const int32_t* __restrict__ hcols,
-                                                        const Unit* __restrict__ units, int32_t nsub, DevCsc<V> A,
-                                                        DevCsc<V> B, const int2* __restrict__ span, Split spl,
-                                                        NumOut<V> out) {
+__global__ void __launch_bounds__(NT) k_num_heavy_known(const KnownUnit* __restrict__ ku,
+                                                        const unsigned long long* __restrict__ nku, DevCsc<V> A,
+                                                        DevCsc<V> B, Split spl, NumOut<V> out) {
   using Acc = typename SRT::Acc;
   constexpr int T = 1 << LOGT;
+  constexpr int RPT = known_rpt<NT>();   // rows per thread (cnt <= RPT*NT)
+  constexpr int NW = NT / kWave;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   int64_t* qb = (int64_t*)smem;                  // NT
   int64_t* off = qb + NT;                        // NT
   int64_t* scr = off + NT;                       // NT/64 + 1
   V* bvs = (V*)(scr + NT / kWave + 1);           // NT
   int32_t* lens = (int32_t*)(bvs + NT);          // NT
-  int* misc = lens + NT;                         // 64 ints
-  Unit* s_units = (Unit*)(misc + 64);            // kItemUnits
-  UnitRows* s_urows = (UnitRows*)(s_units + kItemUnits);   // kItemUnits
-  Acc* vals = (Acc*)(s_urows + kItemUnits);      // (T + NT) * (sizeof(Acc) + 4) bytes: values, then the bitmap
+  KnownUnit* hdr = (KnownUnit*)(lens + NT);      // 2: this unit's and the next unit's header (ring)
+  int32_t* bnd = (int32_t*)(hdr + 2);            // NW*RPT (+1 pad): the last row of every wave, per q
+  Acc* vals = (Acc*)(bnd + ((NW * RPT + 1) & ~1)); // (T + NT) * (sizeof(Acc) + 4) bytes: values, then the bitmap
   uint16_t* pre = (uint16_t*)((char*)vals + (size_t)(T + NT) * (sizeof(Acc) + 4));   // T entries
+  static_assert((NT % 2) == 0, "LDS carve-up must keep 8-byte alignment");
   const SegBuf<V> sb{qb, off, bvs, scr, lens};
+  const int tid = threadIdx.x;
+  const int64_t n = (int64_t)*nku;
+  const int64_t G = gridDim.x;
+  int64_t k = blockIdx.x;
+  if (k >= n) return;   // uniform
   STAMP_DECL
   STAMP(0);
-  const HeavyItem item = items[blockIdx.x];
-  const int32_t j = hcols[item.h];
-  const int2 sp = span[j];
-  const int64_t bs = B.cp[j], nb = B.cp[j + 1] - bs;
-  const int nu = item.u1 - item.u0;
-  if ((int)threadIdx.x < nu) {
-    const int64_t slot = (int64_t)item.h * nsub + item.u0 + threadIdx.x;
-    s_units[threadIdx.x] = units[slot];
-    s_urows[threadIdx.x] = spl.urows[slot];
+  const uint32_t* kw = (const uint32_t*)ku;
+  uint32_t* hw = (uint32_t*)hdr;
+  if (tid < kKnownWords) {
+    hw[tid] = kw[k * kKnownWords + tid];
+    if (k + G < n) hw[kKnownWords + tid] = kw[(k + G) * kKnownWords + tid];
   }
   __syncthreads();
-  auto fetch = [&](int u, int64_t c, int64_t& a0, int64_t& a1, V& bv) {
-    const int64_t i = c + threadIdx.x;
+  int32_t rr[RPT];
+  // rows i = tid + q*NT (coalesced; clamped loads)
+  auto load_rows = [&](const KnownUnit& H) {
+#pragma unroll
+    for (int q = 0; q < RPT; ++q) {
+      const int i = tid + q * NT;
+      rr[q] = spl.hrows[known_row_src(H, i < H.cnt ? i : 0)];
+    }
+  };
+  // every wave's last row per q, for the pair-boundary test of the next wave's first lane
+  const int lane = lane_id(), wv = tid / kWave;
+  auto put_bnd = [&]() {
+    if (lane == kWave - 1) {
+#pragma unroll
+      for (int q = 0; q < RPT; ++q) bnd[wv * RPT + q] = rr[q];
+    }
+  };
+  auto fetch = [&](const KnownUnit& H, int64_t c, int64_t& a0, int64_t& a1, V& bv) {
+    const int64_t i = c + tid;
     a0 = a1 = 0;
     bv = V(0);
-    if (u < nu && i < nb) {
-      const UnitSeg g = spl.useg[s_units[u].segbase + i];
+    if (i < H.nb) {
+      const UnitSeg g = spl.useg[H.segbase + i];
       a0 = g.a0;
       a1 = g.a1;
-      bv = load_val(B.val, bs + i);
+      bv = load_val(B.val, H.bs + i);
     }
   };
   int64_t pa0, pa1;
   V pbv;
-  fetch(0, 0, pa0, pa1, pbv);
-  for (int u = 0; u < nu; ++u) {
-    const Unit un = s_units[u];
-    const UnitRows ur = s_urows[u];
-    const int32_t lo = (int32_t)max((int64_t)sp.x, (int64_t)un.s0 << spl.log);
-    const int32_t hi = (int32_t)min((int64_t)sp.y, ((int64_t)un.s1 << spl.log) - 1);
-    const int cnt = un.cnt;
+  {
+    const KnownUnit H0 = hdr[0];
+    load_rows(H0);
+    fetch(H0, 0, pa0, pa1, pbv);
+    put_bnd();
+    __syncthreads();
+  }
+  for (int slot = 0; k < n; k += G, slot ^= 1) {
+    STAMP(1);
+    const KnownUnit H = hdr[slot];
+    const bool has1 = k + G < n, has2 = k + 2 * G < n;
+    const int32_t lo = __builtin_amdgcn_readfirstlane(H.lo), hi = __builtin_amdgcn_readfirstlane(H.hi);
+    const int32_t cnt = __builtin_amdgcn_readfirstlane(H.cnt);
     const int cpad = (cnt + 1) & ~1;
     uint32_t* bm = (uint32_t*)(vals + cpad);
-    STAMP(1);
-    // a. rows: scratch -> C.row and LDS (staged in the values region); all of a thread's loads are
-    //    issued before any is used (cnt <= T, so at most T/NT per thread)
-    int32_t* urow = (int32_t*)vals;
-    const int64_t o1 = ur.n[0], o2 = o1 + (ur.np > 1 ? ur.n[1] : 0);
-    {
-      constexpr int RPT = (T + NT - 1) / NT;
-      int32_t rr[RPT];
+    // a. value slots cleared; rows -> C.row; the first row of each pair clears the pair, records its rank
+    for (int i = tid; i < cnt; i += NT) vals[i] = SRT::identity();
 #pragma unroll
-      for (int k = 0; k < RPT; ++k) {
-        const int i = threadIdx.x + k * NT;
-        const int ic = i < cnt ? i : 0;
-        const int64_t src = ic < o1 ? ur.off[0] + ic : ic < o2 ? ur.off[1] + (ic - o1) : ur.off[2] + (ic - o2);
-        rr[k] = spl.hrows[src];
-      }
-#pragma unroll
-      for (int k = 0; k < RPT; ++k) {
-        const int i = threadIdx.x + k * NT;
-        if (i < cnt) {
-          out.row[un.outoff + i] = rr[k];
-          urow[i] = rr[k];
+    for (int q = 0; q < RPT; ++q) {
+      const int i = tid + q * NT;
+      const int32_t r = rr[q];
+      const int32_t up = __shfl_up(r, 1, kWave);   // row i-1 within the wave
+      if (i < cnt) {
+        out.row[H.outoff + i] = r;
+        const int pr = (r - lo) >> 6;
+        const int32_t p = lane ? up : (wv ? bnd[(wv - 1) * RPT + q] : (q ? bnd[(NW - 1) * RPT + q - 1] : r));
+        if (i == 0 || ((p - lo) >> 6) != pr) {
+          bm[2 * pr] = 0u;
+          bm[2 * pr + 1] = 0u;
+          pre[pr] = (uint16_t)i;
         }
       }
     }
     __syncthreads();
-    // b. pair words and directory: the first row of a pair clears its two words and records its index,
-    //    then every row sets its bit
-    for (int i = threadIdx.x; i < cnt; i += NT) {
-      const int pr = (urow[i] - lo) >> 6;
-      if (i == 0 || ((urow[i - 1] - lo) >> 6) != pr) {
-        bm[2 * pr] = 0u;
-        bm[2 * pr + 1] = 0u;
-        pre[pr] = (uint16_t)i;
+    uint32_t nh = 0;   // header of unit k+2G, written to this unit's ring slot at the end
+    if (tid < kKnownWords && has2) nh = kw[(k + 2 * G) * kKnownWords + tid];
+    // b. bits
+#pragma unroll
+    for (int q = 0; q < RPT; ++q) {
+      const int i = tid + q * NT;
+      if (i < cnt) {
+        const int o = rr[q] - lo;
+        atomicOr(&bm[o >> 5], 1u << (o & 31));
       }
     }
-    __syncthreads();
-    for (int i = threadIdx.x; i < cnt; i += NT) {
-      const int o = urow[i] - lo;
-      atomicOr(&bm[o >> 5], 1u << (o & 31));
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < cnt; i += NT) vals[i] = SRT::identity();
+    if (has1) load_rows(hdr[slot ^ 1]);   // next unit's rows: in flight during the sweep
     __syncthreads();
     STAMP(2);
     // c. one sweep over the unit's multiplies
-    for (int64_t c = 0; c < nb; c += NT) {
+    const uint64_t* bm2 = (const uint64_t*)bm;
+    for (int64_t c = 0; c < H.nb; c += NT) {
       const int64_t a0 = pa0, a1 = pa1;
       const V bv = pbv;
-      if (c + NT < nb) fetch(u, c + NT, pa0, pa1, pbv);
-      else fetch(u + 1, 0, pa0, pa1, pbv);
+      if (c + NT < H.nb) fetch(H, c + NT, pa0, pa1, pbv);
+      else if (has1) fetch(hdr[slot ^ 1], 0, pa0, pa1, pbv);
       const int64_t F = stage_segments<NT, false, kGroupHeavy, V>(sb, a0, a1, bv);
       STAMP(3);
-      expand_staged<NT, CBG_UNROLL_KNOWN, kGroupHeavy, V>(
-          sb, threadIdx.x, F, bs + c, (int)min<int64_t>(NT, nb - c),
+      expand_staged_slots<NT, CBG_UNROLL_KNOWN, kGroupHeavy, V>(
+          sb, tid, F, H.bs + c, (int)min<int64_t>(NT, H.nb - c),
           [&](int64_t q) { return NumItem<V>{A.ir[q], AV ? A.val[q] : V(1)}; },   // AV: no pointer test per load
-          [&](const NumItem<V>& it, V bv2, int64_t q, int64_t b) {
-            if (it.r < lo || it.r > hi) return;
-            const int o = it.r - lo, w = o >> 5;
-            const int slot = (int)pre[w >> 1] + ((w & 1) ? __popc(bm[w - 1]) : 0) +
-                             __popc(bm[w] & ((1u << (o & 31)) - 1u));
-            SRT::acc(&vals[slot], SRT::mul(it.a, bv2, q, b));
+          [&](const NumItem<V>& it) -> int {
+            const uint32_t o = (uint32_t)(it.r - lo);
+            const bool ok = o <= (uint32_t)(hi - lo);
+            const uint32_t oc = ok ? o : 0u;
+            const int sl = (int)pre[oc >> 6] + __popcll(bm2[oc >> 6] & ((1ull << (oc & 63)) - 1ull));
+            return ok ? sl : -1;
+          },
+          [&](int sl, const NumItem<V>& it, V bv2, int64_t q, int64_t b) {
+            SRT::acc(&vals[sl], SRT::mul(it.a, bv2, q, b));
           });
       __syncthreads();
       STAMP(4);
     }
     // d. values out, row order
-    for (int i = threadIdx.x; i < cnt; i += NT) out.val[un.outoff + i] = SRT::out(vals[i], A.val, B.val);
+    for (int i = tid; i < cnt; i += NT) out.val[H.outoff + i] = SRT::out(vals[i], A.val, B.val);
+    if (tid < kKnownWords && has2) hw[slot * kKnownWords + tid] = nh;
+    if (has1) put_bnd();
     __syncthreads();
     STAMP(5);
   }
@@ -2027,32 +2153,30 @@ __global__ void __launch_bounds__(NT) k_num_heavy_known(const HeavyItem* __restr
 
 template <class SRT, typename V, int LOGT, int NT>
 constexpr size_t num_heavy_known_lds() {
-  return (size_t)NT * (8 + 8 + sizeof(V) + 4) + (size_t)(NT / kWave + 1) * 8 + 64 * 4 +
-         kItemUnits * (sizeof(Unit) + sizeof(UnitRows)) + (size_t)((1 << LOGT) + NT) * (sizeof(typename SRT::Acc) + 4) +
-         (size_t)(1 << LOGT) * 2;
+  return (size_t)NT * (8 + 8 + sizeof(V) + 4) + (size_t)(NT / kWave + 1) * 8 + 2 * sizeof(KnownUnit) +
+         (size_t)(((NT / kWave) * known_rpt<NT>() + 1) & ~1) * 4 +
+         (size_t)((1 << LOGT) + NT) * (sizeof(typename SRT::Acc) + 4) + (size_t)(1 << LOGT) * 2;
 }
 
-// Items of every heavy column: ceil(nunits / kItemUnits) consecutive unit groups, split into the
-// rows-known list (every unit eligible for k_num_heavy_known) and the rest (k_num_heavy); the two
-// counts go to counts[0], counts[1].
+// Every heavy column's units -> the rows-known list (one KnownUnit per eligible unit, for
+// k_num_heavy_known) and items for k_num_heavy (runs of consecutive other units, <= kItemUnits per
+// item); list lengths -> counts[0], counts[1].  Runs after k_unit_segs (segbase).
 template <class SRT, int LOGT, int NT>
-__global__ void k_heavy_items_split(int H, const int32_t* __restrict__ nunits, const Unit* __restrict__ units,
-                                    int32_t nsub, const int2* __restrict__ uspan, const UnitRows* __restrict__ urows,
-                                    HeavyItem* __restrict__ kitems, HeavyItem* __restrict__ oitems,
+__global__ void k_heavy_items_split(int H, const int32_t* __restrict__ cols, const int32_t* __restrict__ nunits,
+                                    const Unit* __restrict__ units, int32_t nsub, const int2* __restrict__ uspan,
+                                    const UnitRows* __restrict__ urows, const int64_t* __restrict__ Bcp,
+                                    KnownUnit* __restrict__ known, HeavyItem* __restrict__ oitems,
                                     unsigned long long* __restrict__ counts) {
   const int h = blockIdx.x * blockDim.x + threadIdx.x;
   const int nu = h < H ? nunits[h] : 0;
-  // pass 1: this column's item kinds (bit i of kmask: item i is rows-known); pass 2: write
-  uint64_t kmask = 0;
+  auto is_known = [&](int u) {
+    const int64_t slot = (int64_t)h * nsub + u;
+    return urows != nullptr && heavy_unit_known<SRT, LOGT, NT>(units[slot], uspan[slot], urows[slot]);
+  };
   int nk = 0, no = 0;
-  for (int u = 0, i = 0; u < nu; u += kItemUnits, ++i) {
-    const int u1 = min(nu, u + kItemUnits);
-    bool known = urows != nullptr && i < 64;
-    for (int k = u; k < u1 && known; ++k) {
-      const int64_t slot = (int64_t)h * nsub + k;
-      known = heavy_unit_known<SRT, LOGT, NT>(units[slot], uspan[slot], urows[slot]);
-    }
-    if (known) { kmask |= 1ull << i; ++nk; } else ++no;
+  for (int u = 0, run = 0; u < nu; ++u) {
+    if (is_known(u)) { ++nk; run = 0; }
+    else { if (run == 0) ++no; if (++run == kItemUnits) run = 0; }
   }
   // one atomic per wave and list (a single counter hit by every column serialises at the L2)
   const int ik = wave_incl_scan(nk), io = wave_incl_scan(no);
@@ -2063,11 +2187,39 @@ __global__ void k_heavy_items_split(int H, const int32_t* __restrict__ nunits, c
   }
   bk = __shfl(bk, kWave - 1, kWave) + (ik - nk);
   bo = __shfl(bo, kWave - 1, kWave) + (io - no);
-  for (int u = 0, i = 0; u < nu; u += kItemUnits, ++i) {
-    const HeavyItem it{h, u, min(nu, u + kItemUnits), 0};
-    if (i < 64 && ((kmask >> i) & 1)) kitems[bk++] = it;
-    else oitems[bo++] = it;
+  if (nu == 0) return;
+  const int32_t j = cols[h];
+  const int64_t bs = Bcp[j];
+  const int32_t nb = (int32_t)(Bcp[j + 1] - bs);
+  int u0 = -1;
+  for (int u = 0; u < nu; ++u) {
+    if (is_known(u)) {
+      if (u0 >= 0) { oitems[bo++] = HeavyItem{h, u0, u, 0}; u0 = -1; }
+      const int64_t slot = (int64_t)h * nsub + u;
+      const Unit un = units[slot];
+      const UnitRows ur = urows[slot];
+      const int2 sp = uspan[slot];
+      KnownUnit K;
+      K.outoff = un.outoff;
+      K.segbase = un.segbase;
+      K.bs = bs;
+      K.roff[0] = ur.off[0];
+      K.roff[1] = ur.np > 1 ? ur.off[1] : 0;
+      K.roff[2] = ur.np > 2 ? ur.off[2] : 0;
+      K.o1 = ur.np > 1 ? ur.n[0] : un.cnt;
+      K.o2 = ur.np > 2 ? ur.n[0] + ur.n[1] : un.cnt;
+      K.cnt = un.cnt;
+      K.nb = nb;
+      K.lo = sp.x;
+      K.hi = sp.y;
+      K.pad[0] = K.pad[1] = 0;
+      known[bk++] = K;
+    } else {
+      if (u0 < 0) u0 = u;
+      if (u + 1 - u0 == kItemUnits) { oitems[bo++] = HeavyItem{h, u0, u + 1, 0}; u0 = -1; }
+    }
   }
+  if (u0 >= 0) oitems[bo++] = HeavyItem{h, u0, nu, 0};
 }
 
 // items of every heavy column: ceil(nunits / kItemUnits) consecutive unit groups

@@ -113,7 +113,7 @@ typedef struct {
   double flops_ms, bin_ms, symbolic_ms, scan_ms, numeric_ms, total_ms;
   int64_t multiplies, nnz_out, bins[16];
   double heavy_ms;      /* k_num_heavy_known + k_num_heavy (heavy-column units), HIP events on the context stream */
-  int64_t known_items;  /* heavy items whose rows came from the symbolic pass (k_num_heavy_known) */
+  int64_t known_items;  /* heavy units whose rows came from the symbolic pass (k_num_heavy_known) */
 } cbg_profile;
 
 int32_t     cbg_abi_version(void);

@@ -39,6 +39,7 @@ def main():
     C = (A @ A[:, pick]).tocsc()
     C.sort_indices()
     tot = dict(mult=0, gathered=0, segs=0, nonempty=0, units=0, chunks=0, nnzc=0, heavy=0, nb=0)
+    hist = np.zeros(66, np.int64)   # nonempty segment lengths (64+ pooled in the last bin)
     first = np.where(alen > 0, ir[np.minimum(cp[:-1], len(ir) - 1)], 0)
     last = np.where(alen > 0, ir[np.maximum(cp[1:] - 1, 0)], -1)
     for t, j in enumerate(pick):
@@ -75,10 +76,12 @@ def main():
                 g = a_hi - a_lo
                 tot["gathered"] += int(g.sum())
                 tot["nonempty"] += int((g > 0).sum())
+                hist += np.bincount(np.minimum(g[g > 0], 65), minlength=66)
             sk = ks[~longk]
             hit = (last[sk] >= r0) & (first[sk] < r1) & (alen[sk] > 0)
             tot["gathered"] += int(alen[sk][hit].sum())
             tot["nonempty"] += int(hit.sum())
+            hist += np.bincount(np.minimum(alen[sk][hit], 65), minlength=66)
             tot["segs"] += nb
     h = tot["heavy"]
     print(f"scale {scale}: {len(cand)} flop-heavy candidate columns, sampled {len(pick)}, heavy {h}")
@@ -87,6 +90,11 @@ def main():
     print(f"  gathered / useful multiplies = {tot['gathered'] / max(tot['mult'], 1):.3f}")
     print(f"  staged segments / multiply   = {tot['segs'] / max(tot['mult'], 1):.3f}   "
           f"nonempty / staged = {tot['nonempty'] / max(tot['segs'], 1):.3f}")
+    L = np.arange(66)
+    print("  nonempty segment lengths:", {int(l): round(float(hist[l] / max(hist.sum(), 1)), 4) for l in L if hist[l]})
+    for G in (1, 2, 4, 8):
+        groups = int((hist * ((L + G - 1) // G)).sum())
+        print(f"  G={G}: groups {groups}, gathered/group {tot['gathered'] / max(groups, 1):.2f} (fill {tot['gathered'] / max(groups * G, 1):.2f})")
     print(f"  multiplies per unit = {tot['mult'] / max(tot['units'], 1):.0f}, outputs per unit = "
           f"{tot['nnzc'] / max(tot['units'], 1):.0f}, chunks per unit = {tot['chunks'] / max(tot['units'], 1):.2f}")
 
