@@ -40,8 +40,20 @@ namespace {  // internal linkage: every translation unit instantiates its own ke
 constexpr int kWave = 64;
 constexpr int32_t kEmpty = -1;
 constexpr int kLong = 64;          // k_window: segment length handed to a whole wavefront
-constexpr int kUnroll = 2;         // groups of G multiplies in flight per lane (numeric)
-constexpr int kUnrollSym = 2;      // same, symbolic (4-byte items)
+#ifndef CBG_UNROLL_NUM
+#define CBG_UNROLL_NUM 2
+#endif
+#ifndef CBG_UNROLL_SYM
+#define CBG_UNROLL_SYM 2
+#endif
+#ifndef CBG_GROUP_SYM
+#define CBG_GROUP_SYM 4
+#endif
+#ifndef CBG_GROUP_NUM
+#define CBG_GROUP_NUM 2
+#endif
+constexpr int kUnroll = CBG_UNROLL_NUM;       // groups of G multiplies in flight per lane (numeric)
+constexpr int kUnrollSym = CBG_UNROLL_SYM;    // same, symbolic (4-byte items)
 #ifndef CBG_UNROLL_HEAVY
 #define CBG_UNROLL_HEAVY 1
 #endif
@@ -49,8 +61,8 @@ constexpr int kUnrollSym = 2;      // same, symbolic (4-byte items)
 #define CBG_GROUP_HEAVY 4
 #endif
 constexpr int kUnrollHeavy = CBG_UNROLL_HEAVY;    // same, k_num_heavy
-constexpr int kGroupSym = 4;       // consecutive A entries per lane group (one segment search each), symbolic
-constexpr int kGroupNum = 2;       // same, numeric
+constexpr int kGroupSym = CBG_GROUP_SYM;  // consecutive A entries per lane group (one segment search each), symbolic
+constexpr int kGroupNum = CBG_GROUP_NUM;  // same, numeric
 constexpr int kGroupHeavy = CBG_GROUP_HEAVY;     // same, k_num_heavy
 constexpr int64_t kHeavy = 4096;   // nnz(C(:,j)) above which a column is split into units
 // k_num_heavy geometry: table 2^CBG_HEAVY_LOGT slots, CBG_HEAVY_NT threads (LDS decides WGs per CU)
@@ -395,6 +407,9 @@ __device__ __forceinline__ int64_t block_excl_scan64(int64_t v, int64_t* scratch
   return scratch[w] + inc - v;
 }
 
+// s_waitcnt vmcnt(0) (expcnt/lgkmcnt left at their maxima; gfx9 encoding)
+__device__ __forceinline__ void wait_vmem_all() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+
 // last s in [0, P) with off[s] <= m (off non-decreasing, off[0] = 0 <= m): the non-empty segment
 // holding flat multiply m.  P is a power of two covering the staged segments (P <= NT).
 template <int NT>
@@ -542,6 +557,9 @@ __device__ __forceinline__ void expand_staged_slots(const SegBuf<V>& sb, int tid
           if (sl[u][i] >= 0) acc(sl[u][i], it[u][i], bv, qq[u] + i, base + ss[u]);
       }
     }
+    // the gathers of a skipped accumulation were never waited on: drain them here, so the next round
+    // (and a loop entered with prefetches in flight) does not start with a full memory-counter wait
+    wait_vmem_all();
   }
 }
 
@@ -960,6 +978,8 @@ __global__ void __launch_bounds__(NT) k_sym_part(const PartItem* __restrict__ it
   uint8_t* bvs = (uint8_t*)(lens + NT);            // NT
   const SegBuf<uint8_t> sb{qb, off, bvs, scr, lens};
   const int count = *count_dev;
+  STAMP_DECL
+  STAMP(31);
   for (int i = blockIdx.x; i < count; i += gridDim.x) {
     const PartItem it = items[i];
     const int2 sp = span[it.j];
@@ -970,6 +990,7 @@ __global__ void __launch_bounds__(NT) k_sym_part(const PartItem* __restrict__ it
     if (threadIdx.x < s1 - s0) scnt[threadIdx.x] = 0;
     if (threadIdx.x == 0) misc[0] = 0;
     __syncthreads();
+    STAMP(26);
     for_each_multiply<NT, false, kUnrollSym, kGroupSym, uint8_t>(
         Bcp[it.j], Bcp[it.j + 1], sb,
         [&](int64_t b, int64_t& a0, int64_t& a1, uint8_t&) {
@@ -993,6 +1014,7 @@ __global__ void __launch_bounds__(NT) k_sym_part(const PartItem* __restrict__ it
           }
         });
     __syncthreads();
+    STAMP(27);
     int c = 0;
     uint32_t wds[WPT];
 #pragma unroll
@@ -1015,6 +1037,7 @@ __global__ void __launch_bounds__(NT) k_sym_part(const PartItem* __restrict__ it
       misc[5] = (int)(off >> 32);
     }
     __syncthreads();
+    STAMP(28);
     const int64_t off = (int64_t)(uint32_t)misc[4] | ((int64_t)misc[5] << 32);
     if (off >= 0) {   // this part's sorted rows for the numeric pass (each thread: its words' rows)
       int64_t pos = off + ex;
@@ -1033,6 +1056,7 @@ __global__ void __launch_bounds__(NT) k_sym_part(const PartItem* __restrict__ it
     int32_t* dst = ho.sub + (int64_t)it.h * ho.nsub;
     for (int s = sf + (int)threadIdx.x; s <= sl; s += NT) dst[s] = scnt[s - s0];
     __syncthreads();
+    STAMP(29);
   }
 }
 
@@ -2001,8 +2025,13 @@ __device__ __forceinline__ int64_t known_row_src(const KnownUnit& H, int i) {
   return i < H.o1 ? H.roff[0] + i : i < H.o2 ? H.roff[1] + (i - H.o1) : H.roff[2] + (i - H.o2);
 }
 
+// k_num_heavy_known: groups of CBG_GROUP_KNOWN entries, CBG_UNROLL_KNOWN groups in flight per lane
+// (s20 f64: G=2/U=4 32.4 ms, G=4/U=2 34.5, G=1/U=8 38.1, G=8/U=1 41.4; G=4/U=3 spills)
 #ifndef CBG_UNROLL_KNOWN
-#define CBG_UNROLL_KNOWN 2   // 3 spills at 1024 threads (128 VGPRs)
+#define CBG_UNROLL_KNOWN 4
+#endif
+#ifndef CBG_GROUP_KNOWN
+#define CBG_GROUP_KNOWN 2
 #endif
 
 template <class SRT, typename V, int LOGT, int NT, bool AV>
@@ -2124,9 +2153,9 @@ __global__ void __launch_bounds__(NT) k_num_heavy_known(const KnownUnit* __restr
       const V bv = pbv;
       if (c + NT < H.nb) fetch(H, c + NT, pa0, pa1, pbv);
       else if (has1) fetch(hdr[slot ^ 1], 0, pa0, pa1, pbv);
-      const int64_t F = stage_segments<NT, false, kGroupHeavy, V>(sb, a0, a1, bv);
+      const int64_t F = stage_segments<NT, false, CBG_GROUP_KNOWN, V>(sb, a0, a1, bv);
       STAMP(3);
-      expand_staged_slots<NT, CBG_UNROLL_KNOWN, kGroupHeavy, V>(
+      expand_staged_slots<NT, CBG_UNROLL_KNOWN, CBG_GROUP_KNOWN, V>(
           sb, tid, F, H.bs + c, (int)min<int64_t>(NT, H.nb - c),
           [&](int64_t q) { return NumItem<V>{A.ir[q], AV ? A.val[q] : V(1)}; },   // AV: no pointer test per load
           [&](const NumItem<V>& it) -> int {

@@ -32,5 +32,6 @@ for i, nm in ((15, "  home count atomics+sync"), (16, "  scan+rewrite+sync"), (1
 print("runs", s[19], "keys in runs", s[20], "max run", s[21], "sum L^2", s[22])
 print(f"rank single-chunk: sweep 1 (rows + marks) {s[24]} cycles, directory {s[25]} cycles "
       f"(phase 4 'expand' = sweep 2 for those units)")
+print("k_sym_part: clear", s[26], "expand", s[27], "count+scan", s[28], "rows+subwindow counts", s[29])
 print("units", s[10], "chunks", s[11], "multiplies", s[12], "hash units", s[13])
 print("profile", {k: prof[k] for k in ("numeric_ms", "symbolic_ms", "total_ms")})

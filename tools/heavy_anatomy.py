@@ -40,6 +40,7 @@ def main():
     C.sort_indices()
     tot = dict(mult=0, gathered=0, segs=0, nonempty=0, units=0, chunks=0, nnzc=0, heavy=0, nb=0)
     hist = np.zeros(66, np.int64)   # nonempty segment lengths (64+ pooled in the last bin)
+    dens = np.zeros(12)             # multiplies of units by span/cnt ratio bucket (log2)
     first = np.where(alen > 0, ir[np.minimum(cp[:-1], len(ir) - 1)], 0)
     last = np.where(alen > 0, ir[np.maximum(cp[1:] - 1, 0)], -1)
     for t, j in enumerate(pick):
@@ -67,6 +68,9 @@ def main():
         tot["chunks"] += len(units) * ((nb + NT - 1) // NT)
         for (s0, s1) in units:
             r0, r1 = s0 << slog, s1 << slog
+            ucnt = int(((rows >= r0) & (rows < r1)).sum())
+            ulo, uhi = max(r0, int(rows[0])), min(r1 - 1, int(rows[-1]))
+            umult = 0
             longk = alen[ks] >= SPLIT_MIN
             # long columns: exact pieces
             lk = ks[longk]
@@ -75,6 +79,7 @@ def main():
                 a_hi = np.array([np.searchsorted(ir[cp[k]:cp[k + 1]], r1) for k in lk])
                 g = a_hi - a_lo
                 tot["gathered"] += int(g.sum())
+                umult += int(g.sum())
                 tot["nonempty"] += int((g > 0).sum())
                 hist += np.bincount(np.minimum(g[g > 0], 65), minlength=66)
             sk = ks[~longk]
@@ -83,6 +88,8 @@ def main():
             tot["nonempty"] += int(hit.sum())
             hist += np.bincount(np.minimum(alen[sk][hit], 65), minlength=66)
             tot["segs"] += nb
+            if ucnt > 0:
+                dens[min(11, int(np.log2(max(1.0, (uhi - ulo + 1) / ucnt))))] += umult
     h = tot["heavy"]
     print(f"scale {scale}: {len(cand)} flop-heavy candidate columns, sampled {len(pick)}, heavy {h}")
     for k, v in tot.items():
@@ -90,6 +97,7 @@ def main():
     print(f"  gathered / useful multiplies = {tot['gathered'] / max(tot['mult'], 1):.3f}")
     print(f"  staged segments / multiply   = {tot['segs'] / max(tot['mult'], 1):.3f}   "
           f"nonempty / staged = {tot['nonempty'] / max(tot['segs'], 1):.3f}")
+    print("  multiplies by unit span/cnt (log2 bucket):", [round(float(x / max(dens.sum(), 1)), 3) for x in dens])
     L = np.arange(66)
     print("  nonempty segment lengths:", {int(l): round(float(hist[l] / max(hist.sum(), 1)), 4) for l in L if hist[l]})
     for G in (1, 2, 4, 8):
