@@ -15,8 +15,9 @@ with row-sorted output; for N > 1 also the stage broadcasts, partial merges and 
 K steps are timed between a barrier + device synchronisation on both sides, max over ranks; value =
 all ranks' multiplies / that time.
 
-Rank 0 prints ONE JSON line.  N = 1 adds `roofline` for the dominant kernel (k_num_heavy: the
-heavy-column units, timed with HIP events on the library stream; algorithmic bytes per SURVEY §8d)
+Rank 0 prints ONE JSON line.  N = 1 adds `roofline` for the dominant phase (the heavy-column units:
+k_num_heavy_known, plus k_num_heavy for the few units it does not take, bracketed by HIP events on the
+library stream; algorithmic bytes per SURVEY §8d)
 and `cpu_baseline` (the oracle CPU restatement on a bounded sample of the same product).
 """
 import argparse
@@ -45,14 +46,14 @@ def balg_bytes(mults, nnzc, nnzb, ncolb):
 
 
 def heavy_bytes(flop_col, nnz_c_col, nnz_b_col, heavy):
-    """SURVEY §8(d) numeric-phase algorithmic bytes of the heavy columns (what k_num_heavy processes):
+    """SURVEY §8(d) numeric-phase algorithmic bytes of the heavy columns (what the heavy kernels process):
     gather A (row, val) per multiply, read B (row, val) + the A colptr pair per B nonzero, write C."""
     return (int(flop_col[heavy].sum()) * (S_I + S_V) + int(nnz_b_col[heavy].sum()) * (S_I + S_V + 2 * S_P)
             + int(nnz_c_col[heavy].sum()) * (S_I + S_V))
 
 
 def load_traffic(scale, edgefactor):
-    """HBM bytes per k_num_heavy launch from the newest committed rocprofv3 PMC summary for this
+    """HBM bytes per product of the heavy kernels from the newest committed rocprofv3 PMC summary for this
     workload (profiles/*_pmc_heavy.json, written by tools/pmc_heavy.py), or (None, None)."""
     best = None
     for f in sorted(glob.glob(os.path.join(HERE, "profiles", "*_pmc_heavy.json"))):
@@ -183,7 +184,7 @@ def bench_local(args):
                       for k in ("flops_ms", "bin_ms", "symbolic_ms", "scan_ms", "numeric_ms", "heavy_ms",
                                 "total_ms")},
         "heavy_items": {"items": int(profs[-1]["bins"][13]), "rows_known_units": int(profs[-1]["known_items"])},
-        "roofline": {"bound": "hbm", "kernel": "k_num_heavy", "achieved": achieved, "peak": HBM_PEAK_GBS,
+        "roofline": {"bound": "hbm", "kernel": "k_num_heavy_known + k_num_heavy (heavy-column units)", "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "traffic_source": tsrc, "algorithmic_bytes_per_launch": hb, "avg_launch_ms": heavy_ms,
                      "heavy_columns": int(heavy.sum()), "heavy_multiplies": int(flop_col[heavy].sum()),

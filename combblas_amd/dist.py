@@ -562,6 +562,114 @@ def SpAsgn(A, ri, ci, B):
     A.block = be.merge([A.block, RBQ.block], pt) if RBQ.block.nnz else A.block
 
 
+# ------------------------------------------------------------------------------- block products
+def _block_offsets(n, b):
+    """BlockSpGEMM::getBlockOffsets / BlockSplit sizes (BlockSpGEMM.h:107-130, SpParMat.cpp:2943-2953):
+    b blocks of n // b, the first n % b of them one larger (unlike the SpParMat distribution, which
+    gives the remainder to the last block)."""
+    sz, r = divmod(int(n), int(b))
+    return [min(i, r) * (sz + 1) + (0 if i < r else i - r) * sz for i in range(b)] + [int(n)]
+
+
+def BlockSplit(A, br, bc):
+    """SpParMat::BlockSplit (SpParMat.cpp:2915-3000): the br x bc grid of sub-matrices of A, each a
+    matrix of its own on A's process grid (block distribution of the sub-matrix's dimensions).  The
+    reference routes tuples with an all-to-all (SparseCommon, no duplicates); here each block is
+    A(rows, cols) through the SpGEMM selection of SubsRef_SR (exact for every value type: v * 1).
+    br == bc == 1, or more blocks than rows / columns, returns [[A]] as the reference does."""
+    if (br == 1 and bc == 1) or br > A.nrow or bc > A.ncol:
+        return [[A]]
+    if A.grid.L != 1:
+        raise ValueError("BlockSplit: SpParMat (one-layer grid) only")
+    ro, co = _block_offsets(A.nrow, br), _block_offsets(A.ncol, bc)
+    out = []
+    for i in range(br):
+        rows = np.arange(ro[i], ro[i + 1], dtype=np.int64)
+        Ai = A if br == 1 else SubsRef_SR_dim(A, rows, "row")
+        out.append([Ai if bc == 1 else SubsRef_SR_dim(Ai, np.arange(co[j], co[j + 1], dtype=np.int64), "column")
+                    for j in range(bc)])
+    return out
+
+
+class BlockSpGEMM:
+    """C = A * B one output block at a time (BlockSpGEMM.h:14-130): A is split into br row blocks, B
+    into bc column blocks (bi = 1: the inner dimension is not split, as the reference's getNextBlock
+    asserts), and block (i, j) = Mult_AnXBn_DoubleBuff(A_i, B_j).  Python returns (C_ij, roffset,
+    coffset) where the reference fills the two offsets by reference."""
+
+    def __init__(self, A, B, br, bc, bi=1):
+        self.br, self.bc, self.bi, self.cur = int(br), int(bc), int(bi), 0
+        self.A_blocks = BlockSplit(A, self.br, self.bi)
+        self.B_blocks = BlockSplit(B, self.bi, self.bc)
+        self.nr, self.nc = A.nrow, B.ncol
+
+    def _offsets(self, rbid, cbid):
+        return _block_offsets(self.nr, self.br)[rbid], _block_offsets(self.nc, self.bc)[cbid]
+
+    def getBlockId(self, SR, rbid, cbid):
+        if self.bi != 1:
+            raise ValueError("BlockSpGEMM: bi must be 1 (BlockSpGEMM.h:55)")
+        if rbid >= len(self.A_blocks) or cbid >= len(self.B_blocks[0]):
+            raise IndexError("BlockSpGEMM: more blocks than rows/columns (BlockSplit returned the whole matrix)")
+        ro, co = self._offsets(rbid, cbid)
+        return Mult_AnXBn_DoubleBuff(SR, self.A_blocks[rbid][0], self.B_blocks[0][cbid]), ro, co
+
+    def getNextBlock(self, SR):
+        rbid, cbid = divmod(self.cur, self.bc)
+        self.cur += 1
+        return self.getBlockId(SR, rbid, cbid)
+
+    def hasNext(self):
+        return self.cur < self.br * self.bc
+
+    def getBlockOffsets(self, is_row):
+        return _block_offsets(self.nr, self.br) if is_row else _block_offsets(self.nc, self.bc)
+
+
+def Convert2D(A):
+    """SpParMat3D::Convert2D, non-special layout (SpParMat3D.cpp:496-564): every local entry's global
+    (row, col) (the layer-part offsets of the colsplit / rowsplit piece) is routed to its owner on the
+    2D grid over all ranks, CommGrid(world, 0, 0) -- a square sqrt(p) x sqrt(p) grid (the reference's
+    CommGrid aborts otherwise) -- with one all-to-all; the received entries form the local CSC."""
+    g, be = A.grid, A.backend
+    s = int(round(g.world ** 0.5))
+    if s * s != g.world:
+        raise ValueError(f"Convert2D: {g.world} processes do not form a square 2D grid (CommGrid.cpp:44-50)")
+    g2 = CommGrid(s, s)
+    (r0, r1), (c0, c1) = A.local_range()
+    b = A.block
+    dev, cd = be.device, be.comm_device
+    col = torch.repeat_interleave(torch.arange(b.ncol, device=dev, dtype=torch.int64), torch.diff(b.cp)) + c0
+    row = b.ir.to(torch.int64) + r0
+    rstep, cstep = max(A.nrow // s, 1), max(A.ncol // s, 1)
+    oi = torch.clamp(row // rstep, max=s - 1)   # SpParMat::Owner: last block takes the remainder
+    oj = torch.clamp(col // cstep, max=s - 1)
+    owner = oi * s + oj
+    order = torch.argsort(owner, stable=True)
+    send_n = torch.bincount(owner, minlength=g.world)
+    sn = [int(x) for x in send_n.cpu().tolist()]
+    recv_n = torch.empty(g.world, dtype=torch.int64, device=cd)
+    dist.all_to_all_single(recv_n, _to_comm(send_n, be))
+    rn = [int(x) for x in recv_n.cpu().tolist()]
+    lr = (row - oi * rstep)[order]
+    lc = (col - oj * cstep)[order]
+    tot = sum(rn)
+    r_r = torch.empty(tot, dtype=torch.int64, device=cd)
+    r_c = torch.empty(tot, dtype=torch.int64, device=cd)
+    r_v = torch.empty(tot, dtype=be.val_dtype, device=cd)
+    dist.all_to_all_single(r_r, _to_comm(lr, be), rn, sn)
+    dist.all_to_all_single(r_c, _to_comm(lc, be), rn, sn)
+    dist.all_to_all_single(r_v, _to_comm(b.val[order], be), rn, sn)
+    r_r, r_c, r_v = _from_comm(r_r, be), _from_comm(r_c, be), _from_comm(r_v, be)
+    (q0, q1), (p0, p1) = block_range(A.nrow, s, g2.row), block_range(A.ncol, s, g2.col)
+    nr, nc = q1 - q0, p1 - p0
+    key = r_c * max(nr, 1) + r_r
+    o = torch.argsort(key)
+    cp = torch.zeros(nc + 1, dtype=torch.int64, device=dev)
+    torch.cumsum(torch.bincount(r_c, minlength=nc), 0, out=cp[1:])
+    return SpParMat3D(g2, A.nrow, A.ncol, Block(nr, nc, cp, r_r[o].to(torch.int32), r_v[o]), True, be)
+
+
 # ------------------------------------------------------------------------------ HipMCL expansion
 def _col_slice(b, c0, c1):
     """Columns [c0, c1) of a Block (one ColSplit piece, SpDCCols.cpp:927-1086)."""

@@ -356,3 +356,55 @@ def run_fixture_case(rank, world, port, backend_kind, cases, errq):
         import traceback
         errq.put(f"rank {rank}: {e!r}\n{traceback.format_exc()}")
         raise
+
+
+def run_block_case(rank, world, port, backend_kind, cases, errq):
+    """Per-rank body of BlockSpGEMM / BlockSplit (BlockSpGEMM.h:14-130, SpParMat.cpp:2915-3000) and
+    SpParMat3D::Convert2D (SpParMat3D.cpp:441-566) on the reference's G500 s10 fixture: every output
+    block of A*A against the same block of the reference-built golden product, every BlockSplit piece
+    against the slice of A, and Convert2D of colsplit / rowsplit 3D layouts against the 2D blocks."""
+    try:
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        import combblas_amd as cb
+        be = cbd.GpuBackend(cb.Context(0)) if backend_kind == "gpu" else ScipyBackend()
+        from helpers import fixture_inputs, fixture_product, load_fixture
+        q = int(round(world ** 0.5))
+        grid = cbd.CommGrid(q, q)
+        z = load_fixture("g500_s10")
+        A, B, sr, dt = fixture_inputs(z, "pt_f64_hash")
+        R = fixture_product(z, "pt_f64_hash")
+        As = sp.csc_matrix((A.val, A.ir, A.cp), shape=(A.nrow, A.ncol))
+        Rs = sp.csc_matrix((R.val, R.ir, R.cp), shape=(A.nrow, B.ncol))
+        SR = cb.PlusTimesSRing("f64")
+
+        def dmat(M, colsplit=True, g=grid):
+            return cbd.SpParMat3D.from_global_csc(g, M.shape[0], M.shape[1], M.indptr, M.indices, M.data, colsplit, be)
+        for (br, bc) in cases:
+            bs = cbd.BlockSpGEMM(dmat(As), dmat(As), br, bc)
+            ro, co = bs.getBlockOffsets(True), bs.getBlockOffsets(False)
+            assert ro[0] == 0 and ro[-1] == A.nrow and co[-1] == A.ncol and len(ro) == br + 1
+            seen = 0
+            while bs.hasNext():
+                C, r0, c0 = bs.getNextBlock(SR)
+                i, j = divmod(seen, bc)
+                assert (r0, c0) == (ro[i], co[j]), (r0, c0, ro[i], co[j])
+                _check_piece(C, Rs[ro[i]:ro[i + 1], co[j]:co[j + 1]], rank, f"BlockSpGEMM {br}x{bc} ({i},{j})")
+                seen += 1
+            assert seen == br * bc
+            for i, row in enumerate(bs.A_blocks):
+                _check_piece(row[0], As[ro[i]:ro[i + 1], :], rank, f"BlockSplit A {i}")
+            C, r0, c0 = bs.getBlockId(SR, br - 1, bc - 1)
+            _check_piece(C, Rs[ro[-2]:, co[-2]:], rank, "BlockSpGEMM getBlockId")
+        for (L, qq) in ((world, 1), (1, q)):
+            g3 = cbd.CommGrid3D(L, qq, qq)
+            for colsplit in (True, False):
+                M2 = cbd.Convert2D(dmat(Rs, colsplit, g3))
+                _check_piece(M2, Rs, rank, f"Convert2D {L}x{qq}x{qq} colsplit={colsplit}")
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:
+        import traceback
+        errq.put(f"rank {rank}: {e!r}\n{traceback.format_exc()}")
+        raise

@@ -35,3 +35,13 @@ def test_2d_drivers_and_indexing_gloo_cpu(world, port):
     2x2 grids (SpParMat.cpp:2028-2562, ParFriends.h:799-1235) against scipy on the global matrices."""
     from dist_support import run_index_case
     spawn_case(world, "scipy", INDEX_CASES, port, body=run_index_case)
+
+
+BLOCK_CASES = [(2, 3), (3, 1), (1, 1)]
+
+
+@pytest.mark.parametrize("world,port", [(1, 29619), (4, 29620)])
+def test_block_spgemm_and_convert2d_gloo_cpu(world, port):
+    """BlockSpGEMM / BlockSplit and SpParMat3D::Convert2D on the reference's G500 s10 fixture product."""
+    from dist_support import run_block_case
+    spawn_case(world, "scipy", BLOCK_CASES, port, body=run_block_case)

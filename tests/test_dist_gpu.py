@@ -50,6 +50,13 @@ def test_reference_fixtures_through_layouts_gloo_gpu(world, port):
     spawn_case(world, "gpu", FIXTURE_CASES, port, body=run_fixture_case)
 
 
+@pytest.mark.parametrize("world,port", [(4, 29635)])
+def test_block_spgemm_and_convert2d_gloo_gpu(world, port):
+    """BlockSpGEMM (DoubleBuff block products through libcbgpu) and Convert2D on the G500 s10 fixture."""
+    from dist_support import run_block_case
+    spawn_case(world, "gpu", [(2, 3), (3, 1)], port, body=run_block_case)
+
+
 def test_rccl_native_grid_single_rank():
     """libcbgpu's RCCL path (cbg_rccl_unique_id, ncclCommInitRank, ncclCommSplit of row/col/fiber
     communicators) on a one-rank nccl process group: the only RCCL shape one GPU can host (RCCL refuses

@@ -50,11 +50,19 @@ def main():
     ap.add_argument("--mcl-n", type=int, default=1 << 18)
     ap.add_argument("--poisson-k", type=int, default=128)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--only", type=int, default=0, help="run only config 4 or 5")
     args = ap.parse_args()
     ctx = cb.Context(0)
     PT = cb.PlusTimesSRing("f64")
 
     # ---------------------------------------------------------------- config 4
+    if args.only in (0, 4):
+        config4(ctx, PT, args)
+    if args.only in (0, 5):
+        config5(ctx, PT, args)
+
+
+def config4(ctx, PT, args):
     t0 = time.perf_counter()
     n, cp, ir, val = protein_like_graph(args.mcl_n, seed=1)
     gen_s = time.perf_counter() - t0
@@ -78,7 +86,8 @@ def main():
                       "multiplies_per_s": mults / t_exp, "unit": "multiplies/s"}), flush=True)
     A.free()
 
-    # ---------------------------------------------------------------- config 5
+
+def config5(ctx, PT, args):
     t0 = time.perf_counter()
     n, acp, air, aval = poisson3d(args.poisson_k)
     nagg, rcp, rir, rval = aggregation_restriction(n, acp, air, seed=1)

@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""HBM traffic of k_num_heavy from rocprofv3 PMC passes -> profiles/<tag>_pmc_heavy.json.
+"""HBM traffic of the heavy-column numeric phase (k_num_heavy_known + k_num_heavy, the kernels between
+the heavy_ms events) from rocprofv3 PMC passes -> profiles/<tag>_pmc_heavy.json.
 
 Run on the GPU box (each counter group is its own rocprofv3 run, MI355X_MICROARCH.md §rocprofv3):
     python tools/pmc_heavy.py run <tag> [scale]      # two PMC passes over bench.py + summary
@@ -45,16 +46,18 @@ def run(tag, scale):
         print(f"pass {ctr}: rc={r.returncode}", flush=True)
         if r.returncode != 0:
             sys.exit(r.returncode)
+    nprod = 2   # --warmup 1 --steps 1: two products; every product launches each heavy kernel once
     f = per_dispatch(os.path.join(out, "pmc0"), "k_num_heavy").get("FETCH_SIZE", [])
     w = per_dispatch(os.path.join(out, "pmc1"), "k_num_heavy").get("WRITE_SIZE", [])
     if not f or not w:
         sys.exit("no k_num_heavy dispatches in the PMC output")
-    fetch = sum(f) / len(f) * 1024.0
-    write = sum(w) / len(w) * 1024.0
-    res = {"kernel": "k_num_heavy", "scale": scale, "edgefactor": 16, "launches": [len(f), len(w)],
+    fetch = sum(f) / nprod * 1024.0
+    write = sum(w) / nprod * 1024.0
+    res = {"kernel": "k_num_heavy_known + k_num_heavy", "scale": scale, "edgefactor": 16,
+           "launches": [len(f), len(w)], "products": nprod,
            "fetch_bytes_per_launch": fetch, "write_bytes_per_launch": write,
            "bytes_per_launch": fetch + write, "bytes_per_launch_fetch_doubled": 2 * fetch + write,
-           "note": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (KiB x 1024), averaged over dispatches; "
+           "note": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (KiB x 1024), summed over the heavy kernels per product; "
                    "gfx950 halves FETCH_SIZE for 16-B/lane streams, gathers are uncalibrated"}
     dst = os.path.join(out, f"{tag}_pmc_heavy.json")   # copied into profiles/ by hand
     json.dump(res, open(dst, "w"), indent=1)
