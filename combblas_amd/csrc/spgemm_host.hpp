@@ -227,23 +227,26 @@ struct Classes {
   std::vector<unsigned long long> off;    // exclusive offsets
 };
 
-// pass 0 of a binning into hist_dev[0..63] (no sync)
-inline void bin_count(hipStream_t st, int64_t n, const int64_t* cnt, const int2* span, BinParams bp,
-                      unsigned long long* hist_dev, int32_t* list) {
-  const int64_t g = (n + 255) / 256;
-  if (g > 0) k_bin<<<(int)g, 256, 0, st>>>(n, cnt, span, bp, 0, kHeavy, hist_dev, hist_dev + 32, list);
+// pass 0 of a binning into hist_dev[0..63] (no sync); flop: lane-class test when cnt is not the flop
+inline void bin_count(hipStream_t st, int64_t n, const int64_t* cnt, const int2* span, const int64_t* flop,
+                      BinParams bp, unsigned long long* hist_dev, int32_t* list) {
+  const int64_t g = (n + 256 * kBinPer - 1) / (256 * kBinPer);
+  if (g > 0) k_bin<<<(int)g, 256, 0, st>>>(n, cnt, span, flop, bp, 0, kHeavy, hist_dev, hist_dev + 32, list);
 }
-// after the host has hist: offsets, cursors, pass 1
-inline cbg_status bin_fill(hipStream_t st, int64_t n, const int64_t* cnt, const int2* span, BinParams bp,
-                           unsigned long long* hist_dev, const unsigned long long* hist_host, int32_t* list,
-                           Classes* cl) {
+// after the host has hist: offsets (the regular classes contiguous in class order, then the lane
+// class), cursors, pass 1
+inline cbg_status bin_fill(hipStream_t st, int64_t n, const int64_t* cnt, const int2* span, const int64_t* flop,
+                           BinParams bp, unsigned long long* hist_dev, const unsigned long long* hist_host,
+                           int32_t* list, Classes* cl) {
   const int ncls = bp.nwave + bp.nblock + 2;
   cl->hist.assign(hist_host, hist_host + 32);
-  cl->off.assign(ncls + 1, 0);
-  for (int c = 0; c < ncls; ++c) cl->off[c + 1] = cl->off[c] + cl->hist[c];
-  HIPCHK(hipMemcpyAsync(hist_dev + 32, cl->off.data(), sizeof(unsigned long long) * ncls, hipMemcpyHostToDevice, st));
-  const int64_t g = (n + 255) / 256;
-  if (g > 0) k_bin<<<(int)g, 256, 0, st>>>(n, cnt, span, bp, 1, kHeavy, hist_dev, hist_dev + 32, list);
+  cl->off.assign(32, 0);
+  unsigned long long acc = 0;
+  for (int c = 0; c < ncls; ++c) { cl->off[c] = acc; acc += cl->hist[c]; }
+  cl->off[kLaneClass] = acc;
+  HIPCHK(hipMemcpyAsync(hist_dev + 32, cl->off.data(), sizeof(unsigned long long) * 32, hipMemcpyHostToDevice, st));
+  const int64_t g = (n + 256 * kBinPer - 1) / (256 * kBinPer);
+  if (g > 0) k_bin<<<(int)g, 256, 0, st>>>(n, cnt, span, flop, bp, 1, kHeavy, hist_dev, hist_dev + 32, list);
   return CBG_OK;
 }
 
@@ -338,6 +341,11 @@ hipError_t launch_numeric_classes(hipStream_t st, const Classes& cl, const int32
                                   const Split& spl, const NumOut<V>& o) {
   auto L = [&](int c) { return list + cl.off[c]; };
   auto n = [&](int c) { return (int64_t)cl.hist[c]; };
+  if constexpr (!UNIT) {
+    if (n(kLaneClass))
+      k_num_lane<SRT, V><<<(int)grid_for(n(kLaneClass), 256, kMaxGrid * 4), 256, 0, st>>>(L(kLaneClass), n(kLaneClass),
+                                                                                          A, B, colptr, o);
+  }
   if (n(1)) launch_num_wave<6, SRT, V, UNIT>(st, L(1), n(1), units, A, B, span, colptr, spl, o);
   if (n(2)) launch_num_wave<7, SRT, V, UNIT>(st, L(2), n(2), units, A, B, span, colptr, spl, o);
   if (n(3)) launch_num_wave<8, SRT, V, UNIT>(st, L(3), n(3), units, A, B, span, colptr, spl, o);
@@ -424,7 +432,7 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
       *fb_ovf_n = si + 6;
   HIPCHK(hipMemsetAsync(sc, 0, 128, st));
   HIPCHK(hipMemsetAsync(nnz, 0, sizeof(int64_t) * N, st));
-  k_col_stats<<<(int)((N * 16 + 255) / 256), 256, 0, st>>>(N, A.cp, A.ir, B.cp, B.ir, flop, span, sc);
+  k_col_stats<<<(int)grid_for(N * 16, 256, kMaxGrid), 256, 0, st>>>(N, A.cp, A.ir, B.cp, B.ir, flop, span, sc);
   k_split_assign<<<(int)grid_for(A.ncol, 256, kMaxGrid), 256, 0, st>>>(A.ncol, A.cp, ctx->split_idx.as<int32_t>(),
                                                                         ctx->long_cols.as<int32_t>(), nlong);
   HIPCHK(hipGetLastError());
@@ -432,15 +440,15 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
 
   // 2. symbolic binning + kernels
   Classes cs;
-  BinParams sbp{kSymWave, kSymBlock, 64, 1};
+  BinParams sbp{kSymWave, kSymBlock, 64, 1, kLaneMax};
   unsigned long long hh[64];
   HIPCHK(hipMemsetAsync(hist, 0, sizeof(unsigned long long) * 64, st));
-  bin_count(st, N, flop, span, sbp, hist, list);
+  bin_count(st, N, flop, span, nullptr, sbp, hist, list);
   HIPCHK(hipMemcpyAsync(hh, hist, sizeof(unsigned long long) * 32, hipMemcpyDeviceToHost, st));
   HIPCHK(hipMemcpyAsync(hh + 32, sc, 96, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
   const int NL = ((int*)&hh[34])[1];
-  if ((s = bin_fill(st, N, flop, span, sbp, hist, hh, list, &cs)) != CBG_OK) return s;
+  if ((s = bin_fill(st, N, flop, span, nullptr, sbp, hist, hh, list, &cs)) != CBG_OK) return s;
   const int64_t hcap = (int64_t)cs.hist[31];
   HIPCHK(ctx->heavy_cols.reserve(sizeof(int32_t) * (hcap + 1)));
   HIPCHK(ctx->sub.reserve(sizeof(int32_t) * (hcap * nsub + 1)));
@@ -482,6 +490,9 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
   {
     auto L = [&](int c) { return list + cs.off[c]; };
     auto n = [&](int c) { return (int64_t)cs.hist[c]; };
+    if (n(kLaneClass))
+      k_sym_lane<<<(int)grid_for(n(kLaneClass), 256, kMaxGrid * 4), 256, 0, st>>>(L(kLaneClass), n(kLaneClass), A.cp,
+                                                                                  A.ir, B.cp, B.ir, nnz);
     if (n(1)) launch_sym_wave<6>(st, L(1), n(1), A.cp, A.ir, B.cp, B.ir, span, nnz, ho);
     if (n(2)) launch_sym_wave<7>(st, L(2), n(2), A.cp, A.ir, B.cp, B.ir, span, nnz, ho);
     if (n(3)) launch_sym_wave<8>(st, L(3), n(3), A.cp, A.ir, B.cp, B.ir, span, nnz, ho);
@@ -584,9 +595,9 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
   // 5. numeric binning (columns and units, one host sync) + kernels; heavy items split into the
   //    rows-known list (k_num_heavy_known) and the rest (k_num_heavy), counts -> sc[12], sc[13]
   Classes cn;
-  BinParams nbp{kNumWave, kNumBlock, 64, 0};
+  BinParams nbp{kNumWave, kNumBlock, 64, 0, kLaneMax};
   HIPCHK(hipMemsetAsync(hist, 0, sizeof(unsigned long long) * 128, st));
-  bin_count(st, N, nnz, span, nbp, hist, list);
+  bin_count(st, N, nnz, span, flop, nbp, hist, list);
   unsigned long long hn[128], tots[2] = {0, 0};
   HIPCHK(hipMemcpyAsync(hn, hist, sizeof(unsigned long long) * 128, hipMemcpyDeviceToHost, st));
   if (H > 0) HIPCHK(hipMemcpyAsync(tots, sc + 8, sizeof(tots), hipMemcpyDeviceToHost, st));
@@ -607,7 +618,7 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
         B.cp, ctx->items.as<KnownUnit>(), ctx->oitems.as<HeavyItem>(), sc + 12);
     HIPCHK(hipGetLastError());
   }
-  if ((s = bin_fill(st, N, nnz, span, nbp, hist, hn, list, &cn)) != CBG_OK) return s;
+  if ((s = bin_fill(st, N, nnz, span, flop, nbp, hist, hn, list, &cn)) != CBG_OK) return s;
   if (cn.hist[kNumWave + kNumBlock + 1] != 0) {   // every column above kHeavy must have become units
     fprintf(stderr, "cbgpu: %llu unbinned numeric columns\n", (unsigned long long)cn.hist[kNumWave + kNumBlock + 1]);
     return CBG_EDEVICE;

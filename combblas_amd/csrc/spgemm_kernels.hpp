@@ -256,12 +256,14 @@ __global__ void __launch_bounds__(256) k_col_stats(int64_t ncol, const int64_t* 
                                                    const int32_t* __restrict__ Bir,
                                                    int64_t* __restrict__ flop, int2* __restrict__ span,
                                                    unsigned long long* __restrict__ total) {
-  const int64_t gid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  const int64_t j = gid >> 4;
+  // 16 lanes per column, grid-stride over column groups; the block totals are added once per block
+  // (one global atomic per block: a same-address atomic per 16 columns serialised at the L2)
   const int sub = threadIdx.x & 15;
-  int64_t f = 0;
-  int lo = INT32_MAX, hi = -1;
-  if (j < ncol) {
+  int64_t wf = 0, hb = 0;
+  for (int64_t j = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 4; j < ncol;
+       j += ((int64_t)gridDim.x * blockDim.x) >> 4) {
+    int64_t f = 0;
+    int lo = INT32_MAX, hi = -1;
     const int64_t e = Bcp[j + 1];
     for (int64_t p = Bcp[j] + sub; p < e; p += 16) {
       const int32_t k = Bir[p];
@@ -272,24 +274,24 @@ __global__ void __launch_bounds__(256) k_col_stats(int64_t ncol, const int64_t* 
         hi = max(hi, Air[a1 - 1]);
       }
     }
-  }
 #pragma unroll
-  for (int d = 8; d > 0; d >>= 1) {
-    f += __shfl_xor(f, d, 16);
-    lo = min(lo, __shfl_xor(lo, d, 16));
-    hi = max(hi, __shfl_xor(hi, d, 16));
+    for (int d = 8; d > 0; d >>= 1) {
+      f += __shfl_xor(f, d, 16);
+      lo = min(lo, __shfl_xor(lo, d, 16));
+      hi = max(hi, __shfl_xor(hi, d, 16));
+    }
+    if (sub == 0) {
+      flop[j] = f;
+      span[j] = make_int2(lo, hi);
+      wf += f;
+      // an upper bound of the heavy columns' outputs, sum of min(flop, span) over columns with
+      // flop > kHeavy -> total[10] (row handoff scratch)
+      if (f > 4096 && hi >= lo) hb += min(f, (int64_t)hi - lo + 1);
+    }
   }
-  if (sub == 0 && j < ncol) {
-    flop[j] = f;
-    span[j] = make_int2(lo, hi);
-  }
-  // block-level totals: multiplies -> total[0]; an upper bound of the heavy columns' outputs,
-  // sum of min(flop, span) over columns with flop > kHeavy -> total[10] (row handoff scratch)
   __shared__ unsigned long long s_tot, s_hb;
   if (threadIdx.x == 0) { s_tot = 0; s_hb = 0; }
   __syncthreads();
-  int64_t wf = (sub == 0) ? f : 0;
-  int64_t hb = (sub == 0 && f > 4096 && hi >= lo) ? min(f, (int64_t)hi - lo + 1) : 0;
   wf = wave_sum64(wf);
   hb = wave_sum64(hb);
   if (lane_id() == 0 && wf) atomicAdd(&s_tot, (unsigned long long)wf);
@@ -309,7 +311,10 @@ struct BinParams {
   int nwave, nblock;     // number of wave / block classes
   int64_t wave_min_T;    // 64
   int sym;               // 1: symbolic (need = min(2*flop, span words)); 0: numeric (need = min(2*nnz, span))
+  int lane_max;          // columns with 0 < flop <= lane_max go to kLaneClass (one lane per column); 0 = off
 };
+constexpr int kLaneClass = 30;   // list class of the one-lane-per-column kernels (hist[30])
+constexpr int kLaneMax = 16;     // their per-lane table size: flop <= kLaneMax
 
 __device__ __forceinline__ int class_of(int64_t need, const BinParams& bp) {
   if (need <= 0) return 0;
@@ -329,10 +334,15 @@ __device__ __forceinline__ int64_t need_of(int64_t cnt, int2 sp, int sym) {
 }
 
 // pass 0: histogram; pass 1: scatter into class-contiguous list using device cursors.
-// hist[31] counts items with cnt > heavy (capacity of the heavy lists).
+// hist[31] counts items with cnt > heavy (capacity of the heavy lists).  Each block takes kBinPer
+// consecutive items per thread, so the per-class global atomics are one per block per class (not one
+// per 256 items: same-address atomics serialise at the L2).  flop (optional): lane-class test for the
+// numeric binning, whose cnt is nnz(C(:,j)).
+constexpr int kBinPer = 8;
 __global__ void __launch_bounds__(256) k_bin(int64_t n, const int64_t* __restrict__ cnt,
-                                             const int2* __restrict__ span, BinParams bp, int pass,
-                                             int64_t heavy, unsigned long long* __restrict__ hist,
+                                             const int2* __restrict__ span, const int64_t* __restrict__ flop,
+                                             BinParams bp, int pass, int64_t heavy,
+                                             unsigned long long* __restrict__ hist,
                                              unsigned long long* __restrict__ cursor,
                                              int32_t* __restrict__ list) {
   __shared__ unsigned int s_h[32];
@@ -340,24 +350,69 @@ __global__ void __launch_bounds__(256) k_bin(int64_t n, const int64_t* __restric
   const int ncls = bp.nwave + bp.nblock + 2;
   if (threadIdx.x < 32) s_h[threadIdx.x] = 0;
   __syncthreads();
-  const int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  int c = -1;
-  unsigned int rank = 0;
-  if (j < n) {
-    const int64_t cj = cnt[j];
-    c = class_of(need_of(cj, span[j], bp.sym), bp);
-    rank = atomicAdd(&s_h[c], 1u);
-    if (pass == 0 && cj > heavy) atomicAdd(&s_h[31], 1u);
+  const int64_t j0 = (int64_t)blockIdx.x * blockDim.x * kBinPer;
+  int cls[kBinPer];
+  unsigned int rank[kBinPer];
+#pragma unroll
+  for (int r = 0; r < kBinPer; ++r) {
+    const int64_t j = j0 + (int64_t)r * blockDim.x + threadIdx.x;
+    cls[r] = -1;
+    rank[r] = 0;
+    if (j < n) {
+      const int64_t cj = cnt[j];
+      const int64_t fj = flop ? flop[j] : cj;
+      const int c = (bp.lane_max > 0 && cj > 0 && fj <= bp.lane_max) ? kLaneClass
+                                                                   : class_of(need_of(cj, span[j], bp.sym), bp);
+      cls[r] = c;
+      rank[r] = atomicAdd(&s_h[c], 1u);
+      if (pass == 0 && cj > heavy) atomicAdd(&s_h[31], 1u);
+    }
   }
   __syncthreads();
+  const bool used = threadIdx.x < ncls || threadIdx.x == kLaneClass;
   if (pass == 0) {
-    if ((threadIdx.x < ncls || threadIdx.x == 31) && s_h[threadIdx.x])
+    if ((used || threadIdx.x == 31) && s_h[threadIdx.x])
       atomicAdd(&hist[threadIdx.x], (unsigned long long)s_h[threadIdx.x]);
     return;
   }
-  if (threadIdx.x < ncls) s_base[threadIdx.x] = s_h[threadIdx.x] ? atomicAdd(&cursor[threadIdx.x], (unsigned long long)s_h[threadIdx.x]) : 0;
+  if (used) s_base[threadIdx.x] = s_h[threadIdx.x] ? atomicAdd(&cursor[threadIdx.x], (unsigned long long)s_h[threadIdx.x]) : 0;
   __syncthreads();
-  if (c >= 0) list[s_base[c] + rank] = (int32_t)j;
+#pragma unroll
+  for (int r = 0; r < kBinPer; ++r)
+    if (cls[r] >= 0) list[s_base[cls[r]] + rank[r]] = (int32_t)(j0 + (int64_t)r * blockDim.x + threadIdx.x);
+}
+
+// ============================================================================ one-lane columns
+// Columns with at most kLaneMax multiplies (e.g. R^T A with an aggregation R: one multiply per A
+// entry) get one LANE each instead of a wavefront: the lane walks its few (B nonzero, A entry) pairs
+// into a private LDS slice, counts (symbolic) or accumulates, sorts and writes (numeric).  A wave
+// per such column spent its time on table set-up and scans for a handful of multiplies.
+constexpr int kLaneStride = kLaneMax + 1;   // odd stride: the 64 lanes' slices start in distinct banks
+
+__global__ void __launch_bounds__(256) k_sym_lane(const int32_t* __restrict__ list, int64_t count,
+                                                  const int64_t* __restrict__ Acp, const int32_t* __restrict__ Air,
+                                                  const int64_t* __restrict__ Bcp, const int32_t* __restrict__ Bir,
+                                                  int64_t* __restrict__ nnz) {
+  __shared__ int32_t s_rows[256 * kLaneStride];
+  int32_t* rows = s_rows + threadIdx.x * kLaneStride;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < count; i += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t j = list[i];
+    int m = 0;
+    const int64_t be = Bcp[j + 1];
+    for (int64_t b = Bcp[j]; b < be; ++b) {
+      const int32_t k = Bir[b];
+      const int64_t a1 = Acp[k + 1];
+      for (int64_t q = Acp[k]; q < a1 && m < kLaneMax; ++q) rows[m++] = Air[q];
+    }
+    int d = 0;   // an entry counts when no earlier entry has its row
+    for (int x = 0; x < m; ++x) {
+      const int32_t r = rows[x];
+      bool dup = false;
+      for (int y = 0; y < x; ++y) dup |= rows[y] == r;
+      d += !dup;
+    }
+    nnz[j] = d;
+  }
 }
 
 // ============================================================================ segment expansion
@@ -1349,6 +1404,63 @@ struct NumOut {
   int* ovf_n;             // fallback list length
   int32_t* ovf_list;      // items whose order-preserving hash overflowed (columns, or unit ids)
 };
+
+// numeric pass of the one-lane columns (kLaneClass, see k_sym_lane)
+template <class SRT, typename V>
+__global__ void __launch_bounds__(256) k_num_lane(const int32_t* __restrict__ list, int64_t count, DevCsc<V> A,
+                                                  DevCsc<V> B, const int64_t* __restrict__ colptr, NumOut<V> out) {
+  using Acc = typename SRT::Acc;
+  __shared__ int32_t s_rows[256 * kLaneStride];
+  __shared__ Acc s_acc[256 * kLaneStride];
+  int32_t* rows = s_rows + threadIdx.x * kLaneStride;
+  Acc* accs = s_acc + threadIdx.x * kLaneStride;
+  bool aerr = false;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < count; i += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t j = list[i];
+    int m = 0;
+    const int64_t be = B.cp[j + 1];
+    // (B nonzero, A entry) in storage order: the first contributor of a row is the first inserted
+    for (int64_t b = B.cp[j]; b < be; ++b) {
+      const int32_t k = B.ir[b];
+      const V bv = load_val(B.val, b);
+      const int64_t a1 = A.cp[k + 1];
+      for (int64_t q = A.cp[k]; q < a1; ++q) {
+        const int32_t r = A.ir[q];
+        const Acc x = SRT::mul(load_val(A.val, q), bv, q, b);
+        int y = 0;
+        while (y < m && rows[y] != r) ++y;
+        if (y == m) {
+          if (m == kLaneMax) continue;   // cannot happen: flop <= kLaneMax
+          rows[m] = r;
+          accs[m] = SRT::identity();
+          ++m;
+        } else if (SRT::kAddIsError) {
+          aerr = true;
+        }
+        SRT::acc(&accs[y], x);
+      }
+    }
+    for (int x = 1; x < m; ++x) {   // insertion sort by row (m <= kLaneMax)
+      const int32_t r = rows[x];
+      const Acc v = accs[x];
+      int y = x - 1;
+      while (y >= 0 && rows[y] > r) {
+        rows[y + 1] = rows[y];
+        accs[y + 1] = accs[y];
+        --y;
+      }
+      rows[y + 1] = r;
+      accs[y + 1] = v;
+    }
+    const int64_t o = colptr[j];
+    for (int x = 0; x < m; ++x) {
+      out.row[o + x] = rows[x];
+      out.val[o + x] = SRT::out(accs[x], A.val, B.val);
+    }
+  }
+  if (aerr) atomicOr(out.adderr, 1);
+}
+
 
 template <bool UNIT>
 __device__ __forceinline__ Work get_work(const int32_t* __restrict__ list, int64_t i, const Unit* __restrict__ units,
