@@ -5,7 +5,8 @@
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
 Workload (BASELINE.json configs): Graph500 Kronecker / R-MAT, edge factor 16, A*A over PlusTimes<double>,
-inputs generated on the host with a fixed seed and resident in HBM before the timed region.
+inputs built on the GPU from the reference's own Graph500 edge stream (seed 0xDECAFBAD, the reference's
+default SEED; the s20 matrix's hash equals refprobe `gen` output) and resident in HBM before the timed region.
   N = 1: configs[1], scale 20, the local hash SpGEMM (cbg_spgemm_local) on one GPU.
   N > 1: the distributed product on the mandated layout (combblas_amd/dist.py):
          2 -> 1x1x2, 4 -> 2x2 SUMMA, 8 -> 2x2x2 (configs[2] at scale 22), RCCL over xGMI.
@@ -114,6 +115,25 @@ def verify_sample(Cdev, cols, R):
             "against": "oracle/oracle.c product of the cpu_baseline sample columns"}
 
 
+def input_record(args, cp, ir, val, build_s):
+    """How the input was made, and whether it is the reference's own matrix: the canonical SHA-256 of the
+    device-built matrix against the hash of refprobe `gen` output for the same scale/seed
+    (tests/golden/kron.json, made by tests/golden/make_golden_kron.py from the reference build)."""
+    sys.path.insert(0, os.path.join(HERE, "tests", "golden"))
+    from cbm import canonical_sha256
+    rec = {"generator": "cbg_generate_rmat on the GPU: the reference's Graph500 edge stream (RefGen21, packed) + "
+                        "duplicate-summing build (SpParMat(DistEdgeList))", "seed": args.seed,
+           "device_build_s": round(build_s, 4), "nnz": int(len(ir))}
+    try:
+        ref = [c for c in json.load(open(os.path.join(HERE, "tests", "golden", "kron.json")))["cases"]
+               if (c["scale"], c["edgefactor"], c["seed"]) == (args.scale, args.edgefactor, args.seed)]
+    except (OSError, ValueError):
+        ref = []
+    if ref:
+        rec["sha256_equals_reference_generator"] = canonical_sha256(cp, ir, val) == ref[0]["sha256"]
+    return rec
+
+
 def workload(scale, edgefactor, parallelism):
     return {"workload": f"R-MAT (Graph500 Kronecker a,b,c,d=.57,.19,.19,.05, scrambled ids, duplicates summed) "
                         f"scale-{scale} edge factor {edgefactor} A*A PlusTimes<double>",
@@ -125,10 +145,14 @@ def bench_local(args):
     import combblas_amd as cb
     from combblas_amd import _abi
 
-    n, cp, ir, val = cb.generate_rmat_host(args.scale, args.edgefactor, seed=args.seed)
-    flop_col = col_flops(cp, ir)
     ctx = cb.Context(0)
-    A = cb.SpDCCols.from_csc(ctx, n, n, cp, ir, val)
+    t0 = time.perf_counter()
+    A = ctx.generate_rmat(args.scale, args.edgefactor, seed=args.seed)   # built in HBM (kron.hip)
+    ctx.synchronize()
+    build_s = time.perf_counter() - t0
+    n = A.getncol()
+    cp, ir, val = A.to_host()            # host copy: column statistics, CPU baseline, input hash
+    flop_col = col_flops(cp, ir)
     va = A._view()
     lib = ctx._lib
     keep = {}
@@ -190,6 +214,7 @@ def bench_local(args):
                      "heavy_columns": int(heavy.sum()), "heavy_multiplies": int(flop_col[heavy].sum()),
                      "heavy_nnz_C": int(nnz_c_col[heavy].sum())},
     }
+    out["input"] = input_record(args, cp, ir, val, build_s)
     if not args.no_cpu:
         out["cpu_baseline"], (cols, R) = cpu_baseline(cp, ir, val, n, flop_col, args.cpu_mults)
         out["verified"] = verify_sample(keep["C"], cols, R)
@@ -217,13 +242,16 @@ def bench_dist(args, world, rank, local_rank):
         dist.init_process_group(backend)
     L, q, _ = cbd.grid_for(world)
     grid = cbd.CommGrid3D(L, q, q)
-    n, cp, ir, val = cb.generate_rmat_host(args.scale, args.edgefactor, seed=args.seed)
     ctx = cb.Context(dev)
     be = cbd.GpuBackend(ctx)
-    A = cbd.SpParMat3D.from_global_csc(grid, n, n, cp, ir, val, True, be)
-    B = cbd.SpParMat3D.from_global_csc(grid, n, n, cp, ir, val, False, be)
-    nnzb = int(cp[-1])
-    del cp, ir, val
+    n = 1 << args.scale
+    t0 = time.perf_counter()
+    # every rank builds only its own pieces, on its GPU (SpParMat3D.from_rmat -> cbg_rmat_block)
+    A = cbd.SpParMat3D.from_rmat(grid, args.scale, args.edgefactor, args.seed, True, be)
+    B = cbd.SpParMat3D.from_rmat(grid, args.scale, args.edgefactor, args.seed, False, be)
+    torch.cuda.synchronize()
+    build_s = time.perf_counter() - t0
+    nnzb = A.getnnz()
     SR = cb.PlusTimesSRing("f64")
 
     phases = {}
@@ -279,7 +307,10 @@ def bench_dist(args, world, rank, local_rank):
                "data": "synthetic", "config": cfg,
                "effective_GBps": balg_bytes(mults / args.steps, nnzc / args.steps, nnzb, n)
                / (elapsed / args.steps) / 1e9,
-               "rank0_phases_per_step": {k: round(v / args.steps, 3) for k, v in phases.items()}}
+               "rank0_phases_per_step": {k: round(v / args.steps, 3) for k, v in phases.items()},
+               "input": {"generator": "SpParMat3D.from_rmat: each rank builds its own A and B pieces on its GPU "
+                                      "(cbg_rmat_block, the reference's Graph500 edge stream)", "seed": args.seed,
+                         "rank0_device_build_s": round(build_s, 4), "nnz": nnzb}}
         print(json.dumps(out), flush=True)
     dist.destroy_process_group()
 
@@ -291,7 +322,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--scale", type=int, default=0, help="R-MAT scale (default 20 + {1:0,2:1,4:1,8:2}[N])")
     ap.add_argument("--edgefactor", type=int, default=16)
-    ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--seed", type=int, default=0xDECAFBAD, help="Graph500 user seed (the reference's SEED)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-mults", type=float, default=1.5e9, help="multiplies in the CPU baseline sample")
     args = ap.parse_args()

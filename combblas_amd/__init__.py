@@ -21,10 +21,12 @@ import numpy as np
 from . import _abi
 from ._abi import CbgError
 
+G500_SEED = 0xDECAFBAD   # the reference's default Graph500 user seed (RefGen21::init_random, RefGen21.h:306-318)
+
 __all__ = ["Context", "SpDCCols", "SpTuples", "PlusTimesSRing", "MinPlusSRing", "Select2ndSRing",
            "SelectMaxSRing", "SelectMaxBoolSRing", "BoolCopy1stSRing", "BoolCopy2ndSRing",
            "LocalSpGEMMHash", "LocalHybridSpGEMM", "LocalSpGEMM", "EstimateLocalFLOP", "MultiwayMerge",
-           "CbgError", "generate_rmat_host", "default_context"]
+           "CbgError", "generate_rmat_host", "default_context", "G500_SEED"]
 
 _NP = {_abi.BOOL: np.uint8, _abi.I32: np.int32, _abi.I64: np.int64, _abi.F32: np.float32, _abi.F64: np.float64}
 _DT = {"bool": _abi.BOOL, "i32": _abi.I32, "i64": _abi.I64, "f32": _abi.F32, "f64": _abi.F64,
@@ -133,10 +135,19 @@ class Context:
                                        _abi.SORTED_COLS if sort else 0, ctypes.byref(res)), "cbg_merge")
         return SpDCCols._from_result(self, res)
 
-    def generate_rmat(self, scale, edgefactor=16, seed=1):
+    def generate_rmat(self, scale, edgefactor=16, seed=G500_SEED):
+        """The reference's Graph500 Kronecker matrix (DistEdgeList::GenGraph500Data packed + SpParMat(DEL),
+        DistEdgeList.cpp:223-280, SpParMat.cpp:3082-3196), built on this context's GPU."""
         res = _abi.CscResult()
         _abi.check(self._lib.cbg_generate_rmat(self._ptr, scale, edgefactor, seed, ctypes.byref(res)),
                    "cbg_generate_rmat")
+        return SpDCCols._from_result(self, res)
+
+    def rmat_block(self, scale, r0, r1, c0, c1, edgefactor=16, seed=G500_SEED):
+        """Rows [r0, r1) x columns [c0, c1) of that matrix (local indices), built on the GPU."""
+        res = _abi.CscResult()
+        _abi.check(self._lib.cbg_rmat_block(self._ptr, scale, edgefactor, seed, r0, r1, c0, c1, ctypes.byref(res)),
+                   "cbg_rmat_block")
         return SpDCCols._from_result(self, res)
 
 
@@ -307,8 +318,9 @@ def MultiwayMerge(SR, lists, mdim=0, ndim=0, delarrs=False):
     return C
 
 
-def generate_rmat_host(scale, edgefactor=16, seed=1):
-    """Host-only Graph500-style Kronecker matrix (no GPU needed): (n, colptr, rows, vals)."""
+def generate_rmat_host(scale, edgefactor=16, seed=G500_SEED):
+    """The reference's Graph500 Kronecker matrix built on the host (no GPU needed): (n, colptr, rows, vals).
+    `seed` is the Graph500 user seed (the reference's SEED environment variable, RefGen21.h:306-318)."""
     L = _abi.lib()
     h = _abi.HostCsc()
     _abi.check(L.cbg_rmat_host(scale, edgefactor, seed, ctypes.byref(h)), "cbg_rmat_host")

@@ -95,6 +95,8 @@ SIGNATURES = {
     "cbg_last_profile": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(Profile)]),
     "cbg_generate_rmat": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint64,
                                          ctypes.POINTER(CscResult)]),
+    "cbg_rmat_block": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint64, ctypes.c_int64,
+                                      ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.POINTER(CscResult)]),
     "cbg_rmat_host": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_uint64, ctypes.POINTER(HostCsc)]),
     "cbg_host_free": (None, [ctypes.POINTER(HostCsc)]),
     "cbg_mcl_prune": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(CscResult), ctypes.c_double, ctypes.c_int64,

@@ -189,21 +189,6 @@ cbg_status cbg_last_profile(cbg_ctx* ctx, cbg_profile* p) {
 
 }  // extern "C"
 
-extern "C" cbg_status cbg_generate_rmat(cbg_ctx* ctx, int32_t scale, int32_t edgefactor, uint64_t seed,
-                                        cbg_csc_result* A) {
-  if (!ctx || !A) return CBG_EINVAL;
-  cbg_host_csc h;
-  cbg_status s = cbg_rmat_host(scale, edgefactor, seed, &h);
-  if (s != CBG_OK) return s;
-  cbg_dcsc_view v{};
-  v.nrow = h.nrow; v.ncol = h.ncol; v.nnz = h.nnz; v.nzc = h.ncol;
-  v.cp = h.colptr; v.ir = h.row; v.idx_bytes = 4; v.ptr_bytes = 8;
-  v.val = h.val; v.val_type = CBG_F64; v.on_device = 0;
-  s = cbg_upload(ctx, &v, A);
-  cbg_host_free(&h);
-  return s;
-}
-
 extern "C" cbg_status cbg_merge(cbg_ctx* ctx, const cbg_csc_result* parts, int32_t nparts, cbg_semiring sr,
                                 cbg_dtype val_type, uint32_t flags, cbg_csc_result* C) {
   if (!ctx || !parts || nparts <= 0 || !C) return CBG_EINVAL;

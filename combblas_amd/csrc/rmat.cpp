@@ -1,76 +1,42 @@
-// rmat.cpp -- deterministic Graph500-style Kronecker (R-MAT) generator, host side.
+// rmat.cpp -- the reference's Graph500 Kronecker (R-MAT) matrix built on the host (no GPU needed).
 //
-// Semantics follow the reference's packed Graph500 path (include/CombBLAS/RefGen21.h:102-225 and
-// DistEdgeList::GenGraph500Data, DistEdgeList.cpp:223-280) and the SpParMat(DistEdgeList) build
-// (SpParMat.cpp:3082-3196, SpTuples.cpp:66-115):
-//   * 16*2^scale edges, initiator a,b,c,d = 0.57,0.19,0.19,0.05 (RefGen21.h:73-75, numerators /10000)
-//   * per level a quadrant draw; "clip-and-flip" keeps src <= tgt while both halves coincide
-//     (RefGen21.h:206-214), so the unscrambled graph is upper triangular
-//   * vertex ids scrambled by a bijection of [0, 2^scale)
-//   * edge (src, tgt) -> A(src, tgt); duplicate edges summed, value = multiplicity (f64), loops kept.
-// The random stream is our own counter-based hash (splitmix64 of (seed, edge, level)), so matrices are
-// statistically equivalent to (not bit-identical with) the reference's MRG stream; golden parity
-// tests use reference-generated inputs stored as fixtures instead.
+// The edge stream is the reference's own (kron.hpp: RefGen21.h:102-318, DistEdgeList.cpp:223-280,
+// packed path); the matrix build follows SpParMat(DistEdgeList, removeloops=false)
+// (SpParMat.cpp:3082-3196) and the duplicate-summing SpTuples constructor (SpTuples.cpp:66-115):
+// edge (v0, v1) -> A(v0, v1), duplicates summed into the value = multiplicity (f64), loops kept.
+// The device build of the same matrix (and of any block of it) is cbg_rmat_block in kron.hip.
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
 #include <vector>
 #include <algorithm>
 #include "cbgpu.h"
-
-namespace {
-
-inline uint64_t mix64(uint64_t z) {
-  z += 0x9E3779B97F4A7C15ull;
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  return z ^ (z >> 31);
-}
-
-// bijection on [0, 2^s): odd multiply, add, xor-shift, odd multiply (all invertible mod 2^s)
-inline uint64_t scramble(uint64_t v, int s, uint64_t k0, uint64_t k1) {
-  const uint64_t mask = (s >= 64) ? ~0ull : ((1ull << s) - 1);
-  v = (v * (k0 | 1ull) + k1) & mask;
-  v ^= v >> ((s + 1) / 2);
-  v = (v * ((k1 << 1) | 1ull)) & mask;
-  v ^= v >> ((s + 2) / 3);
-  v = (v * 0x9E3779B97F4A7C15ull + k0) & mask;
-  return v;
-}
-
-inline void make_edge(uint64_t seed, uint64_t e, int scale, uint64_t k0, uint64_t k1, uint32_t* src, uint32_t* tgt) {
-  uint64_t bs = 0, bt = 0;
-  uint64_t state = mix64(seed ^ mix64(e));
-  for (int lvl = 0; lvl < scale; ++lvl) {
-    if ((lvl & 1) == 0) state = mix64(state + (uint64_t)lvl);
-    const uint32_t draw = (uint32_t)(state >> ((lvl & 1) ? 32 : 0));
-    const uint32_t val = draw % 10000u;          // INITIATOR_DENOMINATOR
-    int sq;                                      // generate_4way_bernoulli quadrant order
-    if (val < 1900u) sq = 1;                     // b
-    else if (val < 3800u) sq = 2;                // c
-    else if (val < 9500u) sq = 0;                // a (5700)
-    else sq = 3;                                 // d
-    int so = sq / 2, to = sq % 2;
-    if (bs == bt && so > to) { int t = so; so = to; to = t; }   // clip-and-flip
-    const uint64_t half = 1ull << (scale - 1 - lvl);
-    bs += half * so;
-    bt += half * to;
-  }
-  *src = (uint32_t)scramble(bs, scale, k0, k1);
-  *tgt = (uint32_t)scramble(bt, scale, k0, k1);
-}
-
-}  // namespace
+#include "kron.hpp"
 
 extern "C" cbg_status cbg_rmat_host(int32_t scale, int32_t edgefactor, uint64_t seed, cbg_host_csc* out) {
   if (!out || scale < 1 || scale > 31 || edgefactor < 1) return CBG_EINVAL;
   memset(out, 0, sizeof(*out));
   const int64_t n = 1ll << scale;
   const int64_t m = (int64_t)edgefactor << scale;
-  const uint64_t k0 = mix64(seed * 0x51ED2705ull + 1), k1 = mix64(seed + 0xA5A5A5A5ull);
+  using namespace cbg::kron;
+  if (((uint64_t)m >> (8 * kSkipBytes)) != 0) return CBG_EUNSUP;
+  std::vector<Mat> tab(kSkipBytes * 256);
+  const Params p = make_params(seed, tab.data());
   std::vector<uint32_t> src(m), tgt(m);
+  const int64_t run = 64;   // one table jump per run of edges, then one A^(2^64) step per edge
 #pragma omp parallel for schedule(static)
-  for (int64_t e = 0; e < m; ++e) make_edge(seed, (uint64_t)e, scale, k0, k1, &src[e], &tgt[e]);
+  for (int64_t r0 = 0; r0 < m; r0 += run) {
+    State z = p.base;
+    for (uint64_t ei = (uint64_t)r0, i = 0; ei; ++i, ei >>= 8)
+      if (ei & 0xFF) apply(tab[i * 256 + (ei & 0xFF)], z);
+    for (int64_t e = r0; e < std::min(m, r0 + run); ++e) {
+      int64_t s0, t0;
+      edge_unscrambled(z, scale, &s0, &t0);
+      src[e] = (uint32_t)scramble(s0, scale, p.val0, p.val1);
+      tgt[e] = (uint32_t)scramble(t0, scale, p.val0, p.val1);
+      apply(tab[1], z);
+    }
+  }
   // counting sort by column (tgt), then per-column row sort + duplicate merge
   std::vector<int64_t> cnt(n + 1, 0);
   for (int64_t e = 0; e < m; ++e) cnt[tgt[e] + 1]++;

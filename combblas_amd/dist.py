@@ -161,6 +161,19 @@ class SpParMat3D:
         self.block = block_from_host(r1 - r0, c1 - c0, lcp, lir, lval, backend.device)
         return self
 
+    @classmethod
+    def from_rmat(cls, grid, scale, edgefactor, seed, colsplit, backend):
+        """This rank's piece of the reference's Graph500 Kronecker matrix, built on the rank's own device
+        (DistEdgeList::GenGraph500Data(packed) + SpParMat(DEL), DistEdgeList.cpp:223-280,
+        SpParMat.cpp:3082-3196; libcbgpu cbg_rmat_block).  The reference generates 1/p of the edges per
+        rank and routes them to their owners with an all-to-all; every rank here replays the edge stream
+        and keeps its own block, so no rank ever holds the global matrix and nothing is communicated."""
+        n = 1 << int(scale)
+        self = cls(grid, n, n, None, colsplit, backend)
+        (r0, r1), (c0, c1) = self.local_range()
+        self.block = backend.rmat_block(scale, edgefactor, seed, r0, r1, c0, c1)
+        return self
+
     def __call__(self, ri, ci):
         """SpParMat::operator()(ri, ci) (SpParMat.h) = SubsRef_SR with PlusTimes semirings."""
         return SubsRef_SR(self, ri, ci)
@@ -1032,6 +1045,12 @@ class GpuBackend:
                                         _abi.SORTED_COLS, ctypes.byref(res), ctypes.byref(m)), "cbg_spgemm_local")
         if stats is not None:
             stats["multiplies"] = stats.get("multiplies", 0) + int(m.value)
+        return self._take(res)
+
+    def rmat_block(self, scale, edgefactor, seed, r0, r1, c0, c1):
+        res = _abi.CscResult()
+        _abi.check(self.ctx._lib.cbg_rmat_block(self.ctx._ptr, int(scale), int(edgefactor), int(seed), int(r0), int(r1),
+                                                int(c0), int(c1), ctypes.byref(res)), "cbg_rmat_block")
         return self._take(res)
 
     def mcl_prune(self, blk, thr, select, recover, pct):

@@ -12,7 +12,8 @@
  *   cbg_merge          MultiwayMerge<SR>(lists, m, n, delarrs)           include/CombBLAS/MultiwayMerge.h:411-412
  *                      MultiwayMergeHash<SR>(lists, m, n, delarrs, sorted) include/CombBLAS/MultiwayMerge.h:536-537
  *   cbg_generate_rmat  DistEdgeList::GenGraph500Data + SpParMat(DEL)     include/CombBLAS/DistEdgeList.cpp:223-280,
- *                                                                        include/CombBLAS/SpParMat.cpp:3082-3196
+ *   cbg_rmat_block     (+ RefGen21 edge stream, SpTuples dup-summing)    include/CombBLAS/SpParMat.cpp:3082-3196,
+ *                                                                        RefGen21.h:102-318, SpTuples.cpp:66-115
  *   cbg_mcl_prune      MCLPruneRecoverySelect(A, thr, select, recover, pct, kselectVersion)
  *                                                                        include/CombBLAS/ParFriends.h:185-353
  *                      (Kselect1 SpParMat.cpp:1413-1700, PruneColumn SpParMat.cpp:2567-2720)
@@ -164,13 +165,22 @@ typedef struct {
 } cbg_host_csc;
 
 /*
- * Graph500 Kronecker/R-MAT input (a,b,c,d = .57,.19,.19,.05, clip-and-flip, scrambled vertex
- * ids, duplicate edges summed into the value = multiplicity), built on the host into a
- * caller-provided or library-owned CSC.  Deterministic in `seed`.
+ * Graph500 Kronecker/R-MAT input exactly as the reference builds it for its R-MAT runs:
+ * DistEdgeList::GenGraph500Data(initiator .57/.19/.19/.05, scale, edgefactor, scramble, packed)
+ * (DistEdgeList.cpp:223-280, RefGen21.h:102-318: MRG stream, clip-and-flip, scrambled vertex ids)
+ * then SpParMat(DistEdgeList, removeloops=false) (SpParMat.cpp:3082-3196): edge (v0, v1) -> A(v0, v1),
+ * duplicate edges summed into the value = multiplicity (f64), loops kept.  `seed` is the Graph500
+ * user seed (the reference's SEED environment variable, default 0xDECAFBAD, RefGen21.h:306-318).
+ *
+ * cbg_rmat_block: the block rows [r0, r1) x cols [c0, c1) of that matrix (local indices), built on
+ *   the device: every rank replays the edge stream and keeps its own block (no communication).
+ * cbg_generate_rmat: the whole matrix on the device.
+ * cbg_rmat_host: the whole matrix built on the host only (no GPU needed).
  */
+cbg_status cbg_rmat_block(cbg_ctx* ctx, int32_t scale, int32_t edgefactor, uint64_t seed, int64_t r0, int64_t r1,
+                          int64_t c0, int64_t c1, cbg_csc_result* A);
 cbg_status cbg_generate_rmat(cbg_ctx* ctx, int32_t scale, int32_t edgefactor, uint64_t seed,
                              cbg_csc_result* A);
-/* The same matrix built on the host only (no GPU needed). */
 cbg_status cbg_rmat_host(int32_t scale, int32_t edgefactor, uint64_t seed, cbg_host_csc* out);
 void       cbg_host_free(cbg_host_csc* m);
 

@@ -8,6 +8,7 @@ them, multiplies, and checks its own output piece against the global product.
 """
 import os
 import sys
+import time
 
 import numpy as np
 import scipy.sparse as sp
@@ -48,6 +49,12 @@ class ScipyBackend:
             m = int(np.diff(A.cp.numpy())[B.ir.numpy()].sum()) if B.nnz else 0
             stats["multiplies"] = stats.get("multiplies", 0) + m
         return self._block(P, A.val.numpy().dtype)
+
+    def rmat_block(self, scale, edgefactor, seed, r0, r1, c0, c1):
+        import combblas_amd as cb
+        n, cp, ir, val = cb.generate_rmat_host(scale, edgefactor, seed=seed)   # host build of the same matrix
+        lcp, lir, lval = cbd.slice_csc(cp, ir, val, r0, r1, c0, c1)
+        return Block(r1 - r0, c1 - c0, torch.as_tensor(lcp), torch.as_tensor(lir), torch.as_tensor(lval))
 
     def mcl_prune(self, blk, thr, select, recover, pct):
         from helpers import Csc, oracle_mcl_prune
@@ -172,8 +179,17 @@ def spawn_case(world, backend_kind, cases, port, body=None):
     procs = [ctx.Process(target=body or run_dist_case, args=(r, world, port, backend_kind, cases, errq)) for r in range(world)]
     for p in procs:
         p.start()
+    # join with a heartbeat (a silent multi-minute wait looks hung to a watchdog) and a 300 s bound
+    t0 = last = time.time()
+    while any(p.is_alive() for p in procs) and time.time() - t0 < 300:
+        time.sleep(0.2)
+        if time.time() - last >= 30:
+            last = time.time()
+            alive = [r for r, p in enumerate(procs) if p.is_alive()]
+            print(f"[spawn_case world={world}] {last - t0:.0f} s, ranks still running: {alive}",
+                  file=sys.stderr, flush=True)
     for p in procs:
-        p.join(timeout=300)
+        p.join(timeout=1)
     errs = []
     while not errq.empty():
         errs.append(errq.get())
@@ -402,6 +418,39 @@ def run_block_case(rank, world, port, backend_kind, cases, errq):
             for colsplit in (True, False):
                 M2 = cbd.Convert2D(dmat(Rs, colsplit, g3))
                 _check_piece(M2, Rs, rank, f"Convert2D {L}x{qq}x{qq} colsplit={colsplit}")
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:
+        import traceback
+        errq.put(f"rank {rank}: {e!r}\n{traceback.format_exc()}")
+        raise
+
+
+def run_rmat_case(rank, world, port, backend_kind, cases, errq):
+    """Per-rank body: every rank builds only its own pieces of the reference's Graph500 Kronecker matrix
+    (SpParMat3D.from_rmat -> cbg_rmat_block), which must equal the same blocks of the reference-generated
+    matrix in the fixture, and the SUMMA3D product of those pieces must equal the reference's product."""
+    try:
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        L, q, _ = cbd.grid_for(world)
+        grid = cbd.CommGrid3D(L, q, q)
+        import combblas_amd as cb
+        be = cbd.GpuBackend(cb.Context(0)) if backend_kind.startswith("gpu") else ScipyBackend()
+        from helpers import fixture_product, load_fixture
+        for (name, scale) in cases:
+            z = load_fixture(name)
+            G = sp.csc_matrix((z["A_val"], z["A_ir"], z["A_cp"]), shape=tuple(z["A_shape"]))
+            Ad = cbd.SpParMat3D.from_rmat(grid, scale, 16, cb.G500_SEED, True, be)
+            Bd = cbd.SpParMat3D.from_rmat(grid, scale, 16, cb.G500_SEED, False, be)
+            _check_piece(Ad, G, rank, f"{name} A piece")
+            _check_piece(Bd, G, rank, f"{name} B piece")
+            assert Ad.getnnz() == G.nnz
+            R = fixture_product(z, "pt_f64_hash")
+            C = cbd.Mult_AnXBn_SUMMA3D(cb.PlusTimesSRing("f64"), Ad, Bd)
+            check_piece_exact_or_f64(C, sp.csc_matrix((R.val, R.ir, R.cp), shape=(G.shape[0], R.ncol)), rank,
+                                     f"{name} C piece")
         dist.barrier()
         dist.destroy_process_group()
     except Exception as e:

@@ -84,15 +84,28 @@ def test_rmat_generator_properties():
     assert not np.array_equal(cp, cp3)
 
 
-def test_rmat_statistics_match_reference_generator():
-    """Our counter-based stream must reproduce the reference generator's product statistics
-    (G500 s12 ef16 A*A has 2,300,751 multiplies and 762,183 nnz, within a few %)."""
+def kron_cases():
+    import json
+    return json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "kron.json")))["cases"]
+
+
+@pytest.mark.parametrize("case", [c for c in kron_cases() if c["scale"] <= 18],
+                         ids=lambda c: f"s{c['scale']}_seed{c['seed']}")
+def test_rmat_host_matches_reference_generator(case):
+    """cbg_rmat_host reproduces the reference's GenGraph500Data(packed) + SpParMat(DEL) matrix exactly:
+    canonical SHA-256 of refprobe `gen` output (tests/golden/make_golden_kron.py, kron.json)."""
     import combblas_amd as cb
-    from helpers import Csc, oracle_spgemm
-    n, cp, ir, val = cb.generate_rmat_host(12, 16, seed=1)
-    A = Csc(n, n, cp, ir, val)
-    C, mults, rc = oracle_spgemm(A, A, "plus_times", "f64")
-    assert rc == 0
-    assert abs(len(ir) / 48_574 - 1) < 0.05              # nnz(A) of the reference G500 s12
-    assert abs(mults / 2_300_751 - 1) < 0.15
-    assert abs(C.nnz / 762_183 - 1) < 0.15
+    from helpers import canonical_sha256
+    n, cp, ir, val = cb.generate_rmat_host(case["scale"], case["edgefactor"], seed=case["seed"])
+    assert len(ir) == case["nnz"] and val.sum() == case["sum_val"]
+    assert canonical_sha256(cp, ir, val) == case["sha256"]
+
+
+def test_rmat_host_equals_reference_fixture_arrays():
+    """The whole s10 / s12 reference matrices stored in the fixtures, array by array."""
+    import combblas_amd as cb
+    from helpers import load_fixture
+    for scale in (10, 12):
+        z = load_fixture(f"g500_s{scale}")
+        n, cp, ir, val = cb.generate_rmat_host(scale, 16)
+        assert np.array_equal(cp, z["A_cp"]) and np.array_equal(ir, z["A_ir"]) and np.array_equal(val, z["A_val"])

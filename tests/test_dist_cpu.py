@@ -45,3 +45,11 @@ def test_block_spgemm_and_convert2d_gloo_cpu(world, port):
     """BlockSpGEMM / BlockSplit and SpParMat3D::Convert2D on the reference's G500 s10 fixture product."""
     from dist_support import run_block_case
     spawn_case(world, "scipy", BLOCK_CASES, port, body=run_block_case)
+
+
+@pytest.mark.parametrize("world,port", [(2, 29641), (4, 29642)])
+def test_rmat_pieces_built_per_rank_gloo_cpu(world, port):
+    """SpParMat3D.from_rmat: each rank builds only its own A/B pieces of the reference's Graph500 matrix;
+    pieces equal the reference-generated s10 fixture blocks and the SUMMA3D product equals its product."""
+    from dist_support import run_rmat_case
+    spawn_case(world, "scipy", [("g500_s10", 10)], port, body=run_rmat_case)
