@@ -797,30 +797,102 @@ def MCLPruneRecoverySelect(A, hardThreshold, selectNum, recoverNum, recoverPct, 
     return {"recovered": r[0], "selected": r[1], "recovered_after_select": r[2]}
 
 
+def _pad_cols(b, ncol, device):
+    """Block b widened to `ncol` columns with empty columns appended."""
+    if b.ncol == ncol:
+        return b
+    tail = b.cp[-1:].expand(ncol - b.ncol)
+    return Block(b.nrow, ncol, torch.cat([b.cp, tail]), b.ir, b.val)
+
+
+def EstPerProcessNnzSUMMA(A, B, hashEstimate=True):
+    """Max over ranks of the nnz of this rank's unmerged SUMMA stage products (ParFriends.h:1242-1347):
+    the symbolic pass of every stage product (estimateFLOP + estimateNNZ_Hash) summed over the q stages
+    of the layer, MAX-reduced over the world.  (The reference's loop computes colnnzC per stage but never
+    adds it to its total, so it returns 0 and its memory model never raises `phases`; the estimate here is
+    the one the formula intends.)"""
+    g, be = A.grid, A.backend
+    if A.ncol != B.nrow:
+        raise _abi.CbgError(_abi.EDIM, "EstPerProcessNnzSUMMA")
+    nnz = 0
+    for P in SUMMALayer(_PATTERN_SR(be), A, B):
+        nnz += P.nnz
+    t = torch.tensor([nnz], dtype=torch.int64, device=be.comm_device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return int(t.item())
+
+
+def _PATTERN_SR(be):
+    from . import PlusTimesSRing
+    return PlusTimesSRing("f64" if be.val_dtype == torch.float64 else "f32")
+
+
+def _phases_for_memory(A, B, phases, selectNum, recoverNum, perProcessMemory):
+    """The phase count of MemEfficientSpGEMM3D's memory model (ParFriends.h:3243-3290): inputs (five copies
+    of the largest layer piece), the layer's A*A estimate (two copies), the k-select buffers and the
+    post-selection output against perProcessMemory GB; the MAX over the fiber, never below `phases`."""
+    g, be = A.grid, A.backend
+    p = g.q * g.q
+    per_in = 4 * 2 + (8 if be.val_dtype == torch.float64 else 4)
+    per_out = per_in
+    t = torch.tensor([A.block.nnz], dtype=torch.int64, device=be.comm_device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    input_mem = int(t.item()) * per_in * 5
+    asq = EstPerProcessNnzSUMMA(A, B)
+    asq_mem = asq * per_out * 2
+    ncl = max(1, B.block.ncol)
+    d = -(-int((asq // g.L) * p ** 0.5) // ncl)
+    k = min(max(selectNum, recoverNum), d)
+    post_nnz = -(-int((ncl // g.L) * k) // max(1, int(p ** 0.5)))
+    remaining = perProcessMemory * 1e9 - input_mem - post_nnz * per_out * 2
+    ksel_mem = ncl * k * per_out * 3
+    calc = int(-(-(asq_mem + ksel_mem) // remaining)) if remaining > 0 else -1
+    return max(phases, calc)
+
+
 def MemEfficientSpGEMM(SR, A, B, phases, hardThreshold, selectNum, recoverNum, recoverPct, kselectVersion=1,
                        computationKernel=1, perProcessMemory=0, stats=None):
-    """HipMCL expansion (ParFriends.h:449-730): B's local columns are cut into `phases` pieces
-    (ColSplit); each phase is a full SUMMA product A * B_p followed by MCLPruneRecoverySelect, and
-    the pruned pieces are concatenated (ColConcatenate).  On a 3D grid (L > 1) the layer exchange
-    would interleave phase pieces, so phases = 1 there (MemEfficientSpGEMM3D's own phasing is not
-    mirrored); the product is phase-count independent either way."""
+    """HipMCL expansion, MemEfficientSpGEMM (ParFriends.h:449-730) on one layer and MemEfficientSpGEMM3D
+    (ParFriends.h:3214-3705) on L > 1 layers.  The rank's B columns are cut into the L layer chunks of
+    the output column split (CalculateColSplitDistributionOfLayer, SpParMat3D.cpp:576-606) and every
+    chunk into `phases` pieces (ColSplit, ParFriends.h:3315-3325); phase p multiplies the p-th piece of
+    every chunk (layer SUMMA), sends piece m to layer m along the fiber, merges, prunes
+    (MCLPruneRecoverySelect on the layer) and keeps only the pruned piece; the rank's pieces are
+    concatenated in phase order.  Pieces are padded to one width so the fiber split falls on piece
+    boundaries.  The pruned product does not depend on `phases`.  perProcessMemory > 0 raises `phases`
+    by the reference's memory model."""
     g, be = A.grid, A.backend
     if A.ncol != B.nrow:
         raise _abi.CbgError(_abi.EDIM, "MemEfficientSpGEMM")
-    if phases < 1 or phases >= A.ncol or g.L > 1:
+    if phases < 1 or phases >= B.ncol:
         phases = 1
+    if perProcessMemory > 0:
+        phases = max(1, min(_phases_for_memory(A, B, phases, selectNum, recoverNum, perProcessMemory),
+                            max(1, B.ncol - 1)))
+    L = g.L
     ncl = B.block.ncol
+    chunks = [block_range(ncl, L, m) for m in range(L)]
+    piece = [[(c0 + a, c0 + b) for (a, b) in (block_range(c1 - c0, phases, p) for p in range(phases))]
+             for (c0, c1) in chunks]
     pieces = []
     counts = {"recovered": 0, "selected": 0, "recovered_after_select": 0}
     for p in range(phases):
-        c0, c1 = block_range(ncl, phases, p)
-        Bp = SpParMat3D(g, B.nrow, B.ncol, _col_slice(B.block, c0, c1) if phases > 1 else B.block, False, be)
-        Cp = Mult_AnXBn_SUMMA3D(SR, A, Bp, stats)
+        sel = [piece[m][p] for m in range(L)]
+        W = max(b - a for (a, b) in sel)
+        if L == 1 and phases == 1:
+            Bb = B.block
+        else:
+            Bb = _col_concat([_pad_cols(_col_slice(B.block, a, b), W, be.device) for (a, b) in sel], be.device) \
+                if L > 1 else _col_slice(B.block, *sel[0])
+        Cp = Mult_AnXBn_SUMMA3D(SR, A, SpParMat3D(g, B.nrow, B.ncol, Bb, False, be), stats)
+        mine = sel[g.layer]
+        if L > 1 and Cp.block.ncol != mine[1] - mine[0]:
+            Cp.block = _col_slice(Cp.block, 0, mine[1] - mine[0])   # drop the padding columns
         st = MCLPruneRecoverySelect(Cp, hardThreshold, selectNum, recoverNum, recoverPct, kselectVersion)
         for k in counts:
             counts[k] += st[k]
         pieces.append(Cp.block)
-    blk = pieces[0] if phases == 1 else _col_concat(pieces, be.device)
+    blk = pieces[0] if len(pieces) == 1 else _col_concat(pieces, be.device)
     if stats is not None:
         stats.update(counts)
         stats["phases"] = phases

@@ -463,3 +463,47 @@ def run_rmat_case(rank, world, port, backend_kind, cases, errq):
         import traceback
         errq.put(f"rank {rank}: {e!r}\n{traceback.format_exc()}")
         raise
+
+
+def run_mcl_fixture_case(rank, world, port, backend_kind, cases, errq):
+    """Per-rank body: the reference's MemEfficientSpGEMM output (tests/golden/mcl.npz, made by refprobe)
+    through MemEfficientSpGEMM / MemEfficientSpGEMM3D on the mandated layout with phases 1..3: every
+    phase count gives the reference's pruned product on every rank's piece and the same branch counts."""
+    try:
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        L, q, _ = cbd.grid_for(world)
+        grid = cbd.CommGrid3D(L, q, q)
+        import combblas_amd as cb
+        be = cbd.GpuBackend(cb.Context(0)) if backend_kind.startswith("gpu") else ScipyBackend()
+        from helpers import Csc, load_fixture, oracle_mcl_prune
+        z = load_fixture("mcl")
+        n = int(z["A_shape"][0])
+        A = sp.csc_matrix((z["A_val"], z["A_ir"], z["A_cp"]), shape=(n, n))
+        thr, sel, rec, pct = (float(x) for x in z["P1_params"])
+        params = (thr, int(sel), int(rec), pct)
+        G = (A @ A).tocsc()
+        G.sort_indices()
+        _, ost = oracle_mcl_prune(Csc(n, n, G.indptr, G.indices, G.data), *params)
+        R = sp.csc_matrix((z["M1_val"], z["M1_ir"], z["M1_cp"]), shape=(n, n))
+        S = (abs(A) @ abs(A)).tocsc()
+        for case in cases:
+            phases, mem = (1, case[1]) if isinstance(case, tuple) else (case, 0)
+            Ad = cbd.SpParMat3D.from_global_csc(grid, n, n, z["A_cp"], z["A_ir"], z["A_val"], True, be)
+            Bd = cbd.SpParMat3D.from_global_csc(grid, n, n, z["A_cp"], z["A_ir"], z["A_val"], False, be)
+            stats = {}
+            C = cbd.MemEfficientSpGEMM(cb.PlusTimesSRing("f64"), Ad, Bd, phases, *params, perProcessMemory=mem,
+                                       stats=stats)
+            if mem:   # a budget just above the inputs: the memory model must raise the phase count
+                assert stats["phases"] > 1, stats
+            else:
+                assert stats["phases"] == phases, stats
+            check_piece_exact_or_f64(C, R, rank, f"memeff phases={phases}", scale=S)
+            assert (stats["recovered"], stats["selected"], stats["recovered_after_select"]) == ost, (stats, ost)
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:
+        import traceback
+        errq.put(f"rank {rank}: {e!r}\n{traceback.format_exc()}")
+        raise

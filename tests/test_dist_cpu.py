@@ -53,3 +53,12 @@ def test_rmat_pieces_built_per_rank_gloo_cpu(world, port):
     pieces equal the reference-generated s10 fixture blocks and the SUMMA3D product equals its product."""
     from dist_support import run_rmat_case
     spawn_case(world, "scipy", [("g500_s10", 10)], port, body=run_rmat_case)
+
+
+@pytest.mark.parametrize("world,port", [(2, 29651), (8, 29652)])
+def test_memeff3d_phases_match_reference_gloo_cpu(world, port):
+    """MemEfficientSpGEMM3D phasing (ParFriends.h:3214-3705; B pieces per layer chunk, fiber exchange per
+    phase, prune per phase): phases 1, 2, 3 reproduce the reference's MemEfficientSpGEMM output
+    (golden/mcl.npz) on every rank's piece, with the same branch counts."""
+    from dist_support import run_mcl_fixture_case
+    spawn_case(world, "scipy", [1, 2, 3, ("mem", 0.0025)], port, body=run_mcl_fixture_case)

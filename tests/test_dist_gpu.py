@@ -71,3 +71,12 @@ def test_rmat_pieces_built_per_rank_gloo_gpu(world, port):
     fixture blocks (s10, s12), and the 1x1x2 / 2x2 / 2x2x2 products of them equal the reference's."""
     from dist_support import run_rmat_case
     spawn_case(world, "gpu", [("g500_s10", 10), ("g500_s12", 12)], port, body=run_rmat_case)
+
+
+@pytest.mark.parametrize("world,port", [(2, 29651), (4, 29652), (8, 29653)])
+def test_memeff3d_phases_match_reference_gloo_gpu(world, port):
+    """MemEfficientSpGEMM3D phasing (ParFriends.h:3214-3705; B pieces per layer chunk, fiber exchange per
+    phase, prune per phase): phases 1, 2, 3 reproduce the reference's MemEfficientSpGEMM output
+    (golden/mcl.npz) on every rank's piece, with the same branch counts."""
+    from dist_support import run_mcl_fixture_case
+    spawn_case(world, "gpu", [1, 2, 3, ("mem", 0.0025)], port, body=run_mcl_fixture_case)
