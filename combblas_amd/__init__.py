@@ -26,7 +26,8 @@ G500_SEED = 0xDECAFBAD   # the reference's default Graph500 user seed (RefGen21:
 __all__ = ["Context", "SpDCCols", "SpTuples", "PlusTimesSRing", "MinPlusSRing", "Select2ndSRing",
            "SelectMaxSRing", "SelectMaxBoolSRing", "BoolCopy1stSRing", "BoolCopy2ndSRing",
            "LocalSpGEMMHash", "LocalHybridSpGEMM", "LocalSpGEMM", "EstimateLocalFLOP", "MultiwayMerge",
-           "CbgError", "generate_rmat_host", "default_context", "G500_SEED"]
+           "CbgError", "generate_rmat_host", "default_context", "G500_SEED", "RestrictionOp",
+           "GalerkinRAP"]
 
 _NP = {_abi.BOOL: np.uint8, _abi.I32: np.int32, _abi.I64: np.int64, _abi.F32: np.float32, _abi.F64: np.float64}
 _DT = {"bool": _abi.BOOL, "i32": _abi.I32, "i64": _abi.I64, "f32": _abi.F32, "f64": _abi.F64,
@@ -316,6 +317,35 @@ def MultiwayMerge(SR, lists, mdim=0, ndim=0, delarrs=False):
         for L in lists:
             L.free()
     return C
+
+
+def RestrictionOp(G, seed=1):
+    """MIS-2 aggregation restriction of the graph of G (3DSpGEMM/RestrictionOp.h:116-290) on G's GPU:
+    (R, RT) as device matrices, R (n x nagg) with R(i, agg(i)) = 1, RT = R^T.  G must be square and
+    symmetric (RestrictionOp symmetrises and drops loops first; self loops are ignored here)."""
+    ctx = G._ctx
+    R, RT, nagg = _abi.CscResult(), _abi.CscResult(), ctypes.c_int64(0)
+    _abi.check(ctx._lib.cbg_mis2_restriction(ctx._ptr, ctypes.byref(G._view()), int(seed), ctypes.byref(R),
+                                             ctypes.byref(RT), ctypes.byref(nagg)), "cbg_mis2_restriction")
+    return SpDCCols._from_result(ctx, R), SpDCCols._from_result(ctx, RT)
+
+
+def GalerkinRAP(A, R, RT=None):
+    """C = R^T A R (RestrictionOp.cpp:188-196).  For an aggregation R (one nonzero per row) whose
+    aggregates each gather at most 512 entries of A: one fused device pass (cbg_galerkin_rap,
+    C.multiplies = nnz(A)).  Otherwise, given RT = R^T, the reference's two products R^T A and
+    (R^T A) R; without RT such an R raises CbgError(CBG_EUNSUP)."""
+    ctx = A._ctx
+    res = _abi.CscResult()
+    st = ctx._lib.cbg_galerkin_rap(ctx._ptr, ctypes.byref(A._view()), ctypes.byref(R._view()), ctypes.byref(res))
+    if st == _abi.EUNSUP and RT is not None:
+        PT = PlusTimesSRing("f64")
+        RA = LocalSpGEMMHash(PT, RT, A)
+        C = LocalSpGEMMHash(PT, RA, R)
+        RA.free()
+        return C
+    _abi.check(st, "cbg_galerkin_rap")
+    return SpDCCols._from_result(ctx, res)
 
 
 def generate_rmat_host(scale, edgefactor=16, seed=G500_SEED):

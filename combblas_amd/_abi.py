@@ -97,6 +97,11 @@ SIGNATURES = {
                                          ctypes.POINTER(CscResult)]),
     "cbg_rmat_block": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint64, ctypes.c_int64,
                                       ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.POINTER(CscResult)]),
+    "cbg_mis2_restriction": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(DcscView), ctypes.c_uint64,
+                                            ctypes.POINTER(CscResult), ctypes.POINTER(CscResult),
+                                            ctypes.POINTER(ctypes.c_int64)]),
+    "cbg_galerkin_rap": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(DcscView), ctypes.POINTER(DcscView),
+                                        ctypes.POINTER(CscResult)]),
     "cbg_rmat_host": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_uint64, ctypes.POINTER(HostCsc)]),
     "cbg_host_free": (None, [ctypes.POINTER(HostCsc)]),
     "cbg_mcl_prune": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(CscResult), ctypes.c_double, ctypes.c_int64,

@@ -1,0 +1,417 @@
+// galerkin.hip -- the Galerkin coarse operator on the device: MIS-2 aggregation restriction and the
+// fused triple product R^T A R (BASELINE config 5).
+//
+// Reference (3DSpGEMM/RestrictionOp.h, RestrictionOp.cpp:155-196, ReleaseTests/GalerkinNew.cpp:100-127):
+//   MIS2 (RestrictionOp.h:116-196): Luby rounds on the symmetrised loop-free graph -- every candidate
+//     draws a random value, a candidate whose value beats all candidates within distance 2 joins the
+//     set, and it and its distance-2 neighbourhood leave the candidate set;
+//   RestrictionOp (RestrictionOp.h:198-290): every vertex joins an aggregate rooted at a set vertex
+//     within distance 1, else within distance 2; R(i, agg(i)) = 1 (n x nagg), RT = R^T;
+//   the driver then forms R^T A and (R^T A) R with two SpGEMMs (RestrictionOp.cpp:188-196).
+// Device formulation:
+//   * priorities are distinct 64-bit keys: a seeded hash of the vertex id above the id itself (the
+//     reference draws from its global Mersenne twister, so its aggregation is seed-specific; the
+//     host restatement combblas_amd.inputs.aggregation_restriction uses these same keys);
+//   * each round is two max-propagation sweeps (distance 1, then 2) and two flag sweeps over the CSC
+//     graph, one thread per vertex, and one counter read by the host;
+//   * R^T A R for an aggregation R (exactly one nonzero per row, any value): C(I, J) =
+//     sum over i in I, j in J of R(i,I) A(i,j) R(j,J).  One workgroup per aggregate J reads the A
+//     columns of J's members (R's row order), maps their rows to aggregates, sorts and sums in LDS
+//     (k_rap_agg: a count pass and a fill pass; one read of nnz(A) each instead of two SpGEMMs with
+//     an R^T A intermediate; deterministic summation order).
+#include "spgemm_host.hpp"
+
+namespace {
+
+__device__ __forceinline__ uint64_t mis_key(uint32_t v, uint64_t seed) {
+  uint64_t z = (uint64_t)v ^ (seed * 0x9E3779B97F4A7C15ull);
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return ((z >> 32) << 32 | v) + 1;   // distinct, nonzero; vertex = (key - 1) & 0xffffffff
+}
+
+__global__ void k_mis_keys(int64_t n, uint64_t seed, uint64_t* __restrict__ key, int8_t* __restrict__ state) {
+  for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < n; v += (int64_t)gridDim.x * blockDim.x) {
+    key[v] = mis_key((uint32_t)v, seed);
+    state[v] = 0;
+  }
+}
+
+// out[v] = max(in[v], max over neighbours u of in[u]); in = masked keys (mask: state == want) or a vector
+template <bool MASKED>
+__global__ void k_nbr_max(int64_t n, const int64_t* __restrict__ cp, const int32_t* __restrict__ ir,
+                          const uint64_t* __restrict__ in, const int8_t* __restrict__ state, int8_t want,
+                          uint64_t* __restrict__ out) {
+  for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < n; v += (int64_t)gridDim.x * blockDim.x) {
+    uint64_t m = (!MASKED || state[v] == want) ? in[v] : 0;
+    for (int64_t p = cp[v]; p < cp[v + 1]; ++p) {
+      const int32_t u = ir[p];
+      const uint64_t x = (!MASKED || state[u] == want) ? in[u] : 0;
+      m = x > m ? x : m;
+    }
+    out[v] = m;
+  }
+}
+
+// new set members: undecided vertices whose key is the distance-2 maximum
+__global__ void k_mis_select(int64_t n, const uint64_t* __restrict__ key, const uint64_t* __restrict__ m2,
+                             const int8_t* __restrict__ state, uint8_t* __restrict__ fresh) {
+  for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < n; v += (int64_t)gridDim.x * blockDim.x)
+    fresh[v] = state[v] == 0 && key[v] == m2[v];
+}
+
+__global__ void k_nbr_or(int64_t n, const int64_t* __restrict__ cp, const int32_t* __restrict__ ir,
+                         const uint8_t* __restrict__ in, uint8_t* __restrict__ out) {
+  for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < n; v += (int64_t)gridDim.x * blockDim.x) {
+    uint8_t f = in[v];
+    for (int64_t p = cp[v]; p < cp[v + 1] && !f; ++p) f = in[ir[p]];
+    out[v] = f;
+  }
+}
+
+// roots <- fresh; undecided vertices within distance 2 of a fresh root are covered; count undecided
+__global__ void k_mis_update(int64_t n, const uint8_t* __restrict__ fresh, const uint8_t* __restrict__ near2,
+                             int8_t* __restrict__ state, unsigned long long* __restrict__ undecided) {
+  unsigned long long c = 0;
+  for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < n; v += (int64_t)gridDim.x * blockDim.x) {
+    int8_t s = state[v];
+    if (fresh[v]) s = 1;
+    else if (s == 0 && near2[v]) s = 2;
+    state[v] = s;
+    c += s == 0;
+  }
+  c = wave_sum64((int64_t)c);
+  if (lane_id() == 0 && c) atomicAdd(undecided, c);
+}
+
+__global__ void k_root_keys(int64_t n, const uint64_t* __restrict__ key, const int8_t* __restrict__ state,
+                            uint64_t* __restrict__ rk, int64_t* __restrict__ isroot) {
+  for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < n; v += (int64_t)gridDim.x * blockDim.x) {
+    rk[v] = state[v] == 1 ? key[v] : 0;
+    isroot[v] = state[v] == 1;
+  }
+}
+
+// agg(v) = id of the highest-key root within distance 1, else within distance 2 (root ids in vertex order)
+__global__ void k_assign(int64_t n, const uint64_t* __restrict__ b1, const uint64_t* __restrict__ b2,
+                         const int64_t* __restrict__ rid, int32_t* __restrict__ agg, unsigned long long* __restrict__ colcnt) {
+  for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < n; v += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t b = b1[v] ? b1[v] : b2[v];
+    const int32_t a = b ? (int32_t)rid[(b - 1) & 0xffffffffull] : -1;
+    agg[v] = a;
+    if (a >= 0) atomicAdd(&colcnt[a], 1ull);
+  }
+}
+
+__global__ void k_scatter_members(int64_t n, const int32_t* __restrict__ agg, unsigned long long* __restrict__ cursor,
+                                  int32_t* __restrict__ rows) {
+  for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < n; v += (int64_t)gridDim.x * blockDim.x)
+    if (agg[v] >= 0) rows[atomicAdd(&cursor[agg[v]], 1ull)] = (int32_t)v;
+}
+
+__global__ void k_rt(int64_t n, const int32_t* __restrict__ agg, int64_t* __restrict__ cp, int32_t* __restrict__ ir,
+                     double* __restrict__ val) {
+  for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v <= n; v += (int64_t)gridDim.x * blockDim.x) {
+    cp[v] = v;
+    if (v < n) { ir[v] = agg[v]; val[v] = 1.0; }
+  }
+}
+
+// ---------------------------------------------------------------- fused R^T A R (aggregation R)
+// per row i of R: its aggregate and value; rows not covered exactly once are counted as bad
+__global__ void k_r_rows(int64_t nagg, const int64_t* __restrict__ rcp, const int32_t* __restrict__ rir,
+                         const double* __restrict__ rval, int32_t* __restrict__ agg, double* __restrict__ rv,
+                         unsigned int* __restrict__ seen) {
+  for (int64_t J = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; J < nagg; J += (int64_t)gridDim.x * blockDim.x)
+    for (int64_t p = rcp[J]; p < rcp[J + 1]; ++p) {
+      const int32_t i = rir[p];
+      agg[i] = (int32_t)J;
+      rv[i] = rval ? rval[p] : 1.0;
+      atomicAdd(&seen[i], 1u);
+    }
+}
+
+__global__ void k_count_bad(int64_t n, const unsigned int* __restrict__ seen, unsigned long long* __restrict__ bad) {
+  unsigned long long c = 0;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    c += seen[i] != 1;
+  c = wave_sum64((int64_t)c);
+  if (lane_id() == 0 && c) atomicAdd(bad, c);
+}
+
+// raw layout: member p of R (entries in column order) contributes |A(:, rir[p])| entries; the exclusive
+// scan of these lengths over p is each member's raw offset, and rawcp[J] = that offset at rcp[J]
+__global__ void k_member_len(int64_t nnzr, const int32_t* __restrict__ rir, const int64_t* __restrict__ acp,
+                             int64_t* __restrict__ len) {
+  for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < nnzr; p += (int64_t)gridDim.x * blockDim.x)
+    len[p] = acp[rir[p] + 1] - acp[rir[p]];
+}
+
+// One 64-lane workgroup per aggregate J: the flattened entries of its members' A columns (member p's
+// entries start at moff[p]) are loaded into LDS as keys (agg(i) << 32 | position) with values
+// R(i,I) A(i,j) R(j,J), bitonic-sorted, and every run of one row is summed in position order
+// (deterministic); count pass -> cnt[J], fill pass -> sorted (row, value) at ccp[J].  Aggregates with
+// more than kRapCap entries are counted in *overflow (the caller falls back to two SpGEMMs).
+constexpr int kRapCap = 512;
+
+__global__ void __launch_bounds__(64) k_rap_agg(int64_t nagg, const int64_t* __restrict__ rcp,
+                                                const int32_t* __restrict__ rir, const int64_t* __restrict__ acp,
+                                                const int32_t* __restrict__ air, const double* __restrict__ aval,
+                                                const int32_t* __restrict__ agg, const double* __restrict__ rv,
+                                                const int64_t* __restrict__ moff, int64_t* __restrict__ cnt,
+                                                int32_t* __restrict__ trow, double* __restrict__ tval, int64_t cap,
+                                                unsigned long long* __restrict__ overflow) {
+  __shared__ uint64_t key[kRapCap];
+  __shared__ double val[kRapCap];
+  const int lane = threadIdx.x;
+  for (int64_t J = blockIdx.x; J < nagg; J += gridDim.x) {
+    const int64_t p0 = rcp[J], p1 = rcp[J + 1];
+    const int64_t base = moff[p0];
+    const int t = (int)min<int64_t>(moff[p1] - base, kRapCap + 1);
+    if (t > kRapCap || base + t > cap) {   // uniform; past `cap` only for an R that is no aggregation
+      if (lane == 0) { atomicAdd(overflow, 1ull); cnt[J] = 0; }
+      continue;
+    }
+    int N = 64;
+    while (N < t) N <<= 1;
+    for (int e = lane; e < N; e += 64) {
+      if (e < t) {
+        int64_t lo = p0, hi = p1 - 1;   // the member holding entry e: last p with moff[p] - base <= e
+        while (lo < hi) {
+          const int64_t mid = (lo + hi + 1) >> 1;
+          if (moff[mid] - base <= e) lo = mid; else hi = mid - 1;
+        }
+        const int32_t j = rir[lo];
+        const int64_t q = acp[j] + (e - (moff[lo] - base));
+        const int32_t i = air[q];
+        key[e] = ((uint64_t)(uint32_t)agg[i] << 32) | (uint32_t)e;
+        val[e] = rv[i] * (aval ? aval[q] : 1.0) * rv[j];
+      } else {
+        key[e] = ~0ull;
+      }
+    }
+    __syncthreads();
+    for (int k = 2; k <= N; k <<= 1)
+      for (int jj = k >> 1; jj > 0; jj >>= 1) {
+        for (int tt = lane; tt < N / 2; tt += 64) {
+          const int a = (tt / jj) * 2 * jj + (tt % jj), b = a + jj;
+          const uint64_t x = key[a], y = key[b];
+          if ((x > y) == ((a & k) == 0)) { key[a] = y; key[b] = x; }
+        }
+        __syncthreads();
+      }
+    int64_t run = 0;   // unique rows so far; written from `base` (this aggregate's entry range bounds them)
+    for (int e0 = 0; e0 < t; e0 += 64) {
+      const int e = e0 + lane;
+      const bool head = e < t && (e == 0 || (key[e] >> 32) != (key[e - 1] >> 32));
+      const uint64_t mask = __ballot(head);
+      if (head) {
+        const int64_t o = base + run + __popcll(mask & ((1ull << lane) - 1));
+        const uint64_t r = key[e] >> 32;
+        double v = val[key[e] & 0xffffffffu];
+        for (int f = e + 1; f < t && (key[f] >> 32) == r; ++f) v += val[key[f] & 0xffffffffu];
+        trow[o] = (int32_t)r;
+        tval[o] = v;
+      }
+      run += __popcll(mask);
+    }
+    if (lane == 0) cnt[J] = run;
+    __syncthreads();
+  }
+}
+
+// C column J = the first cnt[J] entries of aggregate J's range in the scratch (16 lanes per column)
+__global__ void k_rap_compact(int64_t nagg, const int64_t* __restrict__ rcp, const int64_t* __restrict__ moff,
+                              const int64_t* __restrict__ ccp, const int32_t* __restrict__ trow,
+                              const double* __restrict__ tval, int32_t* __restrict__ crow, double* __restrict__ cval) {
+  const int sub = threadIdx.x & 15;
+  for (int64_t J = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 4; J < nagg;
+       J += ((int64_t)gridDim.x * blockDim.x) >> 4) {
+    const int64_t src = moff[rcp[J]], dst = ccp[J], n = ccp[J + 1] - dst;
+    for (int64_t x = sub; x < n; x += 16) {
+      crow[dst + x] = trow[src + x];
+      cval[dst + x] = tval[src + x];
+    }
+  }
+}
+
+cbg_status scan_counts_async(hipStream_t st, int64_t n, const int64_t* cnt, int64_t* out, int64_t* total_dev,
+                             DevBuf* tiles) {
+  const int64_t ntiles = (n + kScanTile - 1) / kScanTile;
+  HIPCHK(tiles->reserve(sizeof(int64_t) * (ntiles + 1)));
+  if (n > 0) {
+    k_scan_tiles<<<(int)ntiles, 256, 0, st>>>(n, cnt, tiles->as<int64_t>());
+    k_scan_sums<<<1, 1024, 0, st>>>(ntiles, tiles->as<int64_t>(), total_dev);
+    k_scan_apply<<<(int)ntiles, 256, 0, st>>>(n, cnt, tiles->as<int64_t>(), out);
+  } else {
+    HIPCHK(hipMemsetAsync(out, 0, sizeof(int64_t), st));
+    HIPCHK(hipMemsetAsync(total_dev, 0, sizeof(int64_t), st));
+  }
+  HIPCHK(hipGetLastError());
+  return CBG_OK;
+}
+
+cbg_status scan_counts(hipStream_t st, int64_t n, const int64_t* cnt, int64_t* out, int64_t* total_dev) {
+  DevBuf tiles;
+  CBGCHK(scan_counts_async(st, n, cnt, out, total_dev, &tiles));
+  HIPCHK(hipStreamSynchronize(st));   // tiles is released on return
+  return CBG_OK;
+}
+
+}  // namespace
+
+extern "C" cbg_status cbg_mis2_restriction(cbg_ctx* ctx, const cbg_dcsc_view* Gv, uint64_t seed, cbg_csc_result* R,
+                                           cbg_csc_result* RT, int64_t* nagg_out) {
+  if (!ctx || !Gv || !R) return CBG_EINVAL;
+  if (Gv->nrow != Gv->ncol) return CBG_EDIM;
+  HIPCHK(hipSetDevice(ctx->device));
+  hipStream_t st = ctx->stream;
+  DevBuf sb[5];
+  DevCsc<double> G;
+  CBGCHK(stage<double>(ctx, Gv, sb, &G));
+  const int64_t n = G.ncol;
+  if (n >= INT32_MAX) return CBG_EUNSUP;
+  DevBuf key, m1, m2, st8, fr, c1, c2, sc;
+  HIPCHK(key.reserve(8 * (n + 1)));
+  HIPCHK(m1.reserve(8 * (n + 1)));
+  HIPCHK(m2.reserve(8 * (n + 1)));
+  HIPCHK(st8.reserve(n + 1));
+  HIPCHK(fr.reserve(n + 1));
+  HIPCHK(c1.reserve(n + 1));
+  HIPCHK(c2.reserve(n + 1));
+  HIPCHK(sc.reserve(64));
+  const int g = (int)grid_for(n, 256, kMaxGrid * 4);
+  int8_t* state = st8.as<int8_t>();
+  unsigned long long* und = sc.as<unsigned long long>();
+  k_mis_keys<<<g, 256, 0, st>>>(n, seed, key.as<uint64_t>(), state);
+  for (int round = 0; n > 0; ++round) {
+    if (round > 4096) return CBG_EDEVICE;   // every round roots the largest undecided key: cannot happen
+    k_nbr_max<true><<<g, 256, 0, st>>>(n, G.cp, G.ir, key.as<uint64_t>(), state, 0, m1.as<uint64_t>());
+    k_nbr_max<false><<<g, 256, 0, st>>>(n, G.cp, G.ir, m1.as<uint64_t>(), state, 0, m2.as<uint64_t>());
+    k_mis_select<<<g, 256, 0, st>>>(n, key.as<uint64_t>(), m2.as<uint64_t>(), state, fr.as<uint8_t>());
+    k_nbr_or<<<g, 256, 0, st>>>(n, G.cp, G.ir, fr.as<uint8_t>(), c1.as<uint8_t>());
+    k_nbr_or<<<g, 256, 0, st>>>(n, G.cp, G.ir, c1.as<uint8_t>(), c2.as<uint8_t>());
+    HIPCHK(hipMemsetAsync(und, 0, 8, st));
+    k_mis_update<<<g, 256, 0, st>>>(n, fr.as<uint8_t>(), c2.as<uint8_t>(), state, und);
+    HIPCHK(hipGetLastError());
+    unsigned long long left = 0;
+    HIPCHK(hipMemcpyAsync(&left, und, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    if (left == 0) break;
+  }
+  // aggregates: nearest root within distance 1, else 2 (m1/m2 reused for the root-key maxima)
+  DevBuf rk, isr, rid, agg, cnt;
+  HIPCHK(rk.reserve(8 * (n + 1)));
+  HIPCHK(isr.reserve(8 * (n + 1)));
+  HIPCHK(rid.reserve(8 * (n + 1)));
+  HIPCHK(agg.reserve(4 * (n + 1)));
+  k_root_keys<<<g, 256, 0, st>>>(n, key.as<uint64_t>(), state, rk.as<uint64_t>(), isr.as<int64_t>());
+  k_nbr_max<false><<<g, 256, 0, st>>>(n, G.cp, G.ir, rk.as<uint64_t>(), state, 0, m1.as<uint64_t>());
+  k_nbr_max<false><<<g, 256, 0, st>>>(n, G.cp, G.ir, m1.as<uint64_t>(), state, 0, m2.as<uint64_t>());
+  HIPCHK(hipGetLastError());
+  CBGCHK(scan_counts(st, n, isr.as<int64_t>(), rid.as<int64_t>(), (int64_t*)(sc.as<char>() + 8)));
+  int64_t nagg = 0;
+  HIPCHK(hipMemcpy(&nagg, sc.as<char>() + 8, 8, hipMemcpyDeviceToHost));
+  HIPCHK(cnt.reserve(8 * (2 * nagg + 2)));
+  unsigned long long* colcnt = cnt.as<unsigned long long>();
+  unsigned long long* cursor = colcnt + nagg + 1;
+  HIPCHK(hipMemsetAsync(cnt.p, 0, 8 * (2 * nagg + 2), st));
+  k_assign<<<g, 256, 0, st>>>(n, m1.as<uint64_t>(), m2.as<uint64_t>(), rid.as<int64_t>(), agg.as<int32_t>(), colcnt);
+  HIPCHK(hipGetLastError());
+  // R (n x nagg): members of each aggregate, row-sorted by the duplicate-summing product (values 1)
+  DevBuf rawcp, rows;
+  HIPCHK(rawcp.reserve(8 * (nagg + 1)));
+  HIPCHK(rows.reserve(4 * (n + 1)));
+  CBGCHK(scan_counts(st, nagg, (const int64_t*)colcnt, rawcp.as<int64_t>(), (int64_t*)(sc.as<char>() + 16)));
+  if (nagg) HIPCHK(hipMemcpyAsync(cursor, rawcp.p, 8 * nagg, hipMemcpyDeviceToDevice, st));
+  k_scatter_members<<<g, 256, 0, st>>>(n, agg.as<int32_t>(), cursor, rows.as<int32_t>());
+  HIPCHK(hipGetLastError());
+  CBGCHK(dedup_columns(ctx, n, nagg, n, rawcp.as<int64_t>(), rows.as<int32_t>(), nullptr, R));
+  R->multiplies = 0;
+  if (RT) {   // R^T (nagg x n): column v holds the single row agg(v)
+    std::unique_ptr<Owner> own(new Owner(ctx->pool));
+    HIPCHK(own->cp.reserve(8 * (n + 1)));
+    HIPCHK(own->ir.reserve(4 * (n + 1)));
+    HIPCHK(own->val.reserve(8 * (n + 1)));
+    k_rt<<<(int)grid_for(n + 1, 256, kMaxGrid * 4), 256, 0, st>>>(n, agg.as<int32_t>(), own->cp.as<int64_t>(),
+                                                                  own->ir.as<int32_t>(), own->val.as<double>());
+    HIPCHK(hipGetLastError());
+    memset(RT, 0, sizeof(*RT));
+    RT->nrow = nagg; RT->ncol = n; RT->nnz = n;
+    RT->colptr = own->cp.as<int64_t>(); RT->row = own->ir.as<int32_t>(); RT->val = own->val.p;
+    RT->val_type = CBG_F64;
+    RT->_owner = own.release();
+  }
+  HIPCHK(hipStreamSynchronize(st));
+  if (nagg_out) *nagg_out = nagg;
+  return CBG_OK;
+}
+
+extern "C" cbg_status cbg_galerkin_rap(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_view* Rv,
+                                       cbg_csc_result* C) {
+  if (!ctx || !Av || !Rv || !C) return CBG_EINVAL;
+  if (Av->nrow != Av->ncol || Rv->nrow != Av->ncol) return CBG_EDIM;   // R^T A R: A square, R n x nagg
+  HIPCHK(hipSetDevice(ctx->device));
+  hipStream_t st = ctx->stream;
+  DevBuf sa[5], sr[5];
+  DevCsc<double> A, R;
+  CBGCHK(stage<double>(ctx, Av, sa, &A));
+  CBGCHK(stage<double>(ctx, Rv, sr, &R));
+  const int64_t n = A.ncol, nagg = R.ncol, nnzr = R.nnz;
+  // For an aggregation every column of A is one member, so the entries to reduce are exactly nnz(A):
+  // the scratch is sized up front and the aggregation check rides on the single read-back below.
+  const int64_t nraw = A.nnz;
+  DevBuf* w = ctx->gal;   // persistent workspace: no allocation on the hot path
+  HIPCHK(w[0].reserve(4 * (n + 1)));            // agg
+  HIPCHK(w[1].reserve(8 * (n + 1)));            // rv
+  HIPCHK(w[2].reserve(4 * (n + 1)));            // seen
+  HIPCHK(w[3].reserve(8 * (std::max(nnzr, nagg) + 1)));   // member lengths, then per-aggregate counts
+  HIPCHK(w[4].reserve(8 * (nnzr + 1)));         // member offsets
+  HIPCHK(w[5].reserve(12 * (nraw + 1)));        // scratch rows + values
+  HIPCHK(w[6].reserve(64));                     // [0] bad rows [1] raw total [2] overflow [3] nnz(C)
+  int32_t* agg = w[0].as<int32_t>();
+  double* rv = w[1].as<double>();
+  int64_t* len = w[3].as<int64_t>();
+  int64_t* moff = w[4].as<int64_t>();
+  double* tval = w[5].as<double>();
+  int32_t* trow = (int32_t*)(tval + nraw + 1);
+  int64_t* sc = w[6].as<int64_t>();
+  HIPCHK(hipMemsetAsync(w[2].p, 0, 4 * (n + 1), st));
+  HIPCHK(hipMemsetAsync(sc, 0, 64, st));
+  const int g = (int)grid_for(std::max(std::max(n, nagg), nnzr), 256, kMaxGrid * 4);
+  k_r_rows<<<g, 256, 0, st>>>(nagg, R.cp, R.ir, R.val, agg, rv, w[2].as<unsigned int>());
+  k_count_bad<<<g, 256, 0, st>>>(n, w[2].as<unsigned int>(), (unsigned long long*)sc);
+  k_member_len<<<g, 256, 0, st>>>(nnzr, R.ir, A.cp, len);
+  HIPCHK(hipGetLastError());
+  CBGCHK(scan_counts_async(st, nnzr, len, moff, sc + 1, &w[7]));
+  const int ga = (int)std::min<int64_t>(std::max<int64_t>(nagg, 1), 65536);
+  std::unique_ptr<Owner> own(new Owner(ctx->pool));
+  HIPCHK(own->cp.reserve(8 * (nagg + 1)));
+  if (nnzr == n) {
+    k_rap_agg<<<ga, 64, 0, st>>>(nagg, R.cp, R.ir, A.cp, A.ir, A.val, agg, rv, moff, len, trow, tval, nraw,
+                                 (unsigned long long*)(sc + 2));
+    HIPCHK(hipGetLastError());
+    CBGCHK(scan_counts_async(st, nagg, len, own->cp.as<int64_t>(), sc + 3, &w[7]));
+  }
+  int64_t h[4] = {0, 0, 0, 0};
+  HIPCHK(hipMemcpyAsync(h, sc, 32, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  if (nnzr != n || h[0] || h[1] != nraw) return CBG_EUNSUP;   // not an aggregation: two products instead
+  if (h[2]) return CBG_EUNSUP;   // an aggregate gathers more than kRapCap entries: two products instead
+  const int64_t nnzc = h[3];
+  HIPCHK(own->ir.reserve(4 * (nnzc + 1)));
+  HIPCHK(own->val.reserve(8 * (nnzc + 1)));
+  k_rap_compact<<<(int)grid_for(nagg * 16, 256, kMaxGrid * 4), 256, 0, st>>>(
+      nagg, R.cp, moff, own->cp.as<int64_t>(), trow, tval, own->ir.as<int32_t>(), own->val.as<double>());
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(st));
+  memset(C, 0, sizeof(*C));
+  C->nrow = nagg; C->ncol = nagg; C->nnz = nnzc;
+  C->colptr = own->cp.as<int64_t>(); C->row = own->ir.as<int32_t>(); C->val = own->val.p;
+  C->val_type = CBG_F64;
+  C->multiplies = nraw;   // one scaled copy per nonzero of A (the fused pass)
+  C->_owner = own.release();
+  return CBG_OK;
+}

@@ -33,11 +33,6 @@ inline double now_ms() {
     }                                                                                                  \
   } while (0)
 
-#define CBGCHK(x)                      \
-  do {                                 \
-    cbg_status s_ = (x);               \
-    if (s_ != CBG_OK) return s_;       \
-  } while (0)
 
 // count[c] = cp[c+1] - cp[c]
 __global__ void k_col_counts(int64_t n, const int64_t* __restrict__ cp, int64_t* __restrict__ cnt) {

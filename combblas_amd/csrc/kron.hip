@@ -16,7 +16,7 @@
 //                  column histogram;
 //   scan           column pointers of the raw (duplicated, unsorted) block;
 //   k_kron_scatter rows into their columns;
-//   I * Araw       the local hash SpGEMM with a pattern identity (PlusTimes<f64>, sorted columns):
+//   dedup_columns  I * Araw, the local hash SpGEMM with a pattern identity (spgemm_host.hpp):
 //                  duplicates of (row, col) sum to the multiplicity and every column comes out
 //                  row-sorted -- the SpTuples duplicate-summing constructor as one device product.
 #include "spgemm_host.hpp"
@@ -82,13 +82,6 @@ __global__ void k_kron_scatter(uint64_t n, const uint2* __restrict__ e, unsigned
   }
 }
 
-__global__ void k_identity(int64_t n, int64_t* __restrict__ cp, int32_t* __restrict__ ir) {
-  for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j <= n; j += (int64_t)gridDim.x * blockDim.x) {
-    cp[j] = j;
-    if (j < n) ir[j] = (int32_t)j;
-  }
-}
-
 }  // namespace
 
 extern "C" cbg_status cbg_rmat_block(cbg_ctx* ctx, int32_t scale, int32_t edgefactor, uint64_t seed, int64_t r0,
@@ -104,7 +97,7 @@ extern "C" cbg_status cbg_rmat_block(cbg_ctx* ctx, int32_t scale, int32_t edgefa
   std::vector<Mat> tab(kSkipBytes * 256);
   const Params p = make_params(seed, tab.data());
 
-  DevBuf dtab, edges, cnt, rows, icp, iir;
+  DevBuf dtab, edges, cnt, rows;
   HIPCHK(dtab.reserve(sizeof(Mat) * tab.size()));
   HIPCHK(hipMemcpyAsync(dtab.p, tab.data(), sizeof(Mat) * tab.size(), hipMemcpyHostToDevice, st));
   // in-block edges: the whole stream for a full block, about m * (nr/n) * (nc/n) * skew otherwise;
@@ -140,22 +133,8 @@ extern "C" cbg_status cbg_rmat_block(cbg_ctx* ctx, int32_t scale, int32_t edgefa
   if (nraw)
     k_kron_scatter<<<(int)grid_for((int64_t)nraw, 256, kMaxGrid), 256, 0, st>>>(nraw, edges.as<uint2>(), cursor,
                                                                                 rows.as<int32_t>());
-  HIPCHK(icp.reserve(sizeof(int64_t) * (nr + 1)));
-  HIPCHK(iir.reserve(sizeof(int32_t) * (nr + 1)));
-  k_identity<<<(int)grid_for(nr + 1, 256, kMaxGrid), 256, 0, st>>>(nr, icp.as<int64_t>(), iir.as<int32_t>());
-  HIPCHK(hipGetLastError());
-  // sum duplicates + row-sort every column: C = I * Araw over PlusTimes<double> with pattern operands.
-  // The raw block is the B operand: B's rows may come in any order and repeat (every B nonzero gathers
-  // one A column), whereas A's columns must be row-sorted (cbgpu.h views), which I's trivially are.
-  cbg_dcsc_view a{}, b{};
-  a.nrow = nr; a.ncol = nr; a.nnz = nr; a.nzc = nr;
-  a.cp = icp.p; a.ir = iir.p; a.idx_bytes = 4; a.ptr_bytes = 8; a.val = nullptr; a.val_type = CBG_F64;
-  a.on_device = 1;
-  b.nrow = nr; b.ncol = nc; b.nnz = (int64_t)nraw; b.nzc = nc;
-  b.cp = rawcp.p; b.ir = rows.p; b.idx_bytes = 4; b.ptr_bytes = 8; b.val = nullptr; b.val_type = CBG_F64;
-  b.on_device = 1;
-  int64_t mult = 0;
-  cbg_status s = cbg_dispatch_f64(ctx, &a, &b, CBG_SR_PLUS_TIMES, CBG_SORTED_COLS, out, &mult);
+  // sum duplicates + row-sort every column (the SpTuples duplicate-summing constructor)
+  cbg_status s = dedup_columns(ctx, nr, nc, (int64_t)nraw, rawcp.as<int64_t>(), rows.as<int32_t>(), nullptr, out);
   HIPCHK(hipStreamSynchronize(st));   // scratch above is released on return
   if (s == CBG_OK) out->multiplies = 0;
   return s;

@@ -28,6 +28,12 @@ using namespace cbg;
     }                                                                                               \
   } while (0)
 
+#define CBGCHK(x)                \
+  do {                           \
+    cbg_status s_ = (x);         \
+    if (s_ != CBG_OK) return s_; \
+  } while (0)
+
 namespace cbg { namespace host {
 
 // symbolic classes: wave T = 64..1024 words, block T = 2048..32768 words, then window
@@ -129,6 +135,7 @@ struct cbg_ctx {
   DevBuf nunits, segsz, segoff, useg, icnt, itemoff, items, parts, wide_win;
   DevBuf hrows, hmode, hpoff, urows;   // symbolic -> numeric row handoff of heavy columns
   DevBuf oitems;                       // heavy items the rows-known kernel does not take
+  DevBuf gal[8];                       // fused Galerkin product scratch (galerkin.hip)
   int ncu = 0;                         // compute units (persistent grids)
   int row_handoff = -1;                // -1: read CBG_ROW_HANDOFF once (default on)
 };
@@ -789,3 +796,39 @@ CBG_DECLARE_DT(f32)
 CBG_DECLARE_DT(i64)
 CBG_DECLARE_DT(i32)
 CBG_DECLARE_DT(b8)
+
+// ------------------------------------------------------------------------------ duplicate summing
+// A raw CSC whose columns hold rows in any order, repeated (values optional: NULL = 1) becomes a proper
+// CSC -- duplicates of (row, col) summed, every column row-sorted -- as one device product
+// C = I * Raw over PlusTimes<double>: each Raw nonzero gathers the single entry of one identity
+// column, so the hash accumulates the duplicates in Raw's storage order (deterministic).  This is the
+// SpTuples duplicate-summing constructor (SpTuples.cpp:66-115) on the device; used by the input
+// builders (kron.hip) and the fused Galerkin product (galerkin.hip).
+static __global__ void k_identity_csc(int64_t n, int64_t* __restrict__ cp, int32_t* __restrict__ ir) {
+  for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j <= n; j += (int64_t)gridDim.x * blockDim.x) {
+    cp[j] = j;
+    if (j < n) ir[j] = (int32_t)j;
+  }
+}
+
+inline cbg_status dedup_columns(cbg_ctx* ctx, int64_t nr, int64_t nc, int64_t nnz, const int64_t* cp,
+                                const int32_t* rows, const double* val, cbg_csc_result* out) {
+  hipStream_t st = ctx->stream;
+  DevBuf icp, iir;
+  HIPCHK(icp.reserve(sizeof(int64_t) * (nr + 1)));
+  HIPCHK(iir.reserve(sizeof(int32_t) * (nr + 1)));
+  k_identity_csc<<<(int)grid_for(nr + 1, 256, kMaxGrid), 256, 0, st>>>(nr, icp.as<int64_t>(), iir.as<int32_t>());
+  HIPCHK(hipGetLastError());
+  // I is A (columns trivially row-sorted, as views require); Raw is B, whose rows may come in any order
+  cbg_dcsc_view a{}, b{};
+  a.nrow = nr; a.ncol = nr; a.nnz = nr; a.nzc = nr;
+  a.cp = icp.p; a.ir = iir.p; a.idx_bytes = 4; a.ptr_bytes = 8; a.val = nullptr; a.val_type = CBG_F64;
+  a.on_device = 1;
+  b.nrow = nr; b.ncol = nc; b.nnz = nnz; b.nzc = nc;
+  b.cp = cp; b.ir = rows; b.idx_bytes = 4; b.ptr_bytes = 8; b.val = val; b.val_type = CBG_F64;
+  b.on_device = 1;
+  int64_t mult = 0;
+  cbg_status s = cbg_dispatch_f64(ctx, &a, &b, CBG_SR_PLUS_TIMES, CBG_SORTED_COLS, out, &mult);
+  HIPCHK(hipStreamSynchronize(st));   // the identity above is released on return
+  return s;
+}

@@ -85,48 +85,59 @@ def poisson3d(k):
     return n, cp, ir, val
 
 
+def mis_keys(n, seed):
+    """Distinct nonzero 64-bit priorities of vertices 0..n-1 (the device's mis_key, galerkin.hip): a
+    seeded splitmix64 hash in the high 32 bits, the vertex id in the low 32 bits, plus one."""
+    M = (1 << 64) - 1
+    v = np.arange(n, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        z = v ^ np.uint64((seed * 0x9E3779B97F4A7C15) & M)
+        z = z + np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(31))
+        return ((z >> np.uint64(32)) << np.uint64(32) | v) + np.uint64(1)
+
+
 def aggregation_restriction(n, cp, ir, seed=1):
     """(nagg, colptr, rows, vals) of R (n x nagg): MIS-2 aggregation of the graph of a symmetric CSC,
-    the shape RestrictionOp.h:116-427 builds.  Vectorised Luby-style rounds: an undecided vertex
-    whose random priority is the largest among the undecided vertices within distance 2 becomes a
-    root, and its distance-2 neighbourhood is decided; then every vertex joins the highest-priority
-    root within distance 1, else within distance 2.  R[i, agg(i)] = 1."""
+    the shape RestrictionOp.h:116-290 builds; host restatement of cbg_mis2_restriction (galerkin.hip),
+    same priorities (mis_keys), same rounds, same aggregate numbering.  Luby rounds: an undecided vertex
+    whose key is the largest among the undecided vertices within distance 2 becomes a root, and its
+    distance-2 neighbourhood is decided; then every vertex joins the highest-key root within distance 1,
+    else within distance 2.  R[i, agg(i)] = 1; aggregates numbered in root-vertex order."""
     import scipy.sparse as sp
     G = sp.csr_matrix((np.ones(len(ir)), ir, cp), shape=(n, n))
     G = G + sp.identity(n, format="csr")
     G2 = (G @ G).tocsr()
     G.sort_indices()
     G2.sort_indices()
-    rng = np.random.default_rng(seed)
-    prio = rng.permutation(n).astype(np.int64) + 1      # distinct priorities
+    prio = mis_keys(n, seed)
     state = np.zeros(n, np.int8)                        # 0 undecided, 1 root, 2 covered
 
     def rowmax(M, v):
-        out = np.zeros(M.shape[0], np.int64)
+        out = np.zeros(M.shape[0], np.uint64)
         nz = np.diff(M.indptr) > 0
         if M.nnz:
             out[nz] = np.maximum.reduceat(v[M.indices], M.indptr[:-1][nz])
         return out
 
     while (state == 0).any():
-        p = np.where(state == 0, prio, 0)
+        p = np.where(state == 0, prio, np.uint64(0))
         m2 = rowmax(G2, p)
         new = (state == 0) & (p == m2)
         state[new] = 1
         covered = (G2 @ new.astype(np.float64)) > 0
         state[(state == 0) & covered] = 2
-    roots = np.nonzero(state == 1)[0]
-    rid = np.full(n, -1, np.int64)
-    rid[roots] = np.arange(len(roots))
-    rp = np.where(state == 1, prio, 0)
+    isroot = state == 1
+    rid = np.cumsum(isroot) - isroot                    # root ids in vertex order
+    rp = np.where(isroot, prio, np.uint64(0))
     agg = np.full(n, -1, np.int64)
     for M in (G, G2):                                   # nearest: distance 1, then 2
         best = rowmax(M, rp)
         undone = (agg < 0) & (best > 0)
-        inv = np.zeros(n + 1, np.int64)
-        inv[prio[roots]] = rid[roots]
-        agg[undone] = inv[best[undone]]
+        agg[undone] = rid[((best[undone] - np.uint64(1)) & np.uint64(0xFFFFFFFF)).astype(np.int64)]
     assert (agg >= 0).all()
-    nagg = len(roots)
+    nagg = int(isroot.sum())
     rcp, rir, rval = _csc_from_coo(n, nagg, np.arange(n), agg, np.ones(n))
     return nagg, rcp, rir, rval

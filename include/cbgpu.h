@@ -17,6 +17,8 @@
  *   cbg_mcl_prune      MCLPruneRecoverySelect(A, thr, select, recover, pct, kselectVersion)
  *                                                                        include/CombBLAS/ParFriends.h:185-353
  *                      (Kselect1 SpParMat.cpp:1413-1700, PruneColumn SpParMat.cpp:2567-2720)
+ *   cbg_mis2_restriction MIS2 + RestrictionOp                            3DSpGEMM/RestrictionOp.h:116-290
+ *   cbg_galerkin_rap   R^T A R (RestrictionOp.cpp:188-196's two products, fused for aggregation R)
  *   cbg_col_range      SpDCCols::ColSplit (one piece)                    include/CombBLAS/SpDCCols.cpp:927-1086
  *   cbg_col_concat     SpDCCols::ColConcatenate                          include/CombBLAS/SpDCCols.cpp:1087-1185
  *   cbg_col_select     SubsRef_SR column form on one block               include/CombBLAS/SpParMat.cpp:2251-2422
@@ -214,6 +216,21 @@ cbg_status cbg_col_select(cbg_ctx* ctx, const cbg_csc_result* in, const int64_t*
                           cbg_csc_result* out);
 /* Horizontal concatenation of nparts device CSCs with equal nrow/val_type. */
 cbg_status cbg_col_concat(cbg_ctx* ctx, const cbg_csc_result* parts, int32_t nparts, cbg_csc_result* out);
+
+/*
+ * Galerkin coarse operator (BASELINE config 5; 3DSpGEMM/RestrictionOp.h:116-290, RestrictionOp.cpp:155-196).
+ *
+ * cbg_mis2_restriction: MIS-2 of the graph G (square, symmetric, pattern; self loops ignored) by Luby
+ *   rounds with seeded distinct priorities, then every vertex joins the highest-priority set vertex
+ *   within distance 1, else 2: R (n x nagg, R(i, agg(i)) = 1, columns row-sorted) and, if RT is not
+ *   NULL, R^T (nagg x n).  Aggregates are numbered in the order of their root vertices.
+ * cbg_galerkin_rap: C = R^T A R in one pass for an aggregation R (exactly one nonzero per row of R, any
+ *   value; otherwise CBG_EUNSUP -- use two cbg_spgemm_local products), PlusTimes<double>, row-sorted.
+ *   C.multiplies = nnz(A) (one scaled copy per nonzero of A).
+ */
+cbg_status cbg_mis2_restriction(cbg_ctx* ctx, const cbg_dcsc_view* G, uint64_t seed, cbg_csc_result* R,
+                                cbg_csc_result* RT, int64_t* nagg);
+cbg_status cbg_galerkin_rap(cbg_ctx* ctx, const cbg_dcsc_view* A, const cbg_dcsc_view* R, cbg_csc_result* C);
 
 /*
  * ---------------------------------------------------------------------------------------------

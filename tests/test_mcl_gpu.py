@@ -176,3 +176,99 @@ def test_galerkin_large_vs_oracle(gpu_ctx):
     OC, _, _ = oracle_spgemm(ORA, R, "plus_times", "f64")
     assert_same_product(RAh, ORA, "f64", what="RtA")   # small integer sums: exact in f64
     assert_same_product(host(C, nagg), OC, "f64", what="RtAR")
+
+
+def _random_symmetric(n, density, seed):
+    import scipy.sparse as sp
+    M = sp.random(n, n, density=density, format="csr", random_state=np.random.default_rng(seed))
+    M = ((M + M.T) > 0).astype(np.float64).tocsc()
+    M.setdiag(0)
+    M.eliminate_zeros()
+    M.sort_indices()
+    return Csc(n, n, M.indptr, M.indices, M.data)
+
+
+@pytest.mark.parametrize("kind,seed", [("poisson24", 1), ("poisson24", 9), ("random", 3), ("isolated", 5)])
+def test_restriction_matches_host(gpu_ctx, kind, seed):
+    """cbg_mis2_restriction (device MIS-2 + aggregation, RestrictionOp.h:116-290) equals the host
+    restatement (inputs.aggregation_restriction) exactly: same roots, same aggregates, same R; RT = R^T."""
+    if kind == "poisson24":
+        n, cp, ir, val = poisson3d(24)
+        G = Csc(n, n, cp, ir, val)
+    elif kind == "random":
+        G = _random_symmetric(6000, 6e-4, seed)
+    else:   # isolated vertices (empty columns) each become their own aggregate
+        G = _random_symmetric(3000, 1e-4, seed)
+    nagg, rcp, rir, rval = aggregation_restriction(G.nrow, G.cp, G.ir, seed=seed)
+    R, RT = cb.RestrictionOp(up(gpu_ctx, G), seed=seed)
+    Rh = host(R, G.nrow)
+    assert R.getncol() == nagg
+    assert np.array_equal(Rh.cp, rcp) and np.array_equal(Rh.ir, rir) and np.array_equal(Rh.val, rval)
+    RTh = host(RT, nagg)
+    T = _transpose(Csc(G.nrow, nagg, rcp, rir, rval))
+    assert np.array_equal(RTh.cp, T.cp) and np.array_equal(RTh.ir, T.ir) and np.array_equal(RTh.val, T.val)
+
+
+def test_galerkin_rap_fused_matches_reference(gpu_ctx):
+    """The fused one-pass R^T A R equals the reference's two-product output (golden/galerkin.npz)."""
+    z = load_fixture("galerkin")
+    n, nagg = (int(x) for x in z["R_shape"])
+    A = Csc(n, n, z["A_cp"], z["A_ir"], z["A_val"])
+    R = Csc(n, nagg, z["R_cp"], z["R_ir"], z["R_val"])
+    C = cb.GalerkinRAP(up(gpu_ctx, A), up(gpu_ctx, R))
+    assert C.multiplies == A.nnz
+    assert_same_product(host(C, nagg), Csc(nagg, nagg, z["C_cp"], z["C_ir"], z["C_val"]), "f64", what="fused RtAR")
+
+
+@pytest.mark.parametrize("k,seed", [(24, 9), (40, 2)])
+def test_galerkin_rap_fused_vs_two_products(gpu_ctx, k, seed):
+    """Device R, then the fused product against the two device SpGEMMs and the oracle's two products
+    (f64 within 1e-12 of sum|r a r|; weighted R rows exercise the value scaling)."""
+    n, acp, air, aval = poisson3d(k)
+    dA = up(gpu_ctx, Csc(n, n, acp, air, aval))
+    R, RT = cb.RestrictionOp(dA, seed=seed)
+    Rh = host(R, n)
+    nagg = R.getncol()
+    w = 0.5 + (np.arange(Rh.nnz) % 7) / 8.0           # a weighted aggregation (one nonzero per row)
+    Rw = Csc(n, nagg, Rh.cp, Rh.ir, w)
+    for Rc in (Rh, Rw):
+        dR = up(gpu_ctx, Rc)
+        C = cb.GalerkinRAP(dA, dR)
+        Rt = _transpose(Rc)
+        two = cb.LocalSpGEMMHash(PT, cb.LocalSpGEMMHash(PT, up(gpu_ctx, Rt), dA), dR)
+        ORA, _, _ = oracle_spgemm(Rt, Csc(n, n, acp, air, aval), "plus_times", "f64")
+        OC, _, _ = oracle_spgemm(ORA, Rc, "plus_times", "f64")
+        assert_same_product(host(C, nagg), OC, "f64", what="fused vs oracle")
+        assert_same_product(host(C, nagg), host(two, nagg), "f64", what="fused vs two products")
+
+
+def test_galerkin_rap_rejects_non_aggregation(gpu_ctx):
+    n = 50
+    A = Csc(n, n, np.arange(n + 1), np.arange(n), np.ones(n))
+    # row 0 in two aggregates
+    R = Csc(n, 2, np.array([0, 26, 51]), np.r_[np.arange(26), 0, np.arange(26, 50)], np.ones(51))
+    with pytest.raises(cb.CbgError) as ei:
+        cb.GalerkinRAP(up(gpu_ctx, A), up(gpu_ctx, R))
+    assert ei.value.status == 11
+
+
+def test_galerkin_rap_large_aggregate_falls_back(gpu_ctx):
+    """An aggregate gathering more than 512 entries of A: the fused kernel declines (CBG_EUNSUP) and,
+    given RT, GalerkinRAP runs the reference's two products."""
+    G = _random_symmetric(400, 0.02, 4)
+    n = G.nrow
+    A = Csc(n, n, G.cp, G.ir, np.linspace(0.5, 1.5, G.nnz))
+    agg = np.r_[np.zeros(300, np.int64), 1 + np.arange(100) % 7]     # aggregate 0 holds 300 vertices
+    import scipy.sparse as sp
+    Rs = sp.csc_matrix((np.ones(n), (np.arange(n), agg)), shape=(n, 8))
+    Rs.sort_indices()
+    R = Csc(n, 8, Rs.indptr, Rs.indices, Rs.data)
+    dA, dR, dRT = up(gpu_ctx, A), up(gpu_ctx, R), up(gpu_ctx, _transpose(R))
+    with pytest.raises(cb.CbgError) as ei:
+        cb.GalerkinRAP(dA, dR)
+    assert ei.value.status == 11
+    C = cb.GalerkinRAP(dA, dR, dRT)
+    Rt = _transpose(R)
+    ORA, _, _ = oracle_spgemm(Rt, A, "plus_times", "f64")
+    OC, _, _ = oracle_spgemm(ORA, R, "plus_times", "f64")
+    assert_same_product(host(C, 8), OC, "f64", what="fallback RtAR")
