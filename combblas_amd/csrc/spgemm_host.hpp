@@ -735,6 +735,162 @@ static __global__ void k_merge_selector(int64_t ncol, int32_t k, int64_t* __rest
   }
 }
 
+// ---- two-way merge of column-sorted partials (the 1x1x2 fiber merge, the q = 2 stage merges) ----
+// One wave per column walks both sorted columns in windows of 64 merged positions: the window's rows
+// are staged in LDS (pads: INT32_MAX), lane l finds merged position l by a merge-path search (ties take
+// part 0 first, so a duplicate row is a (part 0, part 1) pair at adjacent positions), heads of equal-row
+// runs are ranked by ballot, and a window never ends between the two halves of a pair.  Count pass ->
+// nnz per column; fill pass -> rows and values at the scanned offsets.  Duplicates combine as
+// MultiwayMergeHash does (MultiwayMerge.h:357, SR::add in part order): PlusTimes sums (bool: OR), MinPlus
+// min, SelectMax max, Select2nd keeps part 0's value; BoolCopy1st/2nd count them as an error (CBG_EADD).
+template <int SRI, typename V>
+__device__ __forceinline__ V merge_pair(V a, V b) {
+  if constexpr (SRI == SR_PLUS_TIMES) {
+    if constexpr (sizeof(V) == 1) return (V)((a != 0) | (b != 0));
+    else return a + b;
+  } else if constexpr (SRI == SR_MIN_PLUS) {
+    return b < a ? b : a;
+  } else if constexpr (SRI == SR_SELECT_MAX || SRI == SR_SELECT_MAX_BOOL) {
+    return b > a ? b : a;
+  } else {
+    return a;
+  }
+}
+
+template <int SRI, typename V, bool FILL>
+__global__ void __launch_bounds__(256) k_merge2(int64_t ncol, const int64_t* __restrict__ acp,
+                                                const int32_t* __restrict__ air, const V* __restrict__ aval,
+                                                const int64_t* __restrict__ bcp, const int32_t* __restrict__ bir,
+                                                const V* __restrict__ bval, int64_t* __restrict__ cnt,
+                                                const int64_t* __restrict__ ccp, int32_t* __restrict__ crow,
+                                                V* __restrict__ cval, unsigned long long* __restrict__ dups,
+                                                unsigned long long* __restrict__ disorder) {
+  __shared__ int32_t swin[4][2][kWave];
+  const int w = threadIdx.x / kWave, l = lane_id();
+  int32_t* sa = swin[w][0];
+  int32_t* sb = swin[w][1];
+  const uint64_t below = (1ull << l) - 1;
+  for (int64_t j = (int64_t)blockIdx.x * 4 + w; j < ncol; j += (int64_t)gridDim.x * 4) {
+    int64_t ia = acp[j], ib = bcp[j];
+    const int64_t ea = acp[j + 1], eb = bcp[j + 1];
+    int64_t o = FILL ? ccp[j] : 0;
+    unsigned long long nd = 0, bad = 0;
+    const int64_t a0 = ia, b0 = ib;
+    while (ia < ea || ib < eb) {   // wave-uniform
+      sa[l] = ia + l < ea ? air[ia + l] : INT32_MAX;
+      sb[l] = ib + l < eb ? bir[ib + l] : INT32_MAX;
+      wave_sync();
+      if (!FILL) {   // the merge needs strictly ascending rows per column: verify in the count pass
+        const int32_t pa = l > 0 ? sa[l - 1] : (ia > a0 ? air[ia - 1] : -1);
+        const int32_t pb = l > 0 ? sb[l - 1] : (ib > b0 ? bir[ib - 1] : -1);
+        bad += (ia + l < ea && sa[l] <= pa) || (ib + l < eb && sb[l] <= pb);
+      }
+      int lo = l > kWave ? l - kWave : 0, hi = l < kWave ? l : kWave;   // part-0 elements among positions < l
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (sa[mid] <= sb[l - 1 - mid]) lo = mid + 1; else hi = mid;
+      }
+      const int i = lo, jb = l - lo;
+      const bool take_a = i < kWave && (jb >= kWave || sa[i] <= sb[jb]);
+      const int32_t row = take_a ? sa[i] : sb[jb];
+      const bool valid = row != INT32_MAX;
+      const bool pair = take_a && valid && jb < kWave && sb[jb] == row;   // part 1 holds the same row next
+      const int32_t prev = __shfl_up(row, 1, kWave);
+      const bool head = valid && (l == 0 || prev != row);
+      // a pair must not straddle windows: drop position 63 when it is the part-0 half of a pair
+      const int K = __shfl(pair ? kWave - 1 : kWave, kWave - 1, kWave);
+      const bool in = l < K && valid;
+      const uint64_t hm = __ballot(head && in);
+      const uint64_t am = __ballot(take_a && in);
+      const uint64_t bm = __ballot(!take_a && in);
+      if (FILL && head && in) {
+        const int64_t pos = o + __popcll(hm & below);
+        V v = take_a ? (aval ? aval[ia + i] : V(1)) : (bval ? bval[ib + jb] : V(1));
+        if (pair) v = merge_pair<SRI, V>(v, bval ? bval[ib + jb] : V(1));
+        crow[pos] = row;
+        cval[pos] = v;
+      }
+      if (!FILL && pair && in) ++nd;
+      o += __popcll(hm);
+      ia += __popcll(am);
+      ib += __popcll(bm);
+      wave_sync();
+    }
+    if (!FILL) {
+      const unsigned long long d = (unsigned long long)wave_sum64((int64_t)nd);
+      const unsigned long long x = (unsigned long long)wave_sum64((int64_t)bad);
+      if (l == 0) {
+        cnt[j] = o;
+        if (d) atomicAdd(dups, d);
+        if (x) atomicAdd(disorder, x);
+      }
+    }
+  }
+}
+
+template <int SRI, typename V>
+cbg_status merge2_sr(cbg_ctx* ctx, const cbg_csc_result* parts, cbg_csc_result* C) {
+  hipStream_t st = ctx->stream;
+  const int64_t ncol = parts[0].ncol;
+  const bool add_is_error = SRI == SR_BOOL_COPY1ST || SRI == SR_BOOL_COPY2ND;
+  std::unique_ptr<Owner> own(new Owner(ctx->pool));
+  PoolBuf cnt, tiles;
+  cnt.pool = tiles.pool = ctx->pool;
+  HIPCHK(own->cp.reserve(8 * (ncol + 1)));
+  HIPCHK(cnt.reserve(8 * (ncol + 1)));
+  const int64_t ntiles = (ncol + kScanTile - 1) / kScanTile;
+  HIPCHK(tiles.reserve(8 * (ntiles + 1)));
+  HIPCHK(ctx->scalars.reserve(256));
+  unsigned long long* sc = ctx->scalars.as<unsigned long long>();
+  HIPCHK(hipMemsetAsync(sc, 0, 24, st));
+  const int g = (int)grid_for(ncol, 4, kMaxGrid * 8);
+  const V* av = (const V*)parts[0].val;
+  const V* bv = (const V*)parts[1].val;
+  k_merge2<SRI, V, false><<<g, 256, 0, st>>>(ncol, parts[0].colptr, parts[0].row, av, parts[1].colptr, parts[1].row,
+                                             bv, cnt.as<int64_t>(), nullptr, nullptr, nullptr, sc, sc + 2);
+  if (ncol > 0) {
+    k_scan_tiles<<<(int)ntiles, 256, 0, st>>>(ncol, cnt.as<int64_t>(), tiles.as<int64_t>());
+    k_scan_sums<<<1, 1024, 0, st>>>(ntiles, tiles.as<int64_t>(), (int64_t*)(sc + 1));
+    k_scan_apply<<<(int)ntiles, 256, 0, st>>>(ncol, cnt.as<int64_t>(), tiles.as<int64_t>(), own->cp.as<int64_t>());
+  } else {
+    HIPCHK(hipMemsetAsync(own->cp.p, 0, 8, st));
+  }
+  HIPCHK(hipGetLastError());
+  unsigned long long h[3] = {0, 0, 0};   // duplicate pairs, nnz(C), columns out of row order
+  HIPCHK(hipMemcpyAsync(h, sc, 24, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  if (h[2]) return CBG_EINVAL;   // a partial is not row-sorted: the caller takes the hash merge
+  if (add_is_error && h[0]) return CBG_EADD;   // BoolCopy add() would have been called (it throws)
+  const int64_t nnz = (int64_t)h[1];
+  HIPCHK(own->ir.reserve(4 * (nnz + 1)));
+  HIPCHK(own->val.reserve(sizeof(V) * (nnz + 1)));
+  k_merge2<SRI, V, true><<<g, 256, 0, st>>>(ncol, parts[0].colptr, parts[0].row, av, parts[1].colptr, parts[1].row, bv,
+                                            nullptr, own->cp.as<int64_t>(), own->ir.as<int32_t>(), own->val.as<V>(),
+                                            nullptr, nullptr);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(st));   // cnt / tiles go back to the pool on return
+  memset(C, 0, sizeof(*C));
+  C->nrow = parts[0].nrow; C->ncol = ncol; C->nnz = nnz;
+  C->colptr = own->cp.as<int64_t>(); C->row = own->ir.as<int32_t>(); C->val = own->val.p;
+  C->val_type = DtOf<V>::value;
+  C->_owner = own.release();
+  return CBG_OK;
+}
+
+template <typename V>
+cbg_status merge2(cbg_ctx* ctx, const cbg_csc_result* parts, cbg_semiring sr, cbg_csc_result* C) {
+  switch (sr) {
+    case CBG_SR_PLUS_TIMES: return merge2_sr<SR_PLUS_TIMES, V>(ctx, parts, C);
+    case CBG_SR_MIN_PLUS: return merge2_sr<SR_MIN_PLUS, V>(ctx, parts, C);
+    case CBG_SR_SELECT2ND: return merge2_sr<SR_SELECT2ND, V>(ctx, parts, C);
+    case CBG_SR_SELECT_MAX: return merge2_sr<SR_SELECT_MAX, V>(ctx, parts, C);
+    case CBG_SR_SELECT_MAX_BOOL: return merge2_sr<SR_SELECT_MAX_BOOL, V>(ctx, parts, C);
+    case CBG_SR_BOOL_COPY1ST: return merge2_sr<SR_BOOL_COPY1ST, V>(ctx, parts, C);
+    case CBG_SR_BOOL_COPY2ND: return merge2_sr<SR_BOOL_COPY2ND, V>(ctx, parts, C);
+  }
+  return CBG_EUNSUP;
+}
+
 template <typename V>
 cbg_status merge_impl(cbg_ctx* ctx, const cbg_csc_result* parts, int32_t k, cbg_semiring sr, uint32_t flags,
                       cbg_csc_result* C) {
@@ -745,9 +901,18 @@ cbg_status merge_impl(cbg_ctx* ctx, const cbg_csc_result* parts, int32_t k, cbg_
     if (parts[l].val_type != DtOf<V>::value) return CBG_EINVAL;
     tot += parts[l].nnz;
   }
+  // two partials (every mandated layout's merges): the dedicated two-way merge; it verifies that the
+  // partials' columns are row-sorted and declines (CBG_EINVAL) otherwise, then the hash merge below runs
+  if (k == 2 && std::getenv("CBG_MERGE_PRODUCT") == nullptr) {
+    const cbg_status s2 = merge2<V>(ctx, parts, sr, C);
+    if (s2 != CBG_EINVAL) return s2;
+  }
   if ((int64_t)k * ncol >= INT32_MAX) return CBG_EUNSUP;
   hipStream_t st = ctx->stream;
-  DevBuf cat_cp, cat_ir, cat_val, sel_cp, sel_ir;
+  // scratch from the context's caching pool (a fresh hipMalloc/hipFree pair per merge costs more than a
+  // small merge; hipFree also synchronises the device)
+  PoolBuf cat_cp, cat_ir, cat_val, sel_cp, sel_ir;
+  cat_cp.pool = cat_ir.pool = cat_val.pool = sel_cp.pool = sel_ir.pool = ctx->pool;
   HIPCHK(cat_cp.reserve(sizeof(int64_t) * (k * ncol + 1)));
   HIPCHK(cat_ir.reserve(sizeof(int32_t) * (tot + 1)));
   HIPCHK(cat_val.reserve(sizeof(V) * (tot + 1)));
@@ -777,7 +942,7 @@ cbg_status merge_impl(cbg_ctx* ctx, const cbg_csc_result* parts, int32_t k, cbg_
   b.val_type = DtOf<V>::value; b.on_device = 1;
   int64_t m = 0;
   cbg_status s = dispatch_sr<V, true>(ctx, &a, &b, sr, flags, C, &m);
-  HIPCHK(hipStreamSynchronize(st));   // the DevBufs above are released on return
+  HIPCHK(hipStreamSynchronize(st));   // the scratch above goes back to the pool on return
   return s;
 }
 
