@@ -440,6 +440,18 @@ def run_rmat_case(rank, world, port, backend_kind, cases, errq):
         be = cbd.GpuBackend(cb.Context(0)) if backend_kind.startswith("gpu") else ScipyBackend()
         from helpers import fixture_product, load_fixture
         for (name, scale) in cases:
+            if name == "single-gpu":   # no fixture: the layouts against the one-GPU product of the same matrix
+                Ad = cbd.SpParMat3D.from_rmat(grid, scale, 16, cb.G500_SEED, True, be)
+                Bd = cbd.SpParMat3D.from_rmat(grid, scale, 16, cb.G500_SEED, False, be)
+                C = cbd.Mult_AnXBn_SUMMA3D(cb.PlusTimesSRing("f64"), Ad, Bd)
+                M = be.ctx.generate_rmat(scale, 16, seed=cb.G500_SEED)
+                P = cb.LocalSpGEMMHash(cb.PlusTimesSRing("f64"), M, M)
+                cp, ir, val = P.to_host()
+                P.free()
+                M.free()
+                n = 1 << scale
+                check_piece_exact_or_f64(C, sp.csc_matrix((val, ir, cp), shape=(n, n)), rank, f"s{scale} C piece")
+                continue
             z = load_fixture(name)
             G = sp.csc_matrix((z["A_val"], z["A_ir"], z["A_cp"]), shape=tuple(z["A_shape"]))
             Ad = cbd.SpParMat3D.from_rmat(grid, scale, 16, cb.G500_SEED, True, be)

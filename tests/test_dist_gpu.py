@@ -68,9 +68,10 @@ def test_rccl_native_grid_single_rank():
 @pytest.mark.parametrize("world,port", [(2, 29641), (4, 29642), (8, 29643)])
 def test_rmat_pieces_built_per_rank_gloo_gpu(world, port):
     """Each rank's A/B pieces built on the device by cbg_rmat_block equal the reference-generated G500
-    fixture blocks (s10, s12), and the 1x1x2 / 2x2 / 2x2x2 products of them equal the reference's."""
+    fixture blocks (s10, s12), and the 1x1x2 / 2x2 / 2x2x2 products of them equal the reference's; at s16
+    every layout's pieces equal the same blocks of the one-GPU product (bit-exact: multiplicity values)."""
     from dist_support import run_rmat_case
-    spawn_case(world, "gpu", [("g500_s10", 10), ("g500_s12", 12)], port, body=run_rmat_case)
+    spawn_case(world, "gpu", [("g500_s10", 10), ("g500_s12", 12), ("single-gpu", 16)], port, body=run_rmat_case)
 
 
 @pytest.mark.parametrize("world,port", [(2, 29651), (4, 29652), (8, 29653)])
