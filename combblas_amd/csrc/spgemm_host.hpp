@@ -757,6 +757,12 @@ __device__ __forceinline__ V merge_pair(V a, V b) {
   }
 }
 
+#ifndef CBG_MERGE_PL
+#define CBG_MERGE_PL 4   // merged positions per lane per window (window = 64 * CBG_MERGE_PL)
+#endif
+constexpr int kMergePL = CBG_MERGE_PL;
+constexpr int kMergeW = kWave * kMergePL;
+
 template <int SRI, typename V, bool FILL>
 __global__ void __launch_bounds__(256) k_merge2(int64_t ncol, const int64_t* __restrict__ acp,
                                                 const int32_t* __restrict__ air, const V* __restrict__ aval,
@@ -765,11 +771,11 @@ __global__ void __launch_bounds__(256) k_merge2(int64_t ncol, const int64_t* __r
                                                 const int64_t* __restrict__ ccp, int32_t* __restrict__ crow,
                                                 V* __restrict__ cval, unsigned long long* __restrict__ dups,
                                                 unsigned long long* __restrict__ disorder) {
-  __shared__ int32_t swin[4][2][kWave];
+  constexpr int W = kMergeW, PL = kMergePL;
+  __shared__ int32_t swin[4][2][W];
   const int w = threadIdx.x / kWave, l = lane_id();
   int32_t* sa = swin[w][0];
   int32_t* sb = swin[w][1];
-  const uint64_t below = (1ull << l) - 1;
   for (int64_t j = (int64_t)blockIdx.x * 4 + w; j < ncol; j += (int64_t)gridDim.x * 4) {
     int64_t ia = acp[j], ib = bcp[j];
     const int64_t ea = acp[j + 1], eb = bcp[j + 1];
@@ -777,43 +783,80 @@ __global__ void __launch_bounds__(256) k_merge2(int64_t ncol, const int64_t* __r
     unsigned long long nd = 0, bad = 0;
     const int64_t a0 = ia, b0 = ib;
     while (ia < ea || ib < eb) {   // wave-uniform
-      sa[l] = ia + l < ea ? air[ia + l] : INT32_MAX;
-      sb[l] = ib + l < eb ? bir[ib + l] : INT32_MAX;
+#pragma unroll
+      for (int r = 0; r < PL; ++r) {
+        const int x = l + r * kWave;
+        sa[x] = ia + x < ea ? air[ia + x] : INT32_MAX;
+        sb[x] = ib + x < eb ? bir[ib + x] : INT32_MAX;
+      }
       wave_sync();
       if (!FILL) {   // the merge needs strictly ascending rows per column: verify in the count pass
-        const int32_t pa = l > 0 ? sa[l - 1] : (ia > a0 ? air[ia - 1] : -1);
-        const int32_t pb = l > 0 ? sb[l - 1] : (ib > b0 ? bir[ib - 1] : -1);
-        bad += (ia + l < ea && sa[l] <= pa) || (ib + l < eb && sb[l] <= pb);
+#pragma unroll
+        for (int r = 0; r < PL; ++r) {
+          const int x = l + r * kWave;
+          const int32_t pa = x > 0 ? sa[x - 1] : (ia > a0 ? air[ia - 1] : -1);
+          const int32_t pb = x > 0 ? sb[x - 1] : (ib > b0 ? bir[ib - 1] : -1);
+          bad += (ia + x < ea && sa[x] <= pa) || (ib + x < eb && sb[x] <= pb);
+        }
       }
-      int lo = l > kWave ? l - kWave : 0, hi = l < kWave ? l : kWave;   // part-0 elements among positions < l
+      // this lane's merged positions d0 .. d0+PL-1; split at d0 by a merge-path search (ties: part 0 first)
+      const int d0 = l * PL;
+      int lo = d0 > W ? d0 - W : 0, hi = d0 < W ? d0 : W;
       while (lo < hi) {
         const int mid = (lo + hi) >> 1;
-        if (sa[mid] <= sb[l - 1 - mid]) lo = mid + 1; else hi = mid;
+        if (sa[mid] <= sb[d0 - 1 - mid]) lo = mid + 1; else hi = mid;
       }
-      const int i = lo, jb = l - lo;
-      const bool take_a = i < kWave && (jb >= kWave || sa[i] <= sb[jb]);
-      const int32_t row = take_a ? sa[i] : sb[jb];
-      const bool valid = row != INT32_MAX;
-      const bool pair = take_a && valid && jb < kWave && sb[jb] == row;   // part 1 holds the same row next
-      const int32_t prev = __shfl_up(row, 1, kWave);
-      const bool head = valid && (l == 0 || prev != row);
-      // a pair must not straddle windows: drop position 63 when it is the part-0 half of a pair
-      const int K = __shfl(pair ? kWave - 1 : kWave, kWave - 1, kWave);
-      const bool in = l < K && valid;
-      const uint64_t hm = __ballot(head && in);
-      const uint64_t am = __ballot(take_a && in);
-      const uint64_t bm = __ballot(!take_a && in);
-      if (FILL && head && in) {
-        const int64_t pos = o + __popcll(hm & below);
-        V v = take_a ? (aval ? aval[ia + i] : V(1)) : (bval ? bval[ib + jb] : V(1));
-        if (pair) v = merge_pair<SRI, V>(v, bval ? bval[ib + jb] : V(1));
-        crow[pos] = row;
-        cval[pos] = v;
+      int i = lo, jb = d0 - lo;
+      int32_t row[PL];
+      int src[PL];            // part-0 index, or -1 - part-1 index
+      bool pair[PL];
+#pragma unroll
+      for (int e = 0; e < PL; ++e) {
+        const bool take_a = i < W && (jb >= W || sa[i] <= sb[jb]);
+        row[e] = take_a ? sa[i] : sb[jb];
+        pair[e] = take_a && row[e] != INT32_MAX && jb < W && sb[jb] == row[e];
+        src[e] = take_a ? i : -1 - jb;
+        if (take_a) ++i; else ++jb;
       }
-      if (!FILL && pair && in) ++nd;
-      o += __popcll(hm);
-      ia += __popcll(am);
-      ib += __popcll(bm);
+      // a pair must not straddle windows: the window ends before the last position if it is a part-0 half
+      const int K = __shfl(pair[PL - 1] ? W - 1 : W, kWave - 1, kWave);
+      int32_t prev = __shfl_up(row[PL - 1], 1, kWave);
+      int c = 0, na = 0;
+      bool head[PL];
+#pragma unroll
+      for (int e = 0; e < PL; ++e) {
+        const bool in = d0 + e < K && row[e] != INT32_MAX;
+        head[e] = in && ((d0 + e == 0) || prev != row[e]);
+        prev = row[e];
+        c += head[e];
+        na += in && src[e] >= 0;
+        if (!FILL && in && pair[e]) ++nd;
+      }
+      const int incl = wave_incl_scan(c);
+      const int tot = __shfl(incl, kWave - 1, kWave);
+      int nin = 0;
+#pragma unroll
+      for (int e = 0; e < PL; ++e) nin += d0 + e < K && row[e] != INT32_MAX;
+      const int ta = (int)wave_sum64(na), tin = (int)wave_sum64(nin);
+      if (FILL) {
+        int64_t pos = o + incl - c;
+#pragma unroll
+        for (int e = 0; e < PL; ++e)
+          if (head[e]) {
+            const int s = src[e];
+            V v = s >= 0 ? (aval ? aval[ia + s] : V(1)) : (bval ? bval[ib + (-1 - s)] : V(1));
+            if (pair[e]) {   // the part-1 half is the next part-1 element: index (positions so far) - (part-0 taken)
+              const int jn = d0 + e - s;   // part-1 elements before this position
+              v = merge_pair<SRI, V>(v, bval ? bval[ib + jn] : V(1));
+            }
+            crow[pos] = row[e];
+            cval[pos] = v;
+            ++pos;
+          }
+      }
+      o += tot;
+      ia += ta;
+      ib += tin - ta;
       wave_sync();
     }
     if (!FILL) {
