@@ -82,6 +82,28 @@ __global__ void k_cp_sub(int64_t n, const int64_t* __restrict__ cp, const int64_
     hcp[c] = cp[c] - lcp[c];
 }
 
+// panel assembly: B pieces of one grid column stacked by rows (column c = piece 0's rows, then piece
+// 1's rows + its row offset, ...), A pieces of one grid row side by side
+__global__ void k_add_col_counts(int64_t n, const int64_t* __restrict__ cp, int64_t* __restrict__ cnt) {
+  for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < n; c += (int64_t)gridDim.x * blockDim.x)
+    cnt[c] += cp[c + 1] - cp[c];
+}
+template <typename T>
+__global__ void __launch_bounds__(256) k_stack_rows(int64_t ncol, const int64_t* __restrict__ cp,
+                                                    const int32_t* __restrict__ ir, const T* __restrict__ val,
+                                                    int32_t roff, int64_t* __restrict__ cursor,
+                                                    int32_t* __restrict__ oir, T* __restrict__ oval) {
+  const int w = threadIdx.x / kWave, l = lane_id();
+  for (int64_t c = blockIdx.x * 4 + w; c < ncol; c += (int64_t)gridDim.x * 4) {
+    const int64_t s = cp[c], e = cp[c + 1], o = cursor[c];
+    for (int64_t q = s + l; q < e; q += kWave) {
+      oir[o + (q - s)] = ir[q] + roff;
+      if (val) oval[o + (q - s)] = val[q];
+    }
+    if (l == 0) cursor[c] = o + (e - s);
+  }
+}
+
 // device CSC piece (int64 colptr, int32 rows); storage owned by `own` unless borrowed
 struct Piece {
   int64_t nrow = 0, ncol = 0, nnz = 0;
@@ -342,6 +364,89 @@ cbg_status merge_parts(cbg_ctx* ctx, const std::vector<cbg_csc_result>& parts, c
 }
 
 // ------------------------------------------------------------------------------------ layer SUMMA
+// Internal flag: the layer's product as ONE local multiply of its panels (below).
+constexpr uint32_t kPanels = 1u << 30;
+
+// A panel: the q A pieces of the grid row side by side (inner blocks 0..q-1)
+cbg_status panel_cols(cbg_ctx* ctx, const std::vector<Piece>& a, size_t vs, bool has_val, Piece* out) {
+  hipStream_t st = ctx->stream;
+  int64_t ncol = 0, nnz = 0;
+  for (const Piece& p : a) { ncol += p.ncol; nnz += p.nnz; }
+  std::shared_ptr<Owner> o(new Owner(ctx->pool));
+  HIPCHK(o->cp.reserve(8 * (ncol + 1)));
+  HIPCHK(o->ir.reserve(4 * (nnz + 1)));
+  HIPCHK(o->val.reserve(vs * (nnz + 1) + 8));
+  int64_t c0 = 0, e0 = 0;
+  for (const Piece& p : a) {
+    if (p.ncol) k_merge_cat_cp<<<(int)grid_for(p.ncol, 256, kMaxGrid), 256, 0, st>>>(p.ncol, p.cp, e0, o->cp.as<int64_t>() + c0);
+    if (p.nnz) {
+      HIPCHK(hipMemcpyAsync(o->ir.as<int32_t>() + e0, p.ir, 4 * p.nnz, hipMemcpyDeviceToDevice, st));
+      if (has_val) HIPCHK(hipMemcpyAsync(o->val.as<char>() + vs * e0, p.val, vs * p.nnz, hipMemcpyDeviceToDevice, st));
+    }
+    c0 += p.ncol;
+    e0 += p.nnz;
+  }
+  HIPCHK(hipMemcpyAsync(o->cp.as<int64_t>() + ncol, &nnz, 8, hipMemcpyHostToDevice, st));
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(st));   // `nnz` above is a host temporary
+  out->nrow = a[0].nrow; out->ncol = ncol; out->nnz = nnz;
+  out->cp = o->cp.as<int64_t>(); out->ir = o->ir.as<int32_t>(); out->val = has_val ? o->val.p : nullptr;
+  out->own = o;
+  return CBG_OK;
+}
+
+// B panel: the q B pieces of the grid column stacked by rows (inner blocks 0..q-1)
+template <typename T>
+cbg_status panel_rows(cbg_ctx* ctx, const std::vector<Piece>& b, bool has_val, Piece* out) {
+  hipStream_t st = ctx->stream;
+  const int64_t ncol = b[0].ncol;
+  int64_t nrow = 0, nnz = 0;
+  for (const Piece& p : b) { nrow += p.nrow; nnz += p.nnz; }
+  std::shared_ptr<Owner> o(new Owner(ctx->pool));
+  HIPCHK(o->cp.reserve(8 * (ncol + 1)));
+  HIPCHK(o->ir.reserve(4 * (nnz + 1)));
+  HIPCHK(o->val.reserve(sizeof(T) * (nnz + 1)));
+  DevBuf cnt, tiles, scal;
+  HIPCHK(cnt.reserve(8 * (ncol + 1)));
+  HIPCHK(hipMemsetAsync(cnt.p, 0, 8 * (ncol + 1), st));
+  const int g = (int)grid_for(ncol, 256, kMaxGrid);
+  for (const Piece& p : b)
+    if (ncol) k_add_col_counts<<<g, 256, 0, st>>>(ncol, p.cp, cnt.as<int64_t>());
+  const int64_t ntiles = (ncol + kScanTile - 1) / kScanTile;
+  HIPCHK(tiles.reserve(8 * (ntiles + 1)));
+  HIPCHK(scal.reserve(16));
+  if (ncol > 0) {
+    k_scan_tiles<<<(int)ntiles, 256, 0, st>>>(ncol, cnt.as<int64_t>(), tiles.as<int64_t>());
+    k_scan_sums<<<1, 1024, 0, st>>>(ntiles, tiles.as<int64_t>(), scal.as<int64_t>());
+    k_scan_apply<<<(int)ntiles, 256, 0, st>>>(ncol, cnt.as<int64_t>(), tiles.as<int64_t>(), o->cp.as<int64_t>());
+    HIPCHK(hipMemcpyAsync(cnt.p, o->cp.p, 8 * ncol, hipMemcpyDeviceToDevice, st));   // cursors
+  } else {
+    HIPCHK(hipMemsetAsync(o->cp.p, 0, 8, st));
+  }
+  int32_t roff = 0;
+  for (const Piece& p : b) {   // in inner-block order: the stacked rows stay sorted per column
+    if (ncol && p.nnz)
+      k_stack_rows<T><<<(int)grid_for(ncol, 4, kMaxGrid * 2), 256, 0, st>>>(
+          ncol, p.cp, p.ir, has_val ? (const T*)p.val : nullptr, roff, cnt.as<int64_t>(), o->ir.as<int32_t>(),
+          o->val.as<T>());
+    roff += (int32_t)p.nrow;
+  }
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(st));   // cnt/tiles/scal are released on return
+  out->nrow = nrow; out->ncol = ncol; out->nnz = nnz;
+  out->cp = o->cp.as<int64_t>(); out->ir = o->ir.as<int32_t>(); out->val = has_val ? o->val.p : nullptr;
+  out->own = o;
+  return CBG_OK;
+}
+
+cbg_status panel_rows_dt(cbg_ctx* ctx, cbg_dtype dt, const std::vector<Piece>& b, bool has_val, Piece* out) {
+  switch (dt_size(dt)) {
+    case 1: return panel_rows<uint8_t>(ctx, b, has_val, out);
+    case 4: return panel_rows<uint32_t>(ctx, b, has_val, out);
+    default: return panel_rows<uint64_t>(ctx, b, has_val, out);
+  }
+}
+
 cbg_status summa_layer_impl(cbg_grid* G, const cbg_dcsc_view* Av, const cbg_dcsc_view* Bv, cbg_semiring sr,
                             cbg_dtype dt, uint32_t flags, std::vector<Piece>* parts, cbg_grid_stats* st) {
   cbg_ctx* ctx = G->ctx;
@@ -396,6 +501,84 @@ cbg_status summa_layer_impl(cbg_grid* G, const cbg_dcsc_view* Av, const cbg_dcsc
       if (k != G->col) needA = std::max(needA, bytes_of(SA(r, k)));
       if (k != G->row) needB = std::max(needB, bytes_of(SB(r, k)));
     }
+  if ((flags & kPanels) && R == 1 && q > 1) {
+    // Panels: HBM holds the whole grid row of A and grid column of B (1/q of each operand), so the
+    // layer's product is ONE local multiply of A(i, :) and B(:, j) -- the same bytes as the q stage
+    // broadcasts, no stage products and no stage merge.  The inner blocks are concatenated in stage order,
+    // so every duplicate combines in the order the staged merge would (Select2nd: first stage wins).
+    std::vector<PoolBuf> bufA(q), bufB(q);
+    std::vector<Piece> pa(q), pb(q);
+    for (int k = 0; k < q; ++k) {
+      Piece a, b;
+      if (k == G->col) {
+        a = A0;
+      } else {
+        const Sizes& z = SA(0, k);
+        bufA[k].pool = ctx->pool;
+        HIPCHK(bufA[k].reserve(bytes_of(z)));
+        char* base = bufA[k].as<char>();
+        a.nrow = z.nrow; a.ncol = z.ncol; a.nnz = z.nnz;
+        a.cp = (const int64_t*)base;
+        a.ir = (const int32_t*)(base + 8 * (z.ncol + 1));
+        a.val = z.has_val > 0 ? (const void*)(base + 8 * (z.ncol + 1) + ((4 * z.nnz + 15) & ~15LL)) : nullptr;
+      }
+      if (k == G->row) {
+        b = B0;
+      } else {
+        const Sizes& z = SB(0, k);
+        bufB[k].pool = ctx->pool;
+        HIPCHK(bufB[k].reserve(bytes_of(z)));
+        char* base = bufB[k].as<char>();
+        b.nrow = z.nrow; b.ncol = z.ncol; b.nnz = z.nnz;
+        b.cp = (const int64_t*)base;
+        b.ir = (const int32_t*)(base + 8 * (z.ncol + 1));
+        b.val = z.has_val > 0 ? (const void*)(base + 8 * (z.ncol + 1) + ((4 * z.nnz + 15) & ~15LL)) : nullptr;
+      }
+      pa[k] = a;
+      pb[k] = b;
+    }
+    hipEvent_t e0, e1, ready;
+    HIPCHK(hipEventCreate(&e0));
+    HIPCHK(hipEventCreate(&e1));
+    HIPCHK(hipEventCreate(&ready));
+    HIPCHK(hipEventRecord(ready, ctx->stream));   // the own pieces are complete before they are sent
+    HIPCHK(hipStreamWaitEvent(G->cs, ready, 0));
+    HIPCHK(hipEventRecord(e0, G->cs));
+    for (int k = 0; k < q; ++k) {
+      void* ab[3] = {(void*)pa[k].cp, (void*)pa[k].ir, (void*)pa[k].val};
+      int64_t an[3] = {8 * (pa[k].ncol + 1), 4 * pa[k].nnz, pa[k].val ? (int64_t)vs * pa[k].nnz : 0};
+      void* bb[3] = {(void*)pb[k].cp, (void*)pb[k].ir, (void*)pb[k].val};
+      int64_t bn[3] = {8 * (pb[k].ncol + 1), 4 * pb[k].nnz, pb[k].val ? (int64_t)vs * pb[k].nnz : 0};
+      CBGCHK(t_bcast(G, CBG_GROUP_ROW, 3, ab, an, k));
+      CBGCHK(t_bcast(G, CBG_GROUP_COL, 3, bb, bn, k));
+      if (st) st->bcast_bytes += (k == G->col ? 0 : an[0] + an[1] + an[2]) + (k == G->row ? 0 : bn[0] + bn[1] + bn[2]);
+    }
+    HIPCHK(hipEventRecord(e1, G->cs));
+    HIPCHK(hipStreamWaitEvent(ctx->stream, e1, 0));
+    const double t0 = now_ms();
+    Piece AP, BP;
+    CBGCHK(panel_cols(ctx, pa, vs, ha > 0, &AP));
+    CBGCHK(panel_rows_dt(ctx, dt, pb, hb > 0, &BP));
+    pa.clear();
+    pb.clear();
+    cbg_dcsc_view va = view_of(AP, dt, AP.val != nullptr);
+    cbg_dcsc_view vb = view_of(BP, dt, BP.val != nullptr);
+    cbg_csc_result C;
+    int64_t m = 0;
+    CBGCHK(cbg_spgemm_local(ctx, &va, &vb, sr, dt, CBG_SORTED_COLS, &C, &m));
+    if (st) { st->multiplies += m; st->local_ms += now_ms() - t0; st->stages += q; }
+    Piece P = piece_of_result(C);
+    parts->push_back(P);
+    HIPCHK(hipStreamSynchronize(G->cs));
+    HIPCHK(hipStreamSynchronize(ctx->stream));   // panels and receive buffers go back to the pool on return
+    float ms = 0.f;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    if (st) st->bcast_ms += ms;
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    (void)hipEventDestroy(ready);
+    return CBG_OK;
+  }
   if (q > 1)
     for (int s = 0; s < 2; ++s) { HIPCHK(G->slotA[s].reserve(needA)); HIPCHK(G->slotB[s].reserve(needB)); }
   const int S = R * q;
@@ -787,7 +970,11 @@ cbg_status cbg_spgemm_grid(cbg_grid* G, const cbg_dcsc_view* A, const cbg_dcsc_v
   if (st) memset(st, 0, sizeof(*st));
   const double t0 = now_ms();
   std::vector<Piece> ps;
-  CBGCHK(summa_layer_impl(G, A, B, sr, dt, flags, &ps, st));
+  // the panel schedule for the plain product (Mult_AnXBn_Synch / SUMMA3D); DoubleBuff / Overlap keep their
+  // staged schedules, and so does Select2nd on L > 1 layers, whose fiber merge order is (stage, layer)
+  const bool panels = !(flags & (CBG_HALVES | CBG_RUNNING_MERGE)) && !(sr == CBG_SR_SELECT2ND && G->L > 1) &&
+                      std::getenv("CBG_GRID_STAGED") == nullptr;
+  CBGCHK(summa_layer_impl(G, A, B, sr, dt, flags | (panels ? kPanels : 0u), &ps, st));
   CBGCHK(reduce_all_impl(G, ps, sr, dt, C, st));
   if (st) st->total_ms = now_ms() - t0;
   return CBG_OK;

@@ -81,3 +81,12 @@ def test_memeff3d_phases_match_reference_gloo_gpu(world, port):
     (golden/mcl.npz) on every rank's piece, with the same branch counts."""
     from dist_support import run_mcl_fixture_case
     spawn_case(world, "gpu", [1, 2, 3, ("mem", 0.0025)], port, body=run_mcl_fixture_case)
+
+
+@pytest.mark.parametrize("world,port", [(4, 29661), (8, 29662)])
+def test_reference_fixtures_staged_schedule_gloo_gpu(world, port, monkeypatch):
+    """The same reference fixtures through the reference's staged SUMMA schedule (CBG_GRID_STAGED=1: q stage
+    products + stage merge) -- the default panel schedule must agree with it and with the reference."""
+    from dist_support import run_fixture_case
+    monkeypatch.setenv("CBG_GRID_STAGED", "1")
+    spawn_case(world, "gpu", FIXTURE_CASES, port, body=run_fixture_case)

@@ -428,3 +428,46 @@ def test_gpu_merge_matches_reference_multiwaymergehash(gpu_ctx, which, sr):
     cp, ir, val = M.to_host()
     assert np.array_equal(cp, z[f"{which}_{sr}_hash_cp"]) and np.array_equal(ir, z[f"{which}_{sr}_hash_ir"])
     assert np.array_equal(val, z[f"{which}_{sr}_hash_val"])
+
+
+def test_gpu_two_way_merge_edge_cases(gpu_ctx):
+    """The two-way merge kernel: columns longer than one 256-position window with duplicates straddling
+    window ends, empty columns on either side, an unsorted partial (declined, the hash merge takes it:
+    same result), and BoolCopy1st duplicates (CBG_EADD, as the reference's add() throws)."""
+    from helpers import oracle_merge
+    rng = np.random.default_rng(5)
+    n, m = 4000, 7
+    cols_a, cols_b = [], []
+    for j in range(m):
+        la, lb = [0, 300, 1000, 257, 0, 3000, 1][j], [0, 0, 999, 300, 5, 2999, 1][j]
+        base = rng.choice(n, size=min(n, la + lb), replace=False)
+        a = np.sort(base[:la]) if la else np.zeros(0, np.int64)
+        # part 1 shares about half of part 0's rows (duplicate pairs), the rest fresh
+        share = rng.choice(a, size=min(len(a), lb // 2), replace=False) if la else np.zeros(0, np.int64)
+        b = np.unique(np.concatenate([share, base[la:la + lb - len(share)]]))[:lb]
+        cols_a.append(a)
+        cols_b.append(np.sort(b))
+
+    def mk(cols):
+        cp = np.concatenate([[0], np.cumsum([len(c) for c in cols])]).astype(np.int64)
+        ir = np.concatenate(cols).astype(np.int32)
+        return Csc(n, m, cp, ir, rng.integers(1, 9, len(ir)).astype(np.int64))
+    P0, P1 = mk(cols_a), mk(cols_b)
+    for sr in ("plus_times", "min_plus", "select2nd", "select_max"):
+        R, rc = oracle_merge([P0, P1], sr, "i64")
+        assert rc == 0
+        M = cb.MultiwayMerge(SRCLS[sr]("i64"), [upload(gpu_ctx, P0), upload(gpu_ctx, P1)])
+        cp, ir, val = M.to_host()
+        assert_same_product(Csc(n, m, cp, ir, val), R, "i64", what=f"two-way merge {sr}")
+    # unsorted part 1 (column 2 reversed): the hash merge's result, row-sorted
+    ir1 = P1.ir.copy()
+    ir1[P1.cp[2]:P1.cp[3]] = ir1[P1.cp[2]:P1.cp[3]][::-1]
+    P1u = Csc(n, m, P1.cp, ir1, P1.val.copy())
+    P1u.val[P1.cp[2]:P1.cp[3]] = P1.val[P1.cp[2]:P1.cp[3]][::-1]
+    R, rc = oracle_merge([P0, P1], "plus_times", "i64")
+    M = cb.MultiwayMerge(SRCLS["plus_times"]("i64"), [upload(gpu_ctx, P0), upload(gpu_ctx, P1u)])
+    cp, ir, val = M.to_host()
+    assert_same_product(Csc(n, m, cp, ir, val), R, "i64", what="two-way merge, unsorted part")
+    with pytest.raises(cb.CbgError) as ei:
+        cb.MultiwayMerge(SRCLS["bool_copy1st"]("i64"), [upload(gpu_ctx, P0), upload(gpu_ctx, P1)])
+    assert ei.value.status == 13
