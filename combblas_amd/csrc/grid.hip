@@ -104,6 +104,23 @@ __global__ void __launch_bounds__(256) k_stack_rows(int64_t ncol, const int64_t*
   }
 }
 
+// lossless narrowing of f64 messages: values that survive a round trip through f32 bit for bit
+__global__ void k_f32_inexact(int64_t n, const double* __restrict__ v, unsigned long long* __restrict__ bad) {
+  unsigned long long c = 0;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    c += __double_as_longlong((double)(float)v[i]) != __double_as_longlong(v[i]);
+  c = (unsigned long long)wave_sum64((int64_t)c);
+  if (lane_id() == 0 && c) atomicAdd(bad, c);
+}
+__global__ void k_f64_to_f32(int64_t n, const double* __restrict__ in, float* __restrict__ out) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = (float)in[i];
+}
+__global__ void k_f32_to_f64(int64_t n, const float* __restrict__ in, double* __restrict__ out) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = (double)in[i];
+}
+
 // device CSC piece (int64 colptr, int32 rows); storage owned by `own` unless borrowed
 struct Piece {
   int64_t nrow = 0, ncol = 0, nnz = 0;
@@ -692,7 +709,13 @@ cbg_status summa_layer_impl(cbg_grid* G, const cbg_dcsc_view* Av, const cbg_dcsc
 // Fiber all-to-all of one colsplit partial (ParFriends.h:3119-3153, Reductions.h:36-130): layer part m
 // of its columns (block_range(ncol, L, m)) goes to fiber member m; returns the L pieces of this
 // rank's own layer part, in member (layer) order.  The pieces own their receive storage.
-cbg_status fiber_exchange(cbg_grid* G, const Piece& C, size_t vs, std::vector<Piece>* pcs, cbg_grid_stats* st) {
+//
+// Values of an f64 product travel as f32 when every value of every fiber member's message survives the
+// round trip f64 -> f32 -> f64 bit for bit (integers below 2^24, multiplicities, 0/1 patterns, ...): a
+// lossless 1/3 cut of the bytes on the xGMI link.  Each member's verdict rides on the count exchange
+// (bit 62 of its nnz), so all members agree without another collective; CBG_FIBER_NARROW=0 disables it.
+cbg_status fiber_exchange(cbg_grid* G, const Piece& C, size_t vs, bool f64, std::vector<Piece>* pcs,
+                          cbg_grid_stats* st) {
   cbg_ctx* ctx = G->ctx;
   hipStream_t cst = ctx->stream;
   const int L = G->L, me = G->layer;
@@ -702,14 +725,37 @@ cbg_status fiber_exchange(cbg_grid* G, const Piece& C, size_t vs, std::vector<Pi
   HIPCHK(hipStreamSynchronize(cst));
   std::vector<int64_t> snnz(L), rnnz(L);
   for (int m = 0; m < L; ++m) snnz[m] = eb[m + 1] - eb[m];
-  HIPCHK(G->small.reserve(16 * (L + 1)));
+  HIPCHK(G->small.reserve(16 * (L + 1) + 16));
   int64_t* dsn = G->small.as<int64_t>();
   int64_t* drn = dsn + L;
-  HIPCHK(hipMemcpyAsync(dsn, snnz.data(), 8 * L, hipMemcpyHostToDevice, cst));
+  bool narrow = f64 && C.val != nullptr && vs == 8;
+  if (narrow) {
+    const char* e = std::getenv("CBG_FIBER_NARROW");
+    narrow = !(e && e[0] == '0');
+  }
+  if (narrow) {   // does this member's whole outgoing range survive f32?
+    unsigned long long* bad = (unsigned long long*)(drn + L);
+    HIPCHK(hipMemsetAsync(bad, 0, 8, cst));
+    const int64_t n = eb[L] - eb[0];
+    if (n) k_f32_inexact<<<(int)grid_for(n, 256, kMaxGrid), 256, 0, cst>>>(n, (const double*)C.val + eb[0], bad);
+    unsigned long long nb = 0;
+    HIPCHK(hipMemcpyAsync(&nb, bad, 8, hipMemcpyDeviceToHost, cst));
+    HIPCHK(hipStreamSynchronize(cst));
+    narrow = nb == 0;
+  }
+  const int64_t kNarrowBit = 1LL << 62;
+  std::vector<int64_t> sflag(L);
+  for (int m = 0; m < L; ++m) sflag[m] = snnz[m] | (narrow ? kNarrowBit : 0);
+  HIPCHK(hipMemcpyAsync(dsn, sflag.data(), 8 * L, hipMemcpyHostToDevice, cst));
   std::vector<int64_t> eight(L, 8);
   CBGCHK(t_alltoallv(G, CBG_GROUP_FIBER, dsn, eight.data(), drn, eight.data()));
   HIPCHK(hipMemcpyAsync(rnnz.data(), drn, 8 * L, hipMemcpyDeviceToHost, cst));
   HIPCHK(hipStreamSynchronize(cst));
+  bool all_narrow = narrow;
+  for (int m = 0; m < L; ++m) {
+    all_narrow = all_narrow && (rnnz[m] & kNarrowBit);
+    rnnz[m] &= ~kNarrowBit;
+  }
   const int64_t myc = cbnd[me + 1] - cbnd[me];
   int64_t rtot = 0;
   for (int m = 0; m < L; ++m) rtot += rnnz[m];
@@ -729,13 +775,28 @@ cbg_status fiber_exchange(cbg_grid* G, const Piece& C, size_t vs, std::vector<Pi
   for (int m = 0; m < L; ++m) { sb[m] = 4 * snnz[m]; rb[m] = 4 * rnnz[m]; }
   CBGCHK(t_alltoallv(G, CBG_GROUP_FIBER, C.ir + eb[0], sb.data(), rbase, rb.data()));
   const bool has_val = C.val != nullptr;
-  if (has_val) {
+  const int64_t wire_vs = all_narrow ? 4 : (int64_t)vs;
+  if (has_val && all_narrow) {   // f32 on the wire, widened back into the f64 receive region
+    const int64_t stot = eb[L] - eb[0];
+    PoolBuf s32, r32;
+    s32.pool = r32.pool = ctx->pool;
+    HIPCHK(s32.reserve(4 * (stot + 1)));
+    HIPCHK(r32.reserve(4 * (rtot + 1)));
+    if (stot) k_f64_to_f32<<<(int)grid_for(stot, 256, kMaxGrid), 256, 0, cst>>>(stot, (const double*)C.val + eb[0],
+                                                                                 s32.as<float>());
+    for (int m = 0; m < L; ++m) { sb[m] = 4 * snnz[m]; rb[m] = 4 * rnnz[m]; }
+    CBGCHK(t_alltoallv(G, CBG_GROUP_FIBER, s32.p, sb.data(), r32.p, rb.data()));
+    if (rtot) k_f32_to_f64<<<(int)grid_for(rtot, 256, kMaxGrid), 256, 0, cst>>>(rtot, r32.as<float>(),
+                                                                                (double*)(rbase + ir_bytes));
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(cst));   // s32/r32 go back to the pool on return
+  } else if (has_val) {
     for (int m = 0; m < L; ++m) { sb[m] = (int64_t)vs * snnz[m]; rb[m] = (int64_t)vs * rnnz[m]; }
     CBGCHK(t_alltoallv(G, CBG_GROUP_FIBER, (const char*)C.val + vs * eb[0], sb.data(), rbase + ir_bytes, rb.data()));
   }
   if (st)
     for (int m = 0; m < L; ++m)
-      if (m != me) st->fiber_bytes += (4 + (int64_t)vs) * snnz[m] + 8 * (cbnd[m + 1] - cbnd[m]);
+      if (m != me) st->fiber_bytes += (4 + (has_val ? wire_vs : 0)) * snnz[m] + 8 * (cbnd[m + 1] - cbnd[m]);
   pcs->assign(L, Piece());
   const int64_t ntiles = (myc + kScanTile - 1) / kScanTile;
   DevBuf tiles, scal;
@@ -815,7 +876,7 @@ cbg_status reduce_all_impl(cbg_grid* G, std::vector<Piece>& parts, cbg_semiring 
     if (L == 1) return hand_out(ctx, C, dt, out);
     const double t1 = now_ms();
     std::vector<Piece> pcs;
-    CBGCHK(fiber_exchange(G, C, vs, &pcs, st));
+    CBGCHK(fiber_exchange(G, C, vs, dt == CBG_F64, &pcs, st));
     C = Piece();
     if (st) st->fiber_ms += now_ms() - t1;
     const double t2 = now_ms();
@@ -830,7 +891,7 @@ cbg_status reduce_all_impl(cbg_grid* G, std::vector<Piece>& parts, cbg_semiring 
   std::vector<std::vector<Piece>> got(parts.size());
   for (size_t i = 0; i < parts.size(); ++i) {
     ks.push_back(parts[i].k);
-    CBGCHK(fiber_exchange(G, parts[i], vs, &got[i], st));
+    CBGCHK(fiber_exchange(G, parts[i], vs, dt == CBG_F64, &got[i], st));
   }
   parts.clear();
   if (st) st->fiber_ms += now_ms() - t1;
