@@ -833,6 +833,8 @@ def _phases_for_memory(A, B, phases, selectNum, recoverNum, perProcessMemory):
     post-selection output against perProcessMemory GB; the MAX over the fiber, never below `phases`."""
     g, be = A.grid, A.backend
     p = g.q * g.q
+    # bytes per stored nonzero in this implementation: int32 row + value (+ amortised colptr), the role of
+    # the reference's sizeof(IU) * 2 + sizeof(NU)
     per_in = 4 * 2 + (8 if be.val_dtype == torch.float64 else 4)
     per_out = per_in
     t = torch.tensor([A.block.nnz], dtype=torch.int64, device=be.comm_device)
@@ -845,7 +847,7 @@ def _phases_for_memory(A, B, phases, selectNum, recoverNum, perProcessMemory):
     k = min(max(selectNum, recoverNum), d)
     post_nnz = -(-int((ncl // g.L) * k) // max(1, int(p ** 0.5)))
     remaining = perProcessMemory * 1e9 - input_mem - post_nnz * per_out * 2
-    ksel_mem = ncl * k * per_out * 3
+    ksel_mem = ncl * k * (per_out - 8) * 3        # k-select buffers hold values only (sizeof(NUO) * 3)
     calc = int(-(-(asq_mem + ksel_mem) // remaining)) if remaining > 0 else -1
     return max(phases, calc)
 

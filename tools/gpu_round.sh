@@ -10,7 +10,7 @@ OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 if [ "${1:-}" != "--no-tests" ]; then
-  timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread > "$OUT/gpu_tests.log" 2>&1
+  timeout -k 10 900 python -u -m pytest tests -m gpu -v -s --timeout 300 --timeout-method thread > "$OUT/gpu_tests.log" 2>&1
   rc=$?; echo "pytest rc=$rc"; tail -3 "$OUT/gpu_tests.log"
   [ $rc -eq 0 ] || exit $rc
 fi
