@@ -981,6 +981,9 @@ __global__ void __launch_bounds__(NT) k_sym_block(const int32_t* __restrict__ li
 #endif
 constexpr int kPartLog = CBG_PART_LOG;
 constexpr int kPartNT = CBG_PART_NT;
+#ifndef CBG_SYM_TESTOR
+#define CBG_SYM_TESTOR 1   // k_sym_part reads a bitmap word before setting a bit (0: no-return ds_or only)
+#endif
 // first symbolic class (LOGT = class + 5) cut into parts: bitmaps larger than one part; every such
 // column has flop > kHeavy (2*flop > 2^(class+4) words), so the heavy lists can hold it
 constexpr int kWideClass = kPartLog - 9 > 9 ? kPartLog - 9 : 9;
@@ -1038,6 +1041,7 @@ __global__ void __launch_bounds__(NT) k_sym_part(const PartItem* __restrict__ it
   for (int i = blockIdx.x; i < count; i += gridDim.x) {
     const PartItem it = items[i];
     const int2 sp = span[it.j];
+    const int64_t bs = Bcp[it.j], be = Bcp[it.j + 1];
     const int32_t r0 = ((sp.x >> kPartLog) + it.p) << kPartLog;
     const int32_t s0 = r0 >> spl.log;
     const int32_t s1 = min(spl.nsub, (int32_t)(((int64_t)r0 + (1 << kPartLog)) >> spl.log));
@@ -1046,28 +1050,31 @@ __global__ void __launch_bounds__(NT) k_sym_part(const PartItem* __restrict__ it
     if (threadIdx.x == 0) misc[0] = 0;
     __syncthreads();
     STAMP(26);
-    for_each_multiply<NT, false, kUnrollSym, kGroupSym, uint8_t>(
-        Bcp[it.j], Bcp[it.j + 1], sb,
-        [&](int64_t b, int64_t& a0, int64_t& a1, uint8_t&) {
-          const int32_t k = Bir[b];
-          const int64_t c0 = Acp[k], c1 = Acp[k + 1];
-          if (c1 - c0 >= kSplitMin) {
-            const int32_t* t = spl.tab + (int64_t)spl.idx[k] * (spl.nsub + 1);
-            a0 = c0 + t[s0];
-            a1 = c0 + t[s1];
-          } else {
-            a0 = c0;
-            a1 = c1;
-          }
-        },
-        [&](int64_t q) { return Air[q]; },
-        [&](int32_t r, uint8_t, int64_t, int64_t) {
-          const uint32_t o = (uint32_t)(r - r0);
-          if (o < (1u << kPartLog)) {
-            const uint32_t bit = 1u << (o & 31);
-            if (!(tab[o >> 5] & bit)) atomicOr(&tab[o >> 5], bit);
-          }
-        });
+    auto seg = [&](int64_t b, int64_t& a0, int64_t& a1, uint8_t&) {
+      const int32_t k = Bir[b];
+      const int64_t c0 = Acp[k], c1 = Acp[k + 1];
+      if (c1 - c0 >= kSplitMin) {
+        const int32_t* t = spl.tab + (int64_t)spl.idx[k] * (spl.nsub + 1);
+        a0 = c0 + t[s0];
+        a1 = c0 + t[s1];
+      } else {
+        a0 = c0;
+        a1 = c1;
+      }
+    };
+    auto ld = [&](int64_t q) { return Air[q]; };
+    auto ins = [&](int32_t r, uint8_t, int64_t, int64_t) {
+      const uint32_t o = (uint32_t)(r - r0);
+      if (o < (1u << kPartLog)) {
+        const uint32_t bit = 1u << (o & 31);
+#if CBG_SYM_TESTOR
+        if (!(tab[o >> 5] & bit)) atomicOr(&tab[o >> 5], bit);
+#else
+        atomicOr(&tab[o >> 5], bit);
+#endif
+      }
+    };
+    for_each_multiply<NT, false, kUnrollSym, kGroupSym, uint8_t>(bs, be, sb, seg, ld, ins);
     __syncthreads();
     STAMP(27);
     int c = 0;
@@ -1112,6 +1119,7 @@ __global__ void __launch_bounds__(NT) k_sym_part(const PartItem* __restrict__ it
     for (int s = sf + (int)threadIdx.x; s <= sl; s += NT) dst[s] = scnt[s - s0];
     __syncthreads();
     STAMP(29);
+    STAMP_COUNT(30, 1);
   }
 }
 

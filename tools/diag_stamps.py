@@ -33,5 +33,8 @@ print("runs", s[19], "keys in runs", s[20], "max run", s[21], "sum L^2", s[22])
 print(f"rank single-chunk: sweep 1 (rows + marks) {s[24]} cycles, directory {s[25]} cycles "
       f"(phase 4 'expand' = sweep 2 for those units)")
 print("k_sym_part: clear", s[26], "expand", s[27], "count+scan", s[28], "rows+subwindow counts", s[29])
+if s[30]:
+    print("k_sym_part per item (cycles): items", s[30], "clear %.0f expand %.0f count+scan %.0f rows %.0f" %
+          tuple(s[i] / s[30] for i in (26, 27, 28, 29)))
 print("units", s[10], "chunks", s[11], "multiplies", s[12], "hash units", s[13])
 print("profile", {k: prof[k] for k in ("numeric_ms", "symbolic_ms", "total_ms")})
