@@ -237,26 +237,20 @@ __global__ void k_rap_compact(int64_t nagg, const int64_t* __restrict__ rcp, con
   }
 }
 
+template <class Buf>   // DevBuf (persistent workspace) or PoolBuf
 cbg_status scan_counts_async(hipStream_t st, int64_t n, const int64_t* cnt, int64_t* out, int64_t* total_dev,
-                             DevBuf* tiles) {
+                             Buf* tiles) {
   const int64_t ntiles = (n + kScanTile - 1) / kScanTile;
   HIPCHK(tiles->reserve(sizeof(int64_t) * (ntiles + 1)));
   if (n > 0) {
-    k_scan_tiles<<<(int)ntiles, 256, 0, st>>>(n, cnt, tiles->as<int64_t>());
-    k_scan_sums<<<1, 1024, 0, st>>>(ntiles, tiles->as<int64_t>(), total_dev);
-    k_scan_apply<<<(int)ntiles, 256, 0, st>>>(n, cnt, tiles->as<int64_t>(), out);
+    k_scan_tiles<<<(int)ntiles, 256, 0, st>>>(n, cnt, (int64_t*)tiles->p);
+    k_scan_sums<<<1, 1024, 0, st>>>(ntiles, (int64_t*)tiles->p, total_dev);
+    k_scan_apply<<<(int)ntiles, 256, 0, st>>>(n, cnt, (int64_t*)tiles->p, out);
   } else {
     HIPCHK(hipMemsetAsync(out, 0, sizeof(int64_t), st));
     HIPCHK(hipMemsetAsync(total_dev, 0, sizeof(int64_t), st));
   }
   HIPCHK(hipGetLastError());
-  return CBG_OK;
-}
-
-cbg_status scan_counts(hipStream_t st, int64_t n, const int64_t* cnt, int64_t* out, int64_t* total_dev) {
-  DevBuf tiles;
-  CBGCHK(scan_counts_async(st, n, cnt, out, total_dev, &tiles));
-  HIPCHK(hipStreamSynchronize(st));   // tiles is released on return
   return CBG_OK;
 }
 
@@ -273,7 +267,9 @@ extern "C" cbg_status cbg_mis2_restriction(cbg_ctx* ctx, const cbg_dcsc_view* Gv
   CBGCHK(stage<double>(ctx, Gv, sb, &G));
   const int64_t n = G.ncol;
   if (n >= INT32_MAX) return CBG_EUNSUP;
-  DevBuf key, m1, m2, st8, fr, c1, c2, sc;
+  // scratch from the context's caching pool (stream-ordered reuse; no hipMalloc/hipFree per call)
+  PoolBuf key, m1, m2, st8, fr, c1, c2, sc, tiles;
+  for (PoolBuf* b : {&key, &m1, &m2, &st8, &fr, &c1, &c2, &sc, &tiles}) b->pool = ctx->pool;
   HIPCHK(key.reserve(8 * (n + 1)));
   HIPCHK(m1.reserve(8 * (n + 1)));
   HIPCHK(m2.reserve(8 * (n + 1)));
@@ -302,7 +298,8 @@ extern "C" cbg_status cbg_mis2_restriction(cbg_ctx* ctx, const cbg_dcsc_view* Gv
     if (left == 0) break;
   }
   // aggregates: nearest root within distance 1, else 2 (m1/m2 reused for the root-key maxima)
-  DevBuf rk, isr, rid, agg, cnt;
+  PoolBuf rk, isr, rid, agg, cnt;
+  for (PoolBuf* b : {&rk, &isr, &rid, &agg, &cnt}) b->pool = ctx->pool;
   HIPCHK(rk.reserve(8 * (n + 1)));
   HIPCHK(isr.reserve(8 * (n + 1)));
   HIPCHK(rid.reserve(8 * (n + 1)));
@@ -311,9 +308,10 @@ extern "C" cbg_status cbg_mis2_restriction(cbg_ctx* ctx, const cbg_dcsc_view* Gv
   k_nbr_max<false><<<g, 256, 0, st>>>(n, G.cp, G.ir, rk.as<uint64_t>(), state, 0, m1.as<uint64_t>());
   k_nbr_max<false><<<g, 256, 0, st>>>(n, G.cp, G.ir, m1.as<uint64_t>(), state, 0, m2.as<uint64_t>());
   HIPCHK(hipGetLastError());
-  CBGCHK(scan_counts(st, n, isr.as<int64_t>(), rid.as<int64_t>(), (int64_t*)(sc.as<char>() + 8)));
+  CBGCHK(scan_counts_async(st, n, isr.as<int64_t>(), rid.as<int64_t>(), (int64_t*)(sc.as<char>() + 8), &tiles));
   int64_t nagg = 0;
-  HIPCHK(hipMemcpy(&nagg, sc.as<char>() + 8, 8, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpyAsync(&nagg, sc.as<char>() + 8, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
   HIPCHK(cnt.reserve(8 * (2 * nagg + 2)));
   unsigned long long* colcnt = cnt.as<unsigned long long>();
   unsigned long long* cursor = colcnt + nagg + 1;
@@ -321,10 +319,12 @@ extern "C" cbg_status cbg_mis2_restriction(cbg_ctx* ctx, const cbg_dcsc_view* Gv
   k_assign<<<g, 256, 0, st>>>(n, m1.as<uint64_t>(), m2.as<uint64_t>(), rid.as<int64_t>(), agg.as<int32_t>(), colcnt);
   HIPCHK(hipGetLastError());
   // R (n x nagg): members of each aggregate, row-sorted by the duplicate-summing product (values 1)
-  DevBuf rawcp, rows;
+  PoolBuf rawcp, rows;
+  rawcp.pool = rows.pool = ctx->pool;
   HIPCHK(rawcp.reserve(8 * (nagg + 1)));
   HIPCHK(rows.reserve(4 * (n + 1)));
-  CBGCHK(scan_counts(st, nagg, (const int64_t*)colcnt, rawcp.as<int64_t>(), (int64_t*)(sc.as<char>() + 16)));
+  CBGCHK(scan_counts_async(st, nagg, (const int64_t*)colcnt, rawcp.as<int64_t>(), (int64_t*)(sc.as<char>() + 16),
+                           &tiles));
   if (nagg) HIPCHK(hipMemcpyAsync(cursor, rawcp.p, 8 * nagg, hipMemcpyDeviceToDevice, st));
   k_scatter_members<<<g, 256, 0, st>>>(n, agg.as<int32_t>(), cursor, rows.as<int32_t>());
   HIPCHK(hipGetLastError());

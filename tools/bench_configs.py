@@ -98,6 +98,16 @@ def config5(ctx, PT, args):
     ctx.synchronize()
     r_s = time.perf_counter() - t0
     nagg = dR.getncol()
+
+    class _Pair:   # both restriction outputs, freed together by timed()
+        def __init__(self, rr):
+            self.rr = rr
+
+        def free(self):
+            for m in self.rr:
+                m.free()
+
+    t_restrict = timed(ctx, lambda: _Pair(cb.RestrictionOp(dA, seed=1)), args.reps)
     RA = cb.LocalSpGEMMHash(PT, dRt, dA)
     C = cb.LocalSpGEMMHash(PT, RA, dR)
     m1, m2, nnz_ra, nnz_c = RA.multiplies, C.multiplies, RA.getnnz(), C.getnnz()
@@ -117,7 +127,8 @@ def config5(ctx, PT, args):
     t_fused = timed(ctx, fused, args.reps)
     print(json.dumps({"config": "5: Galerkin R^T A R, 3D Poisson 7-point, MIS-2 aggregation (device), 1 GPU",
                       "A": {"k": args.poisson_k, "n": n, "nnz": int(acp[-1])}, "R": {"nagg": nagg},
-                      "gen_s": round(gen_s, 2), "restriction_device_ms": round(r_s * 1e3, 3),
+                      "gen_s": round(gen_s, 2), "restriction_device_ms": round(t_restrict * 1e3, 3),
+                      "restriction_first_call_ms": round(r_s * 1e3, 3),
                       "multiplies": m1 + m2, "nnz_RtA": nnz_ra, "nnz_C": nnz_c,
                       "triple_ms": t_gal * 1e3, "multiplies_per_s": (m1 + m2) / t_gal, "unit": "multiplies/s",
                       "fused_rap_ms": t_fused * 1e3,
