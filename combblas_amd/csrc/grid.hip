@@ -312,7 +312,8 @@ cbg_status row_halves(cbg_ctx* ctx, const Piece& b, Piece* h) {
   const int32_t cut = (int32_t)(b.nrow / 2);
   hipStream_t st = ctx->stream;
   std::shared_ptr<Owner> lo(new Owner(ctx->pool)), hi(new Owner(ctx->pool));
-  DevBuf cnt, tiles, scal;
+  PoolBuf cnt, tiles, scal;
+  cnt.pool = tiles.pool = scal.pool = ctx->pool;
   const int64_t n = b.ncol;
   HIPCHK(cnt.reserve(8 * (2 * n + 2)));
   HIPCHK(lo->cp.reserve(8 * (n + 1)));
@@ -347,7 +348,7 @@ cbg_status row_halves(cbg_ctx* ctx, const Piece& b, Piece* h) {
         n, b.cp, b.ir, (const T*)b.val, cut, lo->cp.as<int64_t>(), hi->cp.as<int64_t>(), lo->ir.as<int32_t>(),
         lo->val.as<T>(), hi->ir.as<int32_t>(), hi->val.as<T>());
   HIPCHK(hipGetLastError());
-  HIPCHK(hipStreamSynchronize(st));   // cnt/tiles/scal are released on return
+  HIPCHK(hipStreamSynchronize(st));   // cnt/tiles/scal go back to the pool on return
   h[0].nrow = cut; h[0].ncol = n; h[0].nnz = tot[0];
   h[0].cp = lo->cp.as<int64_t>(); h[0].ir = lo->ir.as<int32_t>(); h[0].val = b.val ? lo->val.p : nullptr; h[0].own = lo;
   h[1].nrow = b.nrow - cut; h[1].ncol = n; h[1].nnz = tot[1];
@@ -423,7 +424,8 @@ cbg_status panel_rows(cbg_ctx* ctx, const std::vector<Piece>& b, bool has_val, P
   HIPCHK(o->cp.reserve(8 * (ncol + 1)));
   HIPCHK(o->ir.reserve(4 * (nnz + 1)));
   HIPCHK(o->val.reserve(sizeof(T) * (nnz + 1)));
-  DevBuf cnt, tiles, scal;
+  PoolBuf cnt, tiles, scal;
+  cnt.pool = tiles.pool = scal.pool = ctx->pool;
   HIPCHK(cnt.reserve(8 * (ncol + 1)));
   HIPCHK(hipMemsetAsync(cnt.p, 0, 8 * (ncol + 1), st));
   const int g = (int)grid_for(ncol, 256, kMaxGrid);
@@ -449,7 +451,7 @@ cbg_status panel_rows(cbg_ctx* ctx, const std::vector<Piece>& b, bool has_val, P
     roff += (int32_t)p.nrow;
   }
   HIPCHK(hipGetLastError());
-  HIPCHK(hipStreamSynchronize(st));   // cnt/tiles/scal are released on return
+  HIPCHK(hipStreamSynchronize(st));   // cnt/tiles/scal go back to the pool on return
   out->nrow = nrow; out->ncol = ncol; out->nnz = nnz;
   out->cp = o->cp.as<int64_t>(); out->ir = o->ir.as<int32_t>(); out->val = has_val ? o->val.p : nullptr;
   out->own = o;
@@ -799,7 +801,8 @@ cbg_status fiber_exchange(cbg_grid* G, const Piece& C, size_t vs, bool f64, std:
       if (m != me) st->fiber_bytes += (4 + (has_val ? wire_vs : 0)) * snnz[m] + 8 * (cbnd[m + 1] - cbnd[m]);
   pcs->assign(L, Piece());
   const int64_t ntiles = (myc + kScanTile - 1) / kScanTile;
-  DevBuf tiles, scal;
+  PoolBuf tiles, scal;
+  tiles.pool = scal.pool = G->ctx->pool;
   HIPCHK(tiles.reserve(8 * (ntiles + 1)));
   HIPCHK(scal.reserve(16));
   int64_t off = 0;
@@ -823,7 +826,7 @@ cbg_status fiber_exchange(cbg_grid* G, const Piece& C, size_t vs, bool f64, std:
     off += rnnz[m];
   }
   HIPCHK(hipGetLastError());
-  HIPCHK(hipStreamSynchronize(cst));   // tiles/scal are released on return
+  HIPCHK(hipStreamSynchronize(cst));   // tiles/scal go back to the pool on return
   return CBG_OK;
 }
 

@@ -298,7 +298,8 @@ cbg_status mcl_prune_impl(cbg_ctx* ctx, const cbg_csc_result* in, const MclParam
   const int64_t N = in->ncol, nnz = in->nnz;
   std::unique_ptr<Owner> own(new Owner(ctx->pool));
   HIPCHK(own->cp.reserve(sizeof(int64_t) * (N + 1)));
-  DevBuf th, mode, list, cnt, tiles;
+  PoolBuf th, mode, list, cnt, tiles;
+  for (PoolBuf* b : {&th, &mode, &list, &cnt, &tiles}) b->pool = ctx->pool;
   HIPCHK(th.reserve(sizeof(V) * (N + 1)));
   HIPCHK(mode.reserve(sizeof(int32_t) * (N + 1)));
   HIPCHK(list.reserve(sizeof(int32_t) * (N + 1)));
@@ -332,7 +333,7 @@ cbg_status mcl_prune_impl(cbg_ctx* ctx, const cbg_csc_result* in, const MclParam
     k_mcl_compact<V><<<gw, 256, 0, st>>>(N, in->colptr, in->row, val, th.as<V>(), own->cp.as<int64_t>(),
                                          own->ir.as<int32_t>(), own->val.as<V>());
   HIPCHK(hipGetLastError());
-  HIPCHK(hipStreamSynchronize(st));   // th/mode/list/cnt are freed on return
+  HIPCHK(hipStreamSynchronize(st));   // th/mode/list/cnt go back to the pool on return
   memset(out, 0, sizeof(*out));
   out->nrow = in->nrow; out->ncol = N; out->nnz = onnz;
   out->colptr = own->cp.as<int64_t>(); out->row = own->ir.as<int32_t>(); out->val = own->val.p;
@@ -400,7 +401,8 @@ extern "C" cbg_status cbg_col_select(cbg_ctx* ctx, const cbg_csc_result* in, con
   const size_t vs = in->val ? dt_size(in->val_type) : 0;
   std::unique_ptr<Owner> own(new Owner(ctx->pool));
   HIPCHK(own->cp.reserve(sizeof(int64_t) * (ncols + 1)));
-  DevBuf dcols, cnt, tiles;
+  PoolBuf dcols, cnt, tiles;
+  for (PoolBuf* b : {&dcols, &cnt, &tiles}) b->pool = ctx->pool;
   HIPCHK(dcols.reserve(sizeof(int64_t) * (ncols + 1)));
   HIPCHK(cnt.reserve(sizeof(int64_t) * (ncols + 1)));
   HIPCHK(ctx->scalars.reserve(256));
@@ -434,7 +436,7 @@ extern "C" cbg_status cbg_col_select(cbg_ctx* ctx, const cbg_csc_result* in, con
     }
   }
   HIPCHK(hipGetLastError());
-  HIPCHK(hipStreamSynchronize(st));   // dcols/cnt/tiles are freed on return
+  HIPCHK(hipStreamSynchronize(st));   // dcols/cnt/tiles go back to the pool on return
   memset(out, 0, sizeof(*out));
   out->nrow = in->nrow; out->ncol = ncols; out->nnz = nnz;
   out->colptr = own->cp.as<int64_t>(); out->row = own->ir.as<int32_t>(); out->val = vs ? own->val.p : nullptr;
