@@ -1022,7 +1022,8 @@ static __global__ void k_identity_csc(int64_t n, int64_t* __restrict__ cp, int32
 inline cbg_status dedup_columns(cbg_ctx* ctx, int64_t nr, int64_t nc, int64_t nnz, const int64_t* cp,
                                 const int32_t* rows, const double* val, cbg_csc_result* out) {
   hipStream_t st = ctx->stream;
-  DevBuf icp, iir;
+  PoolBuf icp, iir;
+  icp.pool = iir.pool = ctx->pool;
   HIPCHK(icp.reserve(sizeof(int64_t) * (nr + 1)));
   HIPCHK(iir.reserve(sizeof(int32_t) * (nr + 1)));
   k_identity_csc<<<(int)grid_for(nr + 1, 256, kMaxGrid), 256, 0, st>>>(nr, icp.as<int64_t>(), iir.as<int32_t>());
@@ -1037,6 +1038,6 @@ inline cbg_status dedup_columns(cbg_ctx* ctx, int64_t nr, int64_t nc, int64_t nn
   b.on_device = 1;
   int64_t mult = 0;
   cbg_status s = cbg_dispatch_f64(ctx, &a, &b, CBG_SR_PLUS_TIMES, CBG_SORTED_COLS, out, &mult);
-  HIPCHK(hipStreamSynchronize(st));   // the identity above is released on return
+  HIPCHK(hipStreamSynchronize(st));   // the identity goes back to the pool on return
   return s;
 }
