@@ -231,15 +231,22 @@ def bench_dist(args, world, rank, local_rank):
     import combblas_amd as cb
     from combblas_amd import dist as cbd
 
-    # production: RCCL, one GPU per rank.  CBG_DIST_BACKEND=gloo rehearses the same schedule with ranks
-    # sharing the visible GPUs (blocks staged through the host), e.g. on a one-GPU box.
+    # production: RCCL, one GPU per rank.  Rehearsals with ranks sharing the visible GPUs (a one-GPU box):
+    #   CBG_DIST_BACKEND=rccl-net  the same libcbgpu RCCL grid, every rank its own RCCL "node"
+    #                              (NCCL_HOSTID) so RCCL's socket transport carries the bytes;
+    #   CBG_DIST_BACKEND=gloo      the host-staged gloo transport.
     backend = os.environ.get("CBG_DIST_BACKEND", "nccl")
+    if backend not in ("nccl", "rccl-net", "gloo"):
+        sys.exit(f"bench: CBG_DIST_BACKEND={backend!r}: expected nccl, rccl-net or gloo")
     dev = local_rank % torch.cuda.device_count()
     torch.cuda.set_device(dev)
     if backend == "nccl":
         dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
     else:
-        dist.init_process_group(backend)
+        if backend == "rccl-net":
+            os.environ.update({"NCCL_HOSTID": f"cbg-bench-rank-{rank}", "NCCL_SOCKET_IFNAME": "lo",
+                               "NCCL_IB_DISABLE": "1", "CBG_GRID_TRANSPORT": "rccl"})
+        dist.init_process_group("gloo")
     L, q, _ = cbd.grid_for(world)
     grid = cbd.CommGrid3D(L, q, q)
     ctx = cb.Context(dev)
@@ -265,15 +272,11 @@ def bench_dist(args, world, rank, local_rank):
             phases[k] = phases.get(k, 0) + st.get(k, 0)
         return st.get("multiplies", 0), nz
 
-    try:
-        step()   # first product also sets up libcbgpu's grid (RCCL communicators)
-    except Exception as e:   # RCCL grid unavailable: the same schedule over torch's own process groups
-        if os.environ.get("CBG_GRID_TRANSPORT", "rccl") != "rccl":
-            raise
-        print(f"bench: native RCCL grid failed ({e!r}); retrying over torch.distributed", file=sys.stderr)
-        os.environ["CBG_GRID_TRANSPORT"] = "torch"
-        be._grids = {}
-        step()
+    step()   # first product also sets up libcbgpu's grid (its RCCL communicators); a failure ends the run
+    ginfo = be.native_grid(grid).info()
+    if backend != "gloo" and (ginfo["kind"] != "rccl" or ginfo["ranks"] != {"world": world, "row": q, "col": q,
+                                                                          "fiber": L}):
+        sys.exit(f"bench: libcbgpu grid is not the RCCL grid of a {L}x{q}x{q} layout: {ginfo}")
     for _ in range(max(args.warmup - 1, 0)):
         step()
     phases.clear()
@@ -296,10 +299,9 @@ def bench_dist(args, world, rank, local_rank):
     dist.all_reduce(s)
     elapsed, mults, nnzc = float(t.item()), float(s[0].item()), float(s[1].item())
     if rank == 0:
-        ng = be.native_grid(grid)
         cfg = workload(args.scale, args.edgefactor,
                        f"{L}x{q}x{q} ({'3D split SUMMA' if L > 1 else '2D SUMMA'}), "
-                       f"libcbgpu grid over {ng.kind}")
+                       f"libcbgpu grid over {ginfo['kind']}")
         cfg.update({"nnz_A": nnzb, "multiplies": int(mults / args.steps), "nnz_C": int(nnzc / args.steps)})
         out = {"metric": METRIC, "value": mults / elapsed, "unit": "multiplies/s", "n_gpus": world,
                "steps": args.steps, "warmup": args.warmup, "ms_per_step": 1000.0 * elapsed / args.steps,
@@ -308,6 +310,9 @@ def bench_dist(args, world, rank, local_rank):
                "effective_GBps": balg_bytes(mults / args.steps, nnzc / args.steps, nnzb, n)
                / (elapsed / args.steps) / 1e9,
                "rank0_phases_per_step": {k: round(v / args.steps, 3) for k, v in phases.items()},
+               "grid_transport": ginfo["kind"],
+               # members of every communicator as RCCL itself counts them (ncclCommCount)
+               "rccl_ranks": ginfo["ranks"] if ginfo["kind"] == "rccl" else None,
                "input": {"generator": "SpParMat3D.from_rmat: each rank builds its own A and B pieces on its GPU "
                                       "(cbg_rmat_block, the reference's Graph500 edge stream)", "seed": args.seed,
                          "rank0_device_build_s": round(build_s, 4), "nnz": nnzb}}

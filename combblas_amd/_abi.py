@@ -69,6 +69,10 @@ class Transport(ctypes.Structure):
                 ("allgather", ALLGATHER_FN), ("host_buffers", ctypes.c_int32)]
 
 
+class GridInfo(ctypes.Structure):
+    _fields_ = [("rccl", ctypes.c_int32), ("ranks", ctypes.c_int32 * 4)]
+
+
 GROUP_ROW, GROUP_COL, GROUP_FIBER, GROUP_WORLD = range(4)
 HALVES, RUNNING_MERGE = 4, 8
 
@@ -120,6 +124,7 @@ SIGNATURES = {
     "cbg_grid_create": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(Transport), ctypes.c_int32, ctypes.c_int32,
                                        ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(ctypes.c_void_p)]),
     "cbg_grid_destroy": (ctypes.c_int, [ctypes.c_void_p]),
+    "cbg_grid_query": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(GridInfo)]),
     "cbg_spgemm_grid": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(DcscView), ctypes.POINTER(DcscView), ctypes.c_int,
                                        ctypes.c_int, ctypes.c_uint32, ctypes.POINTER(CscResult),
                                        ctypes.POINTER(GridStats)]),

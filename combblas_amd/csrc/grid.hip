@@ -995,6 +995,20 @@ cbg_status cbg_grid_destroy(cbg_grid* G) {
   return CBG_OK;
 }
 
+cbg_status cbg_grid_query(const cbg_grid* G, cbg_grid_info* info) {
+  if (!G || !info) return CBG_EINVAL;
+  info->rccl = G->rccl ? 1 : 0;
+  for (int g = 0; g < 4; ++g) {
+    info->ranks[g] = G->gsize(g);
+    if (G->rccl && G->comm[g]) {
+      int n = 0;
+      NCCLCHK(ncclCommCount(G->comm[g], &n));
+      info->ranks[g] = n;
+    }
+  }
+  return CBG_OK;
+}
+
 cbg_status cbg_summa_layer(cbg_grid* G, const cbg_dcsc_view* A, const cbg_dcsc_view* B, cbg_semiring sr,
                            cbg_dtype dt, uint32_t flags, cbg_csc_result* parts, int32_t* nparts,
                            cbg_grid_stats* st) {

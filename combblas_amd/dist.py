@@ -935,24 +935,29 @@ def _dev_u8(ptr, n, device):
 
 
 class _NativeGrid:
-    """libcbgpu's cbg_grid for one CommGrid3D.  torch.distributed on nccl (RCCL): the library's own
-    RCCL communicators (world + ncclCommSplit row/col/fiber; the unique id travels over the default
-    group).  Otherwise (gloo): a cbg_transport whose callbacks stage device buffers through the host
-    and run the collective on the grid's torch process groups."""
+    """libcbgpu's cbg_grid for one CommGrid3D.  RCCL: the library's own RCCL communicators (world +
+    ncclCommSplit row/col/fiber; the unique id travels over the default torch group) -- the default on
+    an nccl (RCCL) process group, and forced on any group by CBG_GRID_TRANSPORT=rccl (the one-GPU
+    multi-rank tests run it under gloo).  CBG_GRID_TRANSPORT=torch, or a gloo group: a cbg_transport
+    whose callbacks stage device buffers through the host and run the collective on the grid's torch
+    process groups."""
 
     def __init__(self, grid, backend):
         self.lib = backend.ctx._lib
         self.grid, self.backend = grid, backend
         self.ptr = ctypes.c_void_p()
         L, q = grid.L, grid.q
-        use_rccl = dist.get_backend() == "nccl" and os.environ.get("CBG_GRID_TRANSPORT", "rccl") == "rccl"
+        mode = os.environ.get("CBG_GRID_TRANSPORT", "auto")
+        if mode not in ("auto", "rccl", "torch"):
+            raise ValueError(f"CBG_GRID_TRANSPORT={mode!r}: expected auto, rccl or torch")
+        use_rccl = mode == "rccl" or (mode == "auto" and dist.get_backend() == "nccl")
         if use_rccl:
             uid = torch.zeros(128, dtype=torch.uint8)
             if grid.rank == 0:
                 buf = ctypes.create_string_buffer(128)
                 _abi.check(self.lib.cbg_rccl_unique_id(buf), "cbg_rccl_unique_id")
                 uid = torch.frombuffer(bytearray(buf.raw), dtype=torch.uint8).clone()
-            t = uid.to(backend.device)
+            t = uid.to(backend.comm_device)
             dist.broadcast(t, src=0)
             raw = bytes(t.cpu().numpy().tobytes())
             idbuf = ctypes.create_string_buffer(raw, 128)
@@ -1027,6 +1032,16 @@ class _NativeGrid:
         except Exception as e:  # pragma: no cover
             print(f"cbg transport allgather: {e!r}", flush=True)
             return 1
+
+    def info(self):
+        """{"kind": "rccl" | caller transport, "ranks": {world, row, col, fiber}}: for RCCL the member
+        counts RCCL itself reports for each communicator (ncclCommCount)."""
+        gi = _abi.GridInfo()
+        _abi.check(self.lib.cbg_grid_query(self.ptr, ctypes.byref(gi)), "cbg_grid_query")
+        r = list(gi.ranks)
+        return {"kind": "rccl" if gi.rccl else self.kind,
+                "ranks": {"world": r[_abi.GROUP_WORLD], "row": r[_abi.GROUP_ROW], "col": r[_abi.GROUP_COL],
+                          "fiber": r[_abi.GROUP_FIBER]}}
 
     def close(self):
         if self.ptr:

@@ -300,6 +300,14 @@ cbg_status cbg_grid_create_rccl(cbg_ctx* ctx, const char id[128], int32_t world,
 cbg_status cbg_grid_create(cbg_ctx* ctx, const cbg_transport* t, int32_t world, int32_t rank, int32_t layers,
                            int32_t rows, int32_t cols, cbg_grid** grid);
 cbg_status cbg_grid_destroy(cbg_grid* grid);
+/* What a grid runs over.  rccl = 1: the library's RCCL communicators, ranks[g] = ncclCommCount of the
+ * communicator of group g (ROW, COL, FIBER, WORLD; 1 for a group of one, which needs no collective);
+ * rccl = 0: a caller transport, ranks[g] = the group sizes. */
+typedef struct {
+  int32_t rccl;
+  int32_t ranks[4];
+} cbg_grid_info;
+cbg_status cbg_grid_query(const cbg_grid* grid, cbg_grid_info* info);
 
 /* C piece = A (x) B over the grid.  Dimension mismatch on any rank -> CBG_EDIM on every rank. */
 cbg_status cbg_spgemm_grid(cbg_grid* grid, const cbg_dcsc_view* A, const cbg_dcsc_view* B, cbg_semiring sr,

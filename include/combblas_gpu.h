@@ -6,12 +6,16 @@
  *   combblas::gpu::LocalHybridSpGEMM<SR, NTO>(A, B, clearA, clearB, aux)  mtSpGEMM.h:212-217
  *   combblas::gpu::LocalSpGEMM<SR, NTO>(A, B, clearA, clearB)             mtSpGEMM.h:73-78
  *   combblas::gpu::MultiwayMerge<SR>(lists, mdim, ndim, delarrs)          MultiwayMerge.h:411-412
+ *   combblas::gpu::MultiwayMergeHash<SR>(lists, mdim, ndim, delarrs, sorted) MultiwayMerge.h:536-537
  *   combblas::gpu::EstimateLocalFLOP<SR>(A, B)                             mtSpGEMM.h:667-694
  *   combblas::gpu::MCLPruneRecoverySelect(A, thr, select, recover, pct, v) ParFriends.h:185-353
  *   combblas::gpu::Mult_AnXBn_Synch<SR, NUO, UDERO>(A, B, clearA, clearB) ParFriends.h:1004-1108
  *   combblas::gpu::Mult_AnXBn_DoubleBuff / Mult_AnXBn_Overlap           ParFriends.h:798-997, 1110-1235
  *   combblas::gpu::PSpGEMM<SR>(A, B)                                      SpParMat.h:451-464
  *   combblas::gpu::Mult_AnXBn_SUMMA3D<SR, NUO, UDERO>(A3D, B3D)          ParFriends.h:2918-3208
+ *   combblas::gpu::multiply(splitA, splitB, CMG, isBT, threaded)           3DSpGEMM/Multiplier.h:10-61
+ *   combblas::gpu::SUMMALayer(splitA, splitB, C, CMG, isBT, threaded)      3DSpGEMM/SUMMALayer.h:24-97
+ *     (the 3DSpGEMM pair is declared when 3DSpGEMM/CCGrid.h is included before this header)
  *
  * The distributed ones run the whole SUMMA (stage broadcasts, local products, merges, fiber
  * exchange) inside libcbgpu on the device (cbg_spgemm_grid) over the SpParMat's own MPI
@@ -166,48 +170,69 @@ int64_t EstimateLocalFLOP(const SpDCCols<IT, NT1>& A, const SpDCCols<IT, NT2>& B
   return mults;
 }
 
+// device merge of SpTuples lists of one shape (cbg_merge): duplicates combine with SR::add in list order
+// (MultiwayMerge.h:357); `sorted` = whether the output's rows are sorted per column (always true here)
+template <class SR, class IT, class NT>
+SpTuples<IT, NT>* merge_lists(std::vector<SpTuples<IT, NT>*>& lists, IT mdim, IT ndim, bool delarrs, const char* who) {
+  if (lists.empty()) return new SpTuples<IT, NT>(0, mdim, ndim);
+  cbg_ctx* ctx = context();
+  std::vector<cbg_csc_result> parts(lists.size());
+  std::vector<std::vector<int64_t>> cps(lists.size());
+  std::vector<std::vector<int32_t>> rows(lists.size());
+  std::vector<std::vector<Store<NT>>> vals(lists.size());
+  for (size_t l = 0; l < lists.size(); ++l) {   // SpTuples -> host CSC (column order kept) -> device (cbg_upload)
+    SpTuples<IT, NT>& T = *lists[l];
+    const IT m = T.getnrow(), n = T.getncol();
+    if ((mdim && m != mdim) || (ndim && n != ndim)) throw std::runtime_error(std::string(who) + ": dimension mismatch");
+    T.SortColBased();
+    cps[l].assign(n + 1, 0);
+    rows[l].resize(T.getnnz() > 0 ? T.getnnz() : 1);
+    vals[l].resize(T.getnnz() > 0 ? T.getnnz() : 1);
+    for (int64_t k = 0; k < T.getnnz(); ++k) {
+      ++cps[l][T.colindex(k) + 1];
+      rows[l][k] = (int32_t)T.rowindex(k);
+      vals[l][k] = (Store<NT>)T.numvalue(k);
+    }
+    for (IT j = 0; j < n; ++j) cps[l][j + 1] += cps[l][j];
+    cbg_dcsc_view v{};
+    v.nrow = m; v.ncol = n; v.nnz = T.getnnz(); v.nzc = n;
+    v.cp = cps[l].data(); v.ir = rows[l].data(); v.idx_bytes = 4; v.ptr_bytes = 8;
+    v.val = vals[l].data(); v.val_type = DeviceType<NT>::code; v.on_device = 0;
+    cbg_status s = cbg_upload(ctx, &v, &parts[l]);
+    if (s != CBG_OK) {
+      for (size_t k = 0; k < l; ++k) cbg_result_free(ctx, &parts[k]);
+      check(s, "cbg_upload");
+    }
+  }
+  cbg_csc_result C{};
+  cbg_status s = cbg_merge(ctx, parts.data(), (int32_t)parts.size(), DeviceSemiring<SR>::code, DeviceType<NT>::code,
+                           CBG_SORTED_COLS, &C);
+  for (auto& p : parts) cbg_result_free(ctx, &p);
+  check(s, "cbg_merge");
+  if (delarrs)
+    for (auto* T : lists) delete T;
+  return to_tuples<IT, NT>(ctx, C);
+}
+
 // MultiwayMerge: column-sorted partial products of one shape -> one SpTuples (duplicates: SR::add)
 template <class SR, class IT, class NT>
 SpTuples<IT, NT>* MultiwayMerge(std::vector<SpTuples<IT, NT>*>& lists, IT mdim = 0, IT ndim = 0,
                                 bool delarrs = false) {
+  if constexpr (!(DeviceSemiring<SR>::ok && DeviceType<NT>::ok)) return combblas::MultiwayMerge<SR>(lists, mdim, ndim, delarrs);
+  else return merge_lists<SR>(lists, mdim, ndim, delarrs, "MultiwayMerge");
+}
+
+// MultiwayMergeHash (MultiwayMerge.h:536-684): inputs need not be row-sorted; duplicates combine in list
+// order (SR::add(curval, existing), :357).  The device merge always emits row-sorted columns, which
+// is what sorted = true asks for and a valid order for sorted = false.
+template <class SR, class IT, class NT>
+SpTuples<IT, NT>* MultiwayMergeHash(std::vector<SpTuples<IT, NT>*>& lists, IT mdim = 0, IT ndim = 0,
+                                    bool delarrs = false, bool sorted = true) {
   if constexpr (!(DeviceSemiring<SR>::ok && DeviceType<NT>::ok)) {
-    return combblas::MultiwayMerge<SR>(lists, mdim, ndim, delarrs);
+    return combblas::MultiwayMergeHash<SR>(lists, mdim, ndim, delarrs, sorted);
   } else {
-    if (lists.empty()) return new SpTuples<IT, NT>(0, mdim, ndim);
-    cbg_ctx* ctx = context();
-    std::vector<cbg_csc_result> parts(lists.size());
-    std::vector<cbg_dcsc_view> views(lists.size());
-    std::vector<std::vector<int64_t>> cps(lists.size());
-    std::vector<std::vector<int32_t>> rows(lists.size());
-    std::vector<std::vector<Store<NT>>> vals(lists.size());
-    for (size_t l = 0; l < lists.size(); ++l) {   // SpTuples -> host CSC -> device (cbg_upload)
-      SpTuples<IT, NT>& T = *lists[l];
-      const IT m = T.getnrow(), n = T.getncol();
-      if ((mdim && m != mdim) || (ndim && n != ndim)) throw std::runtime_error("MultiwayMerge: dimension mismatch");
-      T.SortColBased();
-      cps[l].assign(n + 1, 0);
-      rows[l].resize(T.getnnz() > 0 ? T.getnnz() : 1);
-      vals[l].resize(T.getnnz() > 0 ? T.getnnz() : 1);
-      for (int64_t k = 0; k < T.getnnz(); ++k) {
-        ++cps[l][T.colindex(k) + 1];
-        rows[l][k] = (int32_t)T.rowindex(k);
-        vals[l][k] = (Store<NT>)T.numvalue(k);
-      }
-      for (IT j = 0; j < n; ++j) cps[l][j + 1] += cps[l][j];
-      cbg_dcsc_view v{};
-      v.nrow = m; v.ncol = n; v.nnz = T.getnnz(); v.nzc = n;
-      v.cp = cps[l].data(); v.ir = rows[l].data(); v.idx_bytes = 4; v.ptr_bytes = 8;
-      v.val = vals[l].data(); v.val_type = DeviceType<NT>::code; v.on_device = 0;
-      check(cbg_upload(ctx, &v, &parts[l]), "cbg_upload");
-    }
-    cbg_csc_result C{};
-    cbg_status s = cbg_merge(ctx, parts.data(), (int32_t)parts.size(), DeviceSemiring<SR>::code,
-                             DeviceType<NT>::code, CBG_SORTED_COLS, &C);
-    for (auto& p : parts) cbg_result_free(ctx, &p);
-    check(s, "cbg_merge");
-    if (delarrs)
-      for (auto* T : lists) delete T;
-    return to_tuples<IT, NT>(ctx, C);
+    (void)sorted;
+    return merge_lists<SR>(lists, mdim, ndim, delarrs, "MultiwayMergeHash");
   }
 }
 
@@ -297,8 +322,10 @@ struct GridHandle {
   ~GridHandle() { if (grid) cbg_grid_destroy(grid); }
 };
 
+// grid_rank: the rank's position l*rows*cols + i*cols + j in the library's grid numbering (default: its
+// rank in `world`, which is that numbering for CommGrid / CommGrid3D; CCGrid numbers layers fastest)
 inline cbg_grid* make_grid(GridHandle& h, MPI_Comm world, MPI_Comm row, MPI_Comm col, MPI_Comm fiber, int layers,
-                           int rows, int cols) {
+                           int rows, int cols, int grid_rank = -1) {
   h.mt.comm[CBG_GROUP_ROW] = row; h.mt.comm[CBG_GROUP_COL] = col;
   h.mt.comm[CBG_GROUP_FIBER] = fiber; h.mt.comm[CBG_GROUP_WORLD] = world;
   cbg_transport t{};
@@ -307,7 +334,8 @@ inline cbg_grid* make_grid(GridHandle& h, MPI_Comm world, MPI_Comm row, MPI_Comm
   int wsize = 0, wrank = 0;
   MPI_Comm_size(world, &wsize);
   MPI_Comm_rank(world, &wrank);
-  check(cbg_grid_create(context(), &t, wsize, wrank, layers, rows, cols, &h.grid), "cbg_grid_create");
+  check(cbg_grid_create(context(), &t, wsize, grid_rank >= 0 ? grid_rank : wrank, layers, rows, cols, &h.grid),
+        "cbg_grid_create");
   return h.grid;
 }
 
@@ -405,6 +433,70 @@ SpParMat3D<IU, NUO, UDERO> Mult_AnXBn_SUMMA3D(SpParMat3D<IU, NU1, UDER1>& A, SpP
     return SpParMat3D<IU, NUO, UDERO>(D, G, true, false);
   }
 }
+
+#ifdef _CC_GRID_
+// ------------------------------------------------------------ 3DSpGEMM (split-3D driver of 2015)
+// CCGrid (3DSpGEMM/CCGrid.h:9-30) numbers ranks layer-fastest; its rowWorld / colWorld / fiberWorld are
+// ordered by proc column / proc row / layer, which are the library's member indices of ROW / COL / FIBER.
+// splitA = A[row block i, layer-l part of column block j], splitB = B[layer-l part of row block i, column
+// block j] (SplitMat, SplitMatDist.h:143-213); the product piece is the layer-l part of C's block (i, j)
+// (ParallelReduce_Alltoall_threaded, Reductions.h:36-130).  PlusTimes over NT, as the reference hard-codes.
+inline int ccgrid_rank(const CCGrid& CMG) {
+  return CMG.layer_grid * CMG.GridRows * CMG.GridCols + CMG.RankInCol * CMG.GridCols + CMG.RankInRow;
+}
+
+inline void ccgrid_handle(GridHandle& h, CCGrid& CMG) {
+  if (CMG.GridRows != CMG.GridCols) throw std::runtime_error("3DSpGEMM: square layer grid required (3002)");
+  make_grid(h, MPI_COMM_WORLD, CMG.rowWorld, CMG.colWorld, CMG.fiberWorld, CMG.GridLayers, CMG.GridRows, CMG.GridCols,
+            ccgrid_rank(CMG));
+}
+
+// isBT: splitB holds B's piece locally transposed ("outer" mode of test_mpipspgemm.cpp:101-117)
+template <typename IT, typename NT>
+cbg_dcsc_view b_view(SpDCCols<IT, NT>& splitB, bool isBT, std::unique_ptr<SpDCCols<IT, NT>>& tmp) {
+  if (!isBT) return view_of(splitB);
+  tmp.reset(new SpDCCols<IT, NT>(splitB));
+  tmp->Transpose();
+  return view_of(*tmp);
+}
+
+// SUMMALayer (SUMMALayer.h:24-97): the q stage products of this rank's layer, unmerged, in stage order
+template <typename IT, typename NT>
+void SUMMALayer(SpDCCols<IT, NT>& SplitA, SpDCCols<IT, NT>& SplitB, std::vector<SpTuples<IT, NT>*>& C, CCGrid& CMG,
+                bool isBT, bool threaded) {
+  static_assert(DeviceType<NT>::ok, "3DSpGEMM on the device: NT must be a device value type");
+  (void)threaded;   // LocalSpGEMM vs MultiplyReturnTuples is a CPU choice: one device product
+  GridHandle h;
+  ccgrid_handle(h, CMG);
+  std::unique_ptr<SpDCCols<IT, NT>> bt;
+  cbg_dcsc_view va = view_of(SplitA), vb = b_view(SplitB, isBT, bt);
+  std::vector<cbg_csc_result> parts(2 * CMG.GridCols + 2);
+  int32_t n = 0;
+  cbg_grid_stats st{};
+  check(cbg_summa_layer(h.grid, &va, &vb, CBG_SR_PLUS_TIMES, DeviceType<NT>::code, CBG_SORTED_COLS, parts.data(), &n,
+                        &st), "cbg_summa_layer");
+  for (int32_t k = 0; k < n; ++k) C.push_back(to_tuples<IT, NT>(context(), parts[k]));
+}
+
+// multiply (Multiplier.h:10-61) = SUMMALayer + ReduceAll_threaded, run as one device product
+template <typename IT, typename NT>
+SpDCCols<IT, NT>* multiply(SpDCCols<IT, NT>& splitA, SpDCCols<IT, NT>& splitB, CCGrid& CMG, bool isBT, bool threaded) {
+  static_assert(DeviceType<NT>::ok, "3DSpGEMM on the device: NT must be a device value type");
+  (void)threaded;
+  GridHandle h;
+  ccgrid_handle(h, CMG);
+  std::unique_ptr<SpDCCols<IT, NT>> bt;
+  cbg_dcsc_view va = view_of(splitA), vb = b_view(splitB, isBT, bt);
+  cbg_csc_result C{};
+  cbg_grid_stats st{};
+  check(cbg_spgemm_grid(h.grid, &va, &vb, CBG_SR_PLUS_TIMES, DeviceType<NT>::code, CBG_SORTED_COLS, &C, &st),
+        "cbg_spgemm_grid");
+  SpTuples<IT, NT>* t = to_tuples<IT, NT>(context(), C);
+  SpDCCols<IT, NT>* D = new SpDCCols<IT, NT>(*t, false);
+  delete t;
+  return D;
+}
+#endif  // _CC_GRID_
 
 }  // namespace gpu
 }  // namespace combblas

@@ -78,12 +78,36 @@ def random_csc(n, m, density, seed, dtype=np.float64, integer=True):
     return M
 
 
+def init_group(rank, world, port, backend_kind):
+    """torch process group of one test rank.  backend_kind:
+      "scipy" / "gpu"  gloo; libcbgpu's grid runs over the host-staged gloo transport;
+      "gpu-rccl"       nccl, one rank (RCCL refuses two ranks of one host on one device);
+      "gpu-rccl-net"   gloo for the harness, libcbgpu's grid over its OWN RCCL communicators with every rank
+                       on cuda:0: NCCL_HOSTID makes each rank its own RCCL "node", so RCCL's duplicate-GPU
+                       check passes and its network (socket, loopback) transport carries the data.  The
+                       broadcasts, grouped send/recv and all-gathers are the production RCCL calls on the
+                       library's streams -- asynchronous, fenced by its HIP events -- not a stand-in."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    if backend_kind == "gpu-rccl":
+        torch.cuda.set_device(0)
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", 0))
+        return
+    if backend_kind == "gpu-rccl-net":
+        os.environ.update({"NCCL_HOSTID": f"cbg-test-rank-{rank}", "NCCL_SOCKET_IFNAME": "lo",
+                           "NCCL_IB_DISABLE": "1", "CBG_GRID_TRANSPORT": "rccl"})
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+
+def rccl_info(grid):
+    """The cbg_grid_query record an RCCL grid of this shape must report."""
+    return {"kind": "rccl", "ranks": {"world": grid.world, "row": grid.q, "col": grid.q, "fiber": grid.L}}
+
+
 def run_dist_case(rank, world, port, backend_kind, cases, errq):
     """Per-rank body: init gloo, build the mandated grid for `world`, run every case."""
     try:
-        os.environ["MASTER_ADDR"] = "127.0.0.1"
-        os.environ["MASTER_PORT"] = str(port)
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        init_group(rank, world, port, backend_kind)
         L, q, _ = cbd.grid_for(world)
         grid = cbd.CommGrid3D(L, q, q)
         if backend_kind == "scipy":
@@ -128,9 +152,7 @@ def run_mcl_case(rank, world, port, backend_kind, cases, errq):
     """Per-rank body of the distributed HipMCL expansion (MemEfficientSpGEMM + prune): every rank
     checks its piece against the oracle's prune of the global product (complete columns)."""
     try:
-        os.environ["MASTER_ADDR"] = "127.0.0.1"
-        os.environ["MASTER_PORT"] = str(port)
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        init_group(rank, world, port, backend_kind)
         L, q, _ = cbd.grid_for(world)
         grid = cbd.CommGrid3D(L, q, q)
         if backend_kind == "scipy":
@@ -226,9 +248,7 @@ def run_index_case(rank, world, port, backend_kind, cases, errq):
     """Per-rank body of the 2D drivers (Synch / DoubleBuff / Overlap) and of the SpGEMM-based
     indexing (SubsRef_SR, Prune, PruneFull, SpAsgn; SpParMat.cpp:2028-2562) on a one-layer grid."""
     try:
-        os.environ["MASTER_ADDR"] = "127.0.0.1"
-        os.environ["MASTER_PORT"] = str(port)
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        init_group(rank, world, port, backend_kind)
         q = int(round(world ** 0.5))
         grid = cbd.CommGrid(q, q)
         if backend_kind == "scipy":
@@ -326,13 +346,7 @@ def run_fixture_case(rank, world, port, backend_kind, cases, errq):
     fixture, with Mult_AnXBn_SUMMA3D and -- on one-layer grids -- Synch / DoubleBuff / Overlap, and
     the 3DSpGEMM multiply (SUMMALayer + ReduceAll_threaded).  Each rank checks its own piece."""
     try:
-        os.environ["MASTER_ADDR"] = "127.0.0.1"
-        os.environ["MASTER_PORT"] = str(port)
-        if backend_kind == "gpu-rccl":   # libcbgpu's own RCCL communicators (one rank per GPU)
-            torch.cuda.set_device(0)
-            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", 0))
-        else:
-            dist.init_process_group("gloo", rank=rank, world_size=world)
+        init_group(rank, world, port, backend_kind)
         L, q, _ = cbd.grid_for(world)
         grid = cbd.CommGrid3D(L, q, q)
         import combblas_amd as cb
@@ -364,8 +378,8 @@ def run_fixture_case(rank, world, port, backend_kind, cases, errq):
             t = torch.tensor([stats.get("multiplies", 0)], dtype=torch.int64, device=be.comm_device)
             dist.all_reduce(t)
             assert int(t.item()) == int(z[f"C_{tag}_flops"]), (int(t.item()), int(z[f"C_{tag}_flops"]))
-            if backend_kind == "gpu-rccl":
-                assert be.native_grid(grid).kind == "rccl"
+            if backend_kind.startswith("gpu-rccl"):   # RCCL itself counted the members of every group
+                assert be.native_grid(grid).info() == rccl_info(grid), be.native_grid(grid).info()
         dist.barrier()
         dist.destroy_process_group()
     except Exception as e:
@@ -380,11 +394,9 @@ def run_block_case(rank, world, port, backend_kind, cases, errq):
     block of A*A against the same block of the reference-built golden product, every BlockSplit piece
     against the slice of A, and Convert2D of colsplit / rowsplit 3D layouts against the 2D blocks."""
     try:
-        os.environ["MASTER_ADDR"] = "127.0.0.1"
-        os.environ["MASTER_PORT"] = str(port)
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        init_group(rank, world, port, backend_kind)
         import combblas_amd as cb
-        be = cbd.GpuBackend(cb.Context(0)) if backend_kind == "gpu" else ScipyBackend()
+        be = cbd.GpuBackend(cb.Context(0)) if backend_kind.startswith("gpu") else ScipyBackend()
         from helpers import fixture_inputs, fixture_product, load_fixture
         q = int(round(world ** 0.5))
         grid = cbd.CommGrid(q, q)
@@ -431,9 +443,7 @@ def run_rmat_case(rank, world, port, backend_kind, cases, errq):
     (SpParMat3D.from_rmat -> cbg_rmat_block), which must equal the same blocks of the reference-generated
     matrix in the fixture, and the SUMMA3D product of those pieces must equal the reference's product."""
     try:
-        os.environ["MASTER_ADDR"] = "127.0.0.1"
-        os.environ["MASTER_PORT"] = str(port)
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        init_group(rank, world, port, backend_kind)
         L, q, _ = cbd.grid_for(world)
         grid = cbd.CommGrid3D(L, q, q)
         import combblas_amd as cb
@@ -482,9 +492,7 @@ def run_mcl_fixture_case(rank, world, port, backend_kind, cases, errq):
     through MemEfficientSpGEMM / MemEfficientSpGEMM3D on the mandated layout with phases 1..3: every
     phase count gives the reference's pruned product on every rank's piece and the same branch counts."""
     try:
-        os.environ["MASTER_ADDR"] = "127.0.0.1"
-        os.environ["MASTER_PORT"] = str(port)
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        init_group(rank, world, port, backend_kind)
         L, q, _ = cbd.grid_for(world)
         grid = cbd.CommGrid3D(L, q, q)
         import combblas_amd as cb

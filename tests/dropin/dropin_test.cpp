@@ -11,6 +11,14 @@
 // SpParMat operands; run it under mpirun -np 1 or 4 (square grids, CommGrid.cpp:44-50).
 //   usage: dropin_test [--expect-no-gpu]
 // Exit 0 = all equal (or, with --expect-no-gpu, the device path threw a device error).
+//
+// 3D mode (mpirun -np q*q*L):  dropin_test --3d <q> <L> <A.mtx> <C.mtx> <G.mtx>
+//   * the split-3D driver of 3DSpGEMM exactly as test_mpipspgemm.cpp:101-153 sets it up (CCGrid, ReadMat
+//     unpermuted, SplitMat): gpu::multiply (column and outer/isBT modes) and gpu::SUMMALayer against the
+//     reference's multiply / SUMMALayer on the same split pieces, and against controlC (C.mtx = MATLAB A*A);
+//   * gpu::Mult_AnXBn_SUMMA3D against the reference's Mult_AnXBn_SUMMA3D (ParFriends.h:2918-3208) on
+//     SpParMat3D(A2D, L, colsplit) x SpParMat3D(A2D, L, rowsplit) for A = A.mtx (real values: within
+//     1e-12 of max(|c|, sum|a*b|)) and A = G.mtx (integer values: bit-exact), rank piece by rank piece.
 #include <mpi.h>
 #include <cstdio>
 #include <cstdlib>
@@ -18,8 +26,16 @@
 #include <tuple>
 #include <vector>
 #include "CombBLAS/CombBLAS.h"
+#include "3DSpGEMM/CCGrid.h"
+#include "3DSpGEMM/Reductions.h"
+#include "3DSpGEMM/Multiplier.h"
+#include "3DSpGEMM/SplitMatDist.h"
 #include "combblas_gpu.h"
 using namespace combblas;
+
+// timers the 3DSpGEMM headers declare extern (3DSpGEMM/Glue.h; test_mpipspgemm.cpp:22-30 defines them)
+double comm_bcast, comm_reduce, comp_summa, comp_reduce, comp_result, comp_reduce_layer, comp_split, comp_trans,
+    comm_split;
 
 typedef int64_t I;
 
@@ -100,8 +116,133 @@ struct MaxTimesSR {   // no device functor: must run the reference CPU template
   static T_promote multiply(const T1& a, const T2& b) { return (T_promote)a * (T_promote)b; }
 };
 
+// device product vs reference product: identical structure; values within 1e-12 * max(|ref|, scale) where
+// `scale` (same structure) holds sum|a*b| per entry, or bit-exact when scale is null
+template <class IT, class T>
+bool close(SpTuples<IT, T>* d, SpTuples<IT, T>* r, SpTuples<IT, T>* scale, const char* what) {
+  d->SortColBased();
+  r->SortColBased();
+  if (scale) scale->SortColBased();
+  if (d->getnnz() != r->getnnz() || (scale && scale->getnnz() != r->getnnz())) {
+    printf("%s: nnz %lld vs %lld\n", what, (long long)d->getnnz(), (long long)r->getnnz());
+    return false;
+  }
+  int64_t off = 0;
+  for (IT k = 0; k < r->getnnz(); ++k) {
+    if (d->rowindex(k) != r->rowindex(k) || d->colindex(k) != r->colindex(k)) {
+      printf("%s: entry %lld at (%lld,%lld) vs (%lld,%lld)\n", what, (long long)k, (long long)d->rowindex(k),
+             (long long)d->colindex(k), (long long)r->rowindex(k), (long long)r->colindex(k));
+      return false;
+    }
+    const double a = (double)d->numvalue(k), b = (double)r->numvalue(k);
+    const double tol = scale ? 1e-12 * std::max(std::fabs(b), (double)scale->numvalue(k)) : 0.0;
+    if (std::fabs(a - b) > tol) ++off;
+  }
+  printf("%s: %lld entries, %lld off\n", what, (long long)r->getnnz(), (long long)off);
+  return off == 0;
+}
+
+template <class IT, class T>
+SpDCCols<IT, T> abs_copy(const SpDCCols<IT, T>& M) {
+  SpDCCols<IT, T> c(M);
+  c.Apply([](T x) { return (T)std::fabs((double)x); });
+  return c;
+}
+
+// the split-3D driver (3DSpGEMM) and Mult_AnXBn_SUMMA3D against the reference's own on the same pieces
+int run3d(int q, int L, const std::string& fa, const std::string& fc, const std::string& fg) {
+  int rc = 0;
+  {
+    CCGrid CMG(L, q);
+    typedef int32_t IT3;
+    SpDCCols<IT3, double> splitA, splitB, controlC;
+    {
+      std::shared_ptr<CommGrid> layerGrid(new CommGrid(CMG.layerWorld, 0, 0));
+      FullyDistVec<IT3, IT3> p(layerGrid);
+      SpDCCols<IT3, double>* A = ReadMat<double>(fa, CMG, false, p);
+      SpDCCols<IT3, double>* B = ReadMat<double>(fa, CMG, false, p);
+      SpDCCols<IT3, double>* C = ReadMat<double>(fc, CMG, false, p);
+      SplitMat(CMG, A, splitA, false);
+      SplitMat(CMG, B, splitB, true);
+      SplitMat(CMG, C, controlC, false);
+    }
+    SpDCCols<IT3, double> absA = abs_copy(splitA), absB = abs_copy(splitB);
+    SpDCCols<IT3, double>* S = multiply(absA, absB, CMG, false, true);   // sum|a*b| per entry (reference)
+    SpDCCols<IT3, double>* R = multiply(splitA, splitB, CMG, false, true);
+    SpDCCols<IT3, double>* D = gpu::multiply(splitA, splitB, CMG, false, true);
+    SpTuples<IT3, double> st(*S);
+    {
+      SpTuples<IT3, double> dt(*D), rt(*R), ct(controlC), s2(st);
+      if (!close(&dt, &rt, &st, "gpu::multiply vs reference multiply")) rc = 1;
+      if (!close(&dt, &ct, &s2, "gpu::multiply vs MATLAB C.mtx (controlC)")) rc = 1;
+    }
+    SpDCCols<IT3, double> splitBT(splitB);
+    splitBT.Transpose();   // "outer": B held locally transposed (test_mpipspgemm.cpp:101-107)
+    SpDCCols<IT3, double>* DO = gpu::multiply(splitA, splitBT, CMG, true, false);
+    {
+      SpTuples<IT3, double> dt(*DO), rt(*R);
+      if (!close(&dt, &rt, &st, "gpu::multiply isBT vs reference multiply")) rc = 1;
+    }
+    std::vector<SpTuples<IT3, double>*> rl, dl, sl;
+    SUMMALayer(splitA, splitB, rl, CMG, false, true);
+    gpu::SUMMALayer(splitA, splitB, dl, CMG, false, true);
+    SUMMALayer(absA, absB, sl, CMG, false, true);
+    if (rl.size() != dl.size()) { printf("SUMMALayer: %zu vs %zu stage products\n", dl.size(), rl.size()); rc = 1; }
+    for (size_t k = 0; k < std::min(rl.size(), dl.size()); ++k) {
+      char what[64];
+      snprintf(what, sizeof what, "gpu::SUMMALayer stage %zu", k);
+      if (!close(dl[k], rl[k], sl[k], what)) rc = 1;
+    }
+    for (auto* t : rl) delete t;
+    for (auto* t : dl) delete t;
+    for (auto* t : sl) delete t;
+    delete S; delete R; delete D; delete DO;
+  }
+  // Mult_AnXBn_SUMMA3D on SpParMat3D(A2D, L, colsplit) x SpParMat3D(A2D, L, rowsplit)
+  for (int f = 0; f < 2; ++f) {
+    typedef SpDCCols<I, double> DCC;
+    typedef SpParMat<I, double, DCC> PM;
+    typedef SpParMat3D<I, double, DCC> PM3;
+    typedef PlusTimesSRing<double, double> PT;
+    const std::string& file = f == 0 ? fa : fg;
+    std::shared_ptr<CommGrid> grid(new CommGrid(MPI_COMM_WORLD, 0, 0));
+    PM A(grid), B(grid);
+    A.ParallelReadMM(file, true, maximum<double>());
+    B.ParallelReadMM(file, true, maximum<double>());
+    PM3 A3(A, L, true, false), B3(B, L, false, false);
+    PM3 R = Mult_AnXBn_SUMMA3D<PT, double, DCC>(A3, B3);
+    PM3 D = gpu::Mult_AnXBn_SUMMA3D<PT, double, DCC>(A3, B3);
+    SpTuples<I, double> rt(*R.seqptr()), dt(*D.seqptr());
+    if (f == 0) {
+      PM Aa(A), Ba(B);
+      Aa.Apply([](double x) { return std::fabs(x); });
+      Ba.Apply([](double x) { return std::fabs(x); });
+      PM3 Aa3(Aa, L, true, false), Ba3(Ba, L, false, false);
+      PM3 S3 = Mult_AnXBn_SUMMA3D<PT, double, DCC>(Aa3, Ba3);
+      SpTuples<I, double> s3(*S3.seqptr());
+      if (!close(&dt, &rt, &s3, "gpu::Mult_AnXBn_SUMMA3D vs reference (A.mtx)")) rc = 1;
+    } else {
+      if (!close(&dt, &rt, (SpTuples<I, double>*)nullptr, "gpu::Mult_AnXBn_SUMMA3D vs reference (G.mtx, exact)")) rc = 1;
+    }
+  }
+  int any = 0;
+  MPI_Allreduce(&rc, &any, 1, MPI_INT, MPI_MAX, MPI_COMM_WORLD);
+  return any;
+}
+
 int main(int argc, char** argv) {
   MPI_Init(&argc, &argv);
+  if (argc == 7 && std::string(argv[1]) == "--3d") {
+    int rc = 1;
+    try {
+      rc = run3d(atoi(argv[2]), atoi(argv[3]), argv[4], argv[5], argv[6]);
+    } catch (std::exception& e) {
+      printf("3d: %s\n", e.what());
+    }
+    MPI_Finalize();
+    printf(rc == 0 ? "DROPIN3D OK\n" : "DROPIN3D FAILED\n");
+    return rc;
+  }
   const bool expect_no_gpu = argc > 1 && std::string(argv[1]) == "--expect-no-gpu";
   int rc = 0;
   {

@@ -65,6 +65,22 @@ def test_rccl_native_grid_single_rank():
     spawn_case(1, "gpu-rccl", FIXTURE_CASES[:3], 29634, body=run_fixture_case)
 
 
+@pytest.mark.parametrize("staged", [False, True])
+@pytest.mark.parametrize("world,port", [(2, 29671), (4, 29672), (8, 29673)])
+def test_reference_fixtures_over_rccl_multirank(world, port, staged, monkeypatch):
+    """The production RCCL grid at world 2 / 4 / 8 (1x1x2, 2x2, 2x2x2) with every rank on cuda:0: libcbgpu's
+    own communicators (ncclCommInitRank + ncclCommSplit), asynchronous ncclBroadcast of the stage pieces on
+    the communication stream, grouped ncclSend/ncclRecv fiber all-to-all-v, ncclAllGather of the sizes.
+    Each rank is its own RCCL "node" (NCCL_HOSTID), so RCCL's socket transport carries the bytes.  Panel
+    schedule (default) and the staged double-buffered schedule; the reference fixtures (bcsstk01^2 + MATLAB
+    C.mtx, G500 s10 under six semirings) must come out on every rank's piece, and RCCL must report the
+    grid's group sizes."""
+    from dist_support import run_fixture_case
+    if staged:
+        monkeypatch.setenv("CBG_GRID_STAGED", "1")
+    spawn_case(world, "gpu-rccl-net", FIXTURE_CASES, port + (10 if staged else 0), body=run_fixture_case)
+
+
 @pytest.mark.parametrize("world,port", [(2, 29641), (4, 29642), (8, 29643)])
 def test_rmat_pieces_built_per_rank_gloo_gpu(world, port):
     """Each rank's A/B pieces built on the device by cbg_rmat_block equal the reference-generated G500

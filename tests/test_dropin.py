@@ -50,3 +50,47 @@ def test_dropin_distributed_drivers_4_ranks_on_gpu():
         pytest.skip("dropin_test or MPICH's mpirun not available")
     r = subprocess.run([mpirun, "-np", "4", BIN], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and r.stdout.count("DROPIN OK") == 4, r.stdout + r.stderr
+
+
+def _write_mtx(path, nrow, ncol, cp, ir, val):
+    """MatrixMarket coordinate real general, 1-based (what ParallelReadMM reads, onebased = true)."""
+    import numpy as np
+    cols = np.repeat(np.arange(ncol), np.diff(cp))
+    with open(path, "w") as f:
+        f.write("%%MatrixMarket matrix coordinate real general\n")
+        f.write(f"{nrow} {ncol} {len(ir)}\n")
+        for r, c, v in zip(ir, cols, val):
+            f.write(f"{int(r) + 1} {int(c) + 1} {float(v)!r}\n")
+
+
+def _fixture_mtx(tmp_path):
+    """bcsstk01 (A) and MATLAB's bcsstk01^2 (3DSpGEMM/matlab/C.mtx, held in bcsstk01.npz), and the reference's
+    Graph500 s10 matrix (integer multiplicities), written from the committed fixtures."""
+    import numpy as np
+    z = np.load(os.path.join(HERE, "golden", "bcsstk01.npz"))
+    n = int(z["A_shape"][0])
+    fa, fc, fg = (str(tmp_path / x) for x in ("A.mtx", "C.mtx", "G.mtx"))
+    _write_mtx(fa, n, n, z["A_cp"], z["A_ir"], z["A_val"])
+    _write_mtx(fc, n, n, z["M_matlab_cp"], z["M_matlab_ir"], z["M_matlab_val"])
+    g = np.load(os.path.join(HERE, "golden", "g500_s10.npz"))
+    m = int(g["A_shape"][0])
+    _write_mtx(fg, m, m, g["A_cp"], g["A_ir"], g["A_val"])
+    return fa, fc, fg
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("q,L", [(1, 2), (2, 1), (1, 4), (2, 2)])
+def test_dropin_3dspgemm_and_summa3d_on_gpu(q, L, tmp_path):
+    """gpu::multiply / gpu::SUMMALayer (3DSpGEMM/Multiplier.h:10-61, SUMMALayer.h:24-97) on a CCGrid of
+    q x q x L MPI ranks sharing cuda:0, set up as test_mpipspgemm.cpp:101-153 does (ReadMat + SplitMat of
+    bcsstk01), against the reference's multiply / SUMMALayer on the same split pieces and against MATLAB's
+    C.mtx; and gpu::Mult_AnXBn_SUMMA3D against the reference's Mult_AnXBn_SUMMA3D on SpParMat3D operands
+    with L layers (bcsstk01 within 1e-12 of sum|a*b|, Graph500 s10 bit-exact), every rank's piece."""
+    mpirun = "/opt/conda/bin/mpirun"
+    if not os.path.exists(BIN) or not os.path.exists(mpirun):
+        pytest.skip("dropin_test or MPICH's mpirun not available")
+    fa, fc, fg = _fixture_mtx(tmp_path)
+    world = q * q * L
+    r = subprocess.run([mpirun, "-np", str(world), BIN, "--3d", str(q), str(L), fa, fc, fg], capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0 and r.stdout.count("DROPIN3D OK") == world, r.stdout + r.stderr
