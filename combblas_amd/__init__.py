@@ -26,7 +26,7 @@ G500_SEED = 0xDECAFBAD   # the reference's default Graph500 user seed (RefGen21:
 __all__ = ["Context", "SpDCCols", "SpTuples", "PlusTimesSRing", "MinPlusSRing", "Select2ndSRing",
            "SelectMaxSRing", "SelectMaxBoolSRing", "BoolCopy1stSRing", "BoolCopy2ndSRing",
            "LocalSpGEMMHash", "LocalHybridSpGEMM", "LocalSpGEMM", "EstimateLocalFLOP", "MultiwayMerge",
-           "CbgError", "generate_rmat_host", "default_context", "G500_SEED", "RestrictionOp",
+           "CbgError", "generate_rmat_host", "default_context", "G500_SEED", "RestrictionOp", "MIS2Restriction", "Transpose",
            "GalerkinRAP"]
 
 _NP = {_abi.BOOL: np.uint8, _abi.I32: np.int32, _abi.I64: np.int64, _abi.F32: np.float32, _abi.F64: np.float64}
@@ -319,10 +319,25 @@ def MultiwayMerge(SR, lists, mdim=0, ndim=0, delarrs=False):
     return C
 
 
-def RestrictionOp(G, seed=1):
-    """MIS-2 aggregation restriction of the graph of G (3DSpGEMM/RestrictionOp.h:116-290) on G's GPU:
-    (R, RT) as device matrices, R (n x nagg) with R(i, agg(i)) = 1, RT = R^T.  G must be square and
-    symmetric (RestrictionOp symmetrises and drops loops first; self loops are ignored here)."""
+def RestrictionOp(A, mt_seed=1, perm_seed=1383098845):
+    """The reference's Galerkin restriction operator (3DSpGEMM/RestrictionOp.h:196-291) of the square matrix A
+    on A's GPU, entry for entry: (R, RT) as device matrices, R (n x nagg) with R(i, agg(i)) = 1, RT = R^T.
+    MIS2 on pattern(A) + pattern(A)^T without loops (:116-193, the MTRand stream of mt_seed), parents and
+    Select2ndRandSR aggregation, aggregate columns permuted as RandPerm does (std::shuffle with
+    std::default_random_engine(perm_seed)).  The defaults are the reference's DETERMINISTIC seeds."""
+    ctx = A._ctx
+    R, RT, nagg = _abi.CscResult(), _abi.CscResult(), ctypes.c_int64(0)
+    _abi.check(ctx._lib.cbg_restriction_op(ctx._ptr, ctypes.byref(A._view()), int(mt_seed) & 0xFFFFFFFF,
+                                           int(perm_seed) & 0xFFFFFFFF, ctypes.byref(R), ctypes.byref(RT),
+                                           ctypes.byref(nagg)), "cbg_restriction_op")
+    return SpDCCols._from_result(ctx, R), SpDCCols._from_result(ctx, RT)
+
+
+def MIS2Restriction(G, seed=1):
+    """A faster MIS-2 aggregation restriction of the graph of G (not the reference's R): Luby rounds with
+    seeded distinct 64-bit priorities (no sequential random stream), every vertex joins the highest-priority
+    set vertex within distance 1, else 2.  (R, RT) as device matrices.  G must be square and symmetric;
+    self loops are ignored."""
     ctx = G._ctx
     R, RT, nagg = _abi.CscResult(), _abi.CscResult(), ctypes.c_int64(0)
     _abi.check(ctx._lib.cbg_mis2_restriction(ctx._ptr, ctypes.byref(G._view()), int(seed), ctypes.byref(R),
@@ -330,19 +345,35 @@ def RestrictionOp(G, seed=1):
     return SpDCCols._from_result(ctx, R), SpDCCols._from_result(ctx, RT)
 
 
-def GalerkinRAP(A, R, RT=None):
-    """C = R^T A R (RestrictionOp.cpp:188-196).  For an aggregation R (one nonzero per row) whose
-    aggregates each gather at most 512 entries of A: one fused device pass (cbg_galerkin_rap,
-    C.multiplies = nnz(A)).  Otherwise, given RT = R^T, the reference's two products R^T A and
-    (R^T A) R; without RT such an R raises CbgError(CBG_EUNSUP)."""
+def Transpose(A):
+    """A^T as a new device matrix (SpDCCols::Transpose, SpDCCols.cpp:845); f64 values or a pattern."""
     ctx = A._ctx
     res = _abi.CscResult()
-    st = ctx._lib.cbg_galerkin_rap(ctx._ptr, ctypes.byref(A._view()), ctypes.byref(R._view()), ctypes.byref(res))
-    if st == _abi.EUNSUP and RT is not None:
+    _abi.check(ctx._lib.cbg_transpose(ctx._ptr, ctypes.byref(A._view()), ctypes.byref(res)), "cbg_transpose")
+    return SpDCCols._from_result(ctx, res)
+
+
+def GalerkinRAP(A, R, RT=None, fused=True):
+    """C = R^T A R (RestrictionOp.cpp:188-196).  For an aggregation R (one nonzero per row) whose
+    aggregates each gather at most 512 entries of A: one fused device pass (cbg_galerkin_rap,
+    C.multiplies = nnz(A)).  Otherwise (or with fused=False) the reference's two products R^T A and
+    (R^T A) R, with RT = R^T built on the device when not given."""
+    ctx = A._ctx
+    res = _abi.CscResult()
+    st = _abi.EUNSUP
+    if fused:
+        st = ctx._lib.cbg_galerkin_rap(ctx._ptr, ctypes.byref(A._view()), ctypes.byref(R._view()),
+                                       ctypes.byref(res))
+    if st == _abi.EUNSUP:
         PT = PlusTimesSRing("f64")
+        own = RT is None
+        if own:
+            RT = Transpose(R)
         RA = LocalSpGEMMHash(PT, RT, A)
         C = LocalSpGEMMHash(PT, RA, R)
         RA.free()
+        if own:
+            RT.free()
         return C
     _abi.check(st, "cbg_galerkin_rap")
     return SpDCCols._from_result(ctx, res)

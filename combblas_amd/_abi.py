@@ -104,6 +104,10 @@ SIGNATURES = {
     "cbg_mis2_restriction": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(DcscView), ctypes.c_uint64,
                                             ctypes.POINTER(CscResult), ctypes.POINTER(CscResult),
                                             ctypes.POINTER(ctypes.c_int64)]),
+    "cbg_restriction_op": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(DcscView), ctypes.c_uint32, ctypes.c_uint32,
+                                          ctypes.POINTER(CscResult), ctypes.POINTER(CscResult),
+                                          ctypes.POINTER(ctypes.c_int64)]),
+    "cbg_transpose": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(DcscView), ctypes.POINTER(CscResult)]),
     "cbg_galerkin_rap": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(DcscView), ctypes.POINTER(DcscView),
                                         ctypes.POINTER(CscResult)]),
     "cbg_rmat_host": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_uint64, ctypes.POINTER(HostCsc)]),
@@ -131,6 +135,8 @@ SIGNATURES = {
     "cbg_summa_layer": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(DcscView), ctypes.POINTER(DcscView), ctypes.c_int,
                                        ctypes.c_int, ctypes.c_uint32, ctypes.POINTER(CscResult),
                                        ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(GridStats)]),
+    "cbg_summa_estimate": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(DcscView), ctypes.POINTER(DcscView),
+                                          ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]),
     "cbg_reduce_all": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(CscResult), ctypes.c_int32, ctypes.c_int,
                                       ctypes.c_int, ctypes.POINTER(CscResult), ctypes.POINTER(GridStats)]),
 }

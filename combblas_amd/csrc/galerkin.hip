@@ -20,6 +20,9 @@
 //     (k_rap_agg: a count pass and a fill pass; one read of nnz(A) each instead of two SpGEMMs with
 //     an R^T A intermediate; deterministic summation order).
 #include "spgemm_host.hpp"
+#include <algorithm>
+#include <numeric>
+#include <random>
 
 namespace {
 
@@ -237,6 +240,194 @@ __global__ void k_rap_compact(int64_t nagg, const int64_t* __restrict__ rcp, con
   }
 }
 
+// ---------------------------------------------------------------- the reference's RestrictionOp
+// MTRand (psort-1.0/include/psort/MersenneTwister.h:137-147, 179-196, 283-314) = MT19937 with init_genrand
+// seeding.  The state (624 words + read index) lives in HBM between launches; one 256-lane workgroup
+// draws the next *count values of the stream: each reload is the three data-parallel spans of the twist
+// ([0,227) reads old words, [227,454) and [454,623) read words the previous span rewrote) staged in LDS.
+constexpr int kMtN = 624;
+
+__global__ void k_mt_seed(uint32_t seed, uint32_t* __restrict__ st) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    uint32_t x = seed;
+    st[0] = x;
+    for (uint32_t i = 1; i < kMtN; ++i) {
+      x = 1812433253u * (x ^ (x >> 30)) + i;
+      st[i] = x;
+    }
+    st[kMtN] = kMtN;   // read index: the first draw reloads
+  }
+}
+
+__device__ __forceinline__ uint32_t mt_twist(uint32_t m, uint32_t s0, uint32_t s1) {
+  return m ^ (((s0 & 0x80000000u) | (s1 & 0x7fffffffu)) >> 1) ^ ((s1 & 1u) ? 0x9908b0dfu : 0u);
+}
+__device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
+  y ^= y >> 11;
+  y ^= (y << 7) & 0x9d2c5680u;
+  y ^= (y << 15) & 0xefc60000u;
+  return y ^ (y >> 18);
+}
+
+__global__ void __launch_bounds__(256) k_mt_draw(uint32_t* __restrict__ st, const int64_t* __restrict__ count,
+                                                 uint32_t* __restrict__ out) {
+  __shared__ uint32_t s[kMtN];
+  const int t = threadIdx.x;
+  for (int i = t; i < kMtN; i += 256) s[i] = st[i];
+  uint32_t idx = st[kMtN];
+  const int64_t n = *count;
+  __syncthreads();
+  for (int64_t done = 0; done < n;) {
+    if (idx == kMtN) {
+      uint32_t v = 0;
+      if (t < 227) v = mt_twist(s[t + 397], s[t], s[t + 1]);
+      __syncthreads();
+      if (t < 227) s[t] = v;
+      __syncthreads();
+      if (t < 227) v = mt_twist(s[t], s[t + 227], s[t + 228]);
+      __syncthreads();
+      if (t < 227) s[t + 227] = v;
+      __syncthreads();
+      if (t < 169) v = mt_twist(s[t + 227], s[t + 454], s[t + 455]);
+      __syncthreads();
+      if (t < 169) s[t + 454] = v;
+      __syncthreads();
+      if (t == 0) s[623] = mt_twist(s[396], s[623], s[0]);
+      __syncthreads();
+      idx = 0;
+    }
+    const int64_t take = min<int64_t>(kMtN - idx, n - done);
+    for (int64_t k = t; k < take; k += 256) out[done + k] = mt_temper(s[idx + k]);
+    idx += (uint32_t)take;
+    done += take;
+  }
+  __syncthreads();
+  for (int i = t; i < kMtN; i += 256) st[i] = s[i];
+  if (t == 0) st[kMtN] = idx;
+}
+
+// B = pattern(A) + pattern(A)^T without the diagonal (RestrictionOp.h:201-208): raw column counts ...
+__global__ void k_sym_count(int64_t n, const int64_t* __restrict__ cp, const int32_t* __restrict__ ir,
+                            unsigned long long* __restrict__ cnt) {
+  for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < n; j += (int64_t)gridDim.x * blockDim.x) {
+    unsigned long long own = 0;
+    for (int64_t p = cp[j]; p < cp[j + 1]; ++p) {
+      const int32_t i = ir[p];
+      if (i == j) continue;
+      ++own;
+      atomicAdd(&cnt[i], 1ull);
+    }
+    if (own) atomicAdd(&cnt[j], own);
+  }
+}
+// ... and the raw entries (column j gets row i, column i gets row j); rows are sorted and deduplicated after
+__global__ void k_sym_fill(int64_t n, const int64_t* __restrict__ cp, const int32_t* __restrict__ ir,
+                           unsigned long long* __restrict__ cursor, int32_t* __restrict__ rows) {
+  for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < n; j += (int64_t)gridDim.x * blockDim.x)
+    for (int64_t p = cp[j]; p < cp[j + 1]; ++p) {
+      const int32_t i = ir[p];
+      if (i == j) continue;
+      rows[atomicAdd(&cursor[j], 1ull)] = i;
+      rows[atomicAdd(&cursor[i], 1ull)] = (int32_t)j;
+    }
+}
+
+constexpr uint64_t kNoVal = ~0ull;
+
+// flag[v] = cand[v] (int64, for the candidate ranks)
+__global__ void k_flag64(int64_t n, const uint8_t* __restrict__ f, int64_t* __restrict__ out) {
+  for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < n; v += (int64_t)gridDim.x * blockDim.x)
+    out[v] = f[v];
+}
+// r[v] = this round's draw of candidate v (the pos[v]-th value of the round), else none
+__global__ void k_cand_vals(int64_t n, const uint8_t* __restrict__ cand, const int64_t* __restrict__ pos,
+                            const uint32_t* __restrict__ draw, uint64_t* __restrict__ r) {
+  for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < n; v += (int64_t)gridDim.x * blockDim.x)
+    r[v] = cand[v] ? (uint64_t)draw[pos[v]] : kNoVal;
+}
+// out[v] = min over neighbours u of in[u] (SpMV with Select2ndMinSR, RestrictionOp.h:146-147)
+__global__ void k_nbr_min(int64_t n, const int64_t* __restrict__ cp, const int32_t* __restrict__ ir,
+                          const uint64_t* __restrict__ in, uint64_t* __restrict__ out) {
+  for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < n; v += (int64_t)gridDim.x * blockDim.x) {
+    uint64_t m = kNoVal;
+    for (int64_t p = cp[v]; p < cp[v + 1]; ++p) m = min(m, in[ir[p]]);
+    out[v] = m;
+  }
+}
+// new members: candidates whose draw is <= the 1- and 2-hop minimum (RestrictionOp.h:149-161)
+__global__ void k_mis_new(int64_t n, const uint8_t* __restrict__ cand, const uint64_t* __restrict__ r,
+                          const uint64_t* __restrict__ m1, const uint64_t* __restrict__ m2, uint8_t* __restrict__ fresh) {
+  for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < n; v += (int64_t)gridDim.x * blockDim.x)
+    fresh[v] = cand[v] && r[v] <= min(m1[v], m2[v]);
+}
+// out[v] = 1 iff a neighbour u has in[u] (SpMV of the new members and of their neighbours, :170-171)
+__global__ void k_nbr_any(int64_t n, const int64_t* __restrict__ cp, const int32_t* __restrict__ ir,
+                          const uint8_t* __restrict__ in, uint8_t* __restrict__ out) {
+  for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < n; v += (int64_t)gridDim.x * blockDim.x) {
+    uint8_t f = 0;
+    for (int64_t p = cp[v]; p < cp[v + 1] && !f; ++p) f = in[ir[p]];
+    out[v] = f;
+  }
+}
+// members leave the candidates with their 1- and 2-hop neighbours and join the set (:164-189)
+__global__ void k_mis_round(int64_t n, const uint8_t* __restrict__ fresh, const uint8_t* __restrict__ nb1,
+                            const uint8_t* __restrict__ nb2, uint8_t* __restrict__ cand, uint8_t* __restrict__ mis,
+                            int64_t* __restrict__ left) {
+  int64_t c = 0;
+  for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < n; v += (int64_t)gridDim.x * blockDim.x) {
+    const uint8_t f = fresh[v];
+    const uint8_t k = cand[v] && !f && !nb1[v] && !nb2[v];
+    cand[v] = k;
+    if (f) mis[v] = 1;
+    c += k;
+  }
+  c = wave_sum64(c);
+  if (lane_id() == 0 && c) atomicAdd((unsigned long long*)left, (unsigned long long)c);
+}
+// parent[v] = v for set members, else the (unique) set member among the neighbours (MIS2verifySR and the union
+// with mis2, :216-222), else -1; flag = has a parent
+__global__ void k_mis_parent(int64_t n, const int64_t* __restrict__ cp, const int32_t* __restrict__ ir,
+                             const uint8_t* __restrict__ mis, int64_t* __restrict__ parent, int64_t* __restrict__ has,
+                             int64_t* __restrict__ misflag) {
+  for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < n; v += (int64_t)gridDim.x * blockDim.x) {
+    int64_t p = -1;
+    if (mis[v]) {
+      p = v;
+    } else {
+      for (int64_t q = cp[v]; q < cp[v + 1]; ++q)
+        if (mis[ir[q]]) { p = p < 0 ? ir[q] : min<int64_t>(p, ir[q]); }
+    }
+    parent[v] = p;
+    has[v] = p >= 0;
+    misflag[v] = mis[v];
+  }
+}
+// key[v] = (draw, larger vertex first) of parented vertices (mis2neigh_p, :225-229)
+__global__ void k_parent_keys(int64_t n, const int64_t* __restrict__ has, const int64_t* __restrict__ pos,
+                              const uint32_t* __restrict__ draw, uint64_t* __restrict__ key) {
+  for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < n; v += (int64_t)gridDim.x * blockDim.x)
+    key[v] = has[v] ? ((uint64_t)draw[pos[v]] << 32 | (uint64_t)(0xffffffffu - (uint32_t)v)) : kNoVal;
+}
+// aggregate column of v: its parent, else the parent of the neighbour with the smallest draw (Select2ndRandSR,
+// :63-84, 233-247); the column is the parent's rank among the set members, permuted (RandPerm, :268-275)
+__global__ void k_restrict_cols(int64_t n, const int64_t* __restrict__ parent, const uint64_t* __restrict__ best,
+                                const int64_t* __restrict__ misrank, const int32_t* __restrict__ inv,
+                                int32_t* __restrict__ agg, unsigned long long* __restrict__ colcnt,
+                                int64_t* __restrict__ bad) {
+  for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < n; v += (int64_t)gridDim.x * blockDim.x) {
+    int64_t p = parent[v];
+    if (p < 0 && best[v] != kNoVal) p = parent[0xffffffffu - (uint32_t)(best[v] & 0xffffffffu)];
+    if (p < 0) {
+      agg[v] = -1;
+      atomicAdd((unsigned long long*)bad, 1ull);
+      continue;
+    }
+    const int32_t a = inv[misrank[p]];
+    agg[v] = a;
+    atomicAdd(&colcnt[a], 1ull);
+  }
+}
+
 template <class Buf>   // DevBuf (persistent workspace) or PoolBuf
 cbg_status scan_counts_async(hipStream_t st, int64_t n, const int64_t* cnt, int64_t* out, int64_t* total_dev,
                              Buf* tiles) {
@@ -346,6 +537,201 @@ extern "C" cbg_status cbg_mis2_restriction(cbg_ctx* ctx, const cbg_dcsc_view* Gv
   }
   HIPCHK(hipStreamSynchronize(st));
   if (nagg_out) *nagg_out = nagg;
+  return CBG_OK;
+}
+
+// The reference's RestrictionOp (3DSpGEMM/RestrictionOp.h:196-291) at one rank: MIS2 (:116-193) with the
+// MTRand stream seeded by mt_seed, parents, Select2ndRandSR aggregation and RandPerm of the aggregate columns
+// (FullyDistVec.cpp:783-900: std::shuffle of 0..nagg-1 with std::default_random_engine(perm_seed), the one
+// host step -- the reference's RandPerm is host code too, O(nagg)).  The reference's DETERMINISTIC seeds are
+// mt_seed = 1, perm_seed = 1383098845.  Every vertex-parallel step is one thread per vertex over B's CSC;
+// the draws of a round are ranked by a scan of the candidate flags, so the round needs no host copy except
+// the count of remaining candidates.
+extern "C" cbg_status cbg_restriction_op(cbg_ctx* ctx, const cbg_dcsc_view* Av, uint32_t mt_seed, uint32_t perm_seed,
+                                         cbg_csc_result* R, cbg_csc_result* RT, int64_t* nagg_out) {
+  if (!ctx || !Av || !R) return CBG_EINVAL;
+  if (Av->nrow != Av->ncol) return CBG_EDIM;
+  HIPCHK(hipSetDevice(ctx->device));
+  hipStream_t st = ctx->stream;
+  DevBuf sb[5];
+  DevCsc<double> A;
+  CBGCHK(stage<double>(ctx, Av, sb, &A));
+  const int64_t n = A.ncol;
+  if (n >= INT32_MAX) return CBG_EUNSUP;
+  const int g = (int)grid_for(std::max<int64_t>(n, 1), 256, kMaxGrid * 4);
+  PoolBuf cnt, tiles, rows, sc, mt;
+  for (PoolBuf* b : {&cnt, &tiles, &rows, &sc, &mt}) b->pool = ctx->pool;
+  HIPCHK(sc.reserve(64));
+  int64_t* scal = sc.as<int64_t>();   // [0] raw B entries [1] draws this round [2] left [3] parented [4] nagg [5] bad
+  HIPCHK(hipMemsetAsync(scal, 0, 64, st));
+  // B: symmetric, loop-free pattern of A, rows sorted and unique per column
+  HIPCHK(cnt.reserve(8 * (2 * n + 2)));
+  unsigned long long* bcnt = cnt.as<unsigned long long>();
+  unsigned long long* cursor = bcnt + n + 1;
+  HIPCHK(hipMemsetAsync(bcnt, 0, 8 * (n + 1), st));
+  PoolBuf rawcp;
+  rawcp.pool = ctx->pool;
+  HIPCHK(rawcp.reserve(8 * (n + 1)));
+  if (n) k_sym_count<<<g, 256, 0, st>>>(n, A.cp, A.ir, bcnt);
+  HIPCHK(hipGetLastError());
+  CBGCHK(scan_counts_async(st, n, (const int64_t*)bcnt, rawcp.as<int64_t>(), scal, &tiles));
+  int64_t nraw = 0;
+  HIPCHK(hipMemcpyAsync(&nraw, scal, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  HIPCHK(rows.reserve(4 * (nraw + 1)));
+  if (n) HIPCHK(hipMemcpyAsync(cursor, rawcp.p, 8 * n, hipMemcpyDeviceToDevice, st));
+  if (n) k_sym_fill<<<g, 256, 0, st>>>(n, A.cp, A.ir, cursor, rows.as<int32_t>());
+  HIPCHK(hipGetLastError());
+  cbg_csc_result Bres;
+  CBGCHK(dedup_columns(ctx, n, n, nraw, rawcp.as<int64_t>(), rows.as<int32_t>(), nullptr, &Bres));
+  std::unique_ptr<Owner> bown((Owner*)Bres._owner);
+  const int64_t* bcp = Bres.colptr;
+  const int32_t* bir = Bres.row;
+  // MIS2
+  PoolBuf cand, mis, fresh, nb1, nb2, flag, pos, draw, r, m1, m2;
+  for (PoolBuf* b : {&cand, &mis, &fresh, &nb1, &nb2, &flag, &pos, &draw, &r, &m1, &m2}) b->pool = ctx->pool;
+  for (PoolBuf* b : {&cand, &mis, &fresh, &nb1, &nb2}) HIPCHK(b->reserve(n + 1));
+  for (PoolBuf* b : {&flag, &pos, &r, &m1, &m2}) HIPCHK(b->reserve(8 * (n + 1)));
+  HIPCHK(draw.reserve(4 * (n + 1)));
+  HIPCHK(mt.reserve(4 * (kMtN + 1)));
+  HIPCHK(hipMemsetAsync(cand.p, 1, n + 1, st));
+  HIPCHK(hipMemsetAsync(mis.p, 0, n + 1, st));
+  k_mt_seed<<<1, 64, 0, st>>>(mt_seed, mt.as<uint32_t>());
+  HIPCHK(hipGetLastError());
+  int64_t left = n;
+  for (int round = 0; left > 0; ++round) {
+    if (round > 4096) return CBG_EDEVICE;   // every round admits the smallest draw: cannot happen
+    k_flag64<<<g, 256, 0, st>>>(n, cand.as<uint8_t>(), flag.as<int64_t>());
+    CBGCHK(scan_counts_async(st, n, flag.as<int64_t>(), pos.as<int64_t>(), scal + 1, &tiles));
+    k_mt_draw<<<1, 256, 0, st>>>(mt.as<uint32_t>(), scal + 1, draw.as<uint32_t>());
+    k_cand_vals<<<g, 256, 0, st>>>(n, cand.as<uint8_t>(), pos.as<int64_t>(), draw.as<uint32_t>(), r.as<uint64_t>());
+    k_nbr_min<<<g, 256, 0, st>>>(n, bcp, bir, r.as<uint64_t>(), m1.as<uint64_t>());
+    k_nbr_min<<<g, 256, 0, st>>>(n, bcp, bir, m1.as<uint64_t>(), m2.as<uint64_t>());
+    k_mis_new<<<g, 256, 0, st>>>(n, cand.as<uint8_t>(), r.as<uint64_t>(), m1.as<uint64_t>(), m2.as<uint64_t>(),
+                                 fresh.as<uint8_t>());
+    k_nbr_any<<<g, 256, 0, st>>>(n, bcp, bir, fresh.as<uint8_t>(), nb1.as<uint8_t>());
+    k_nbr_any<<<g, 256, 0, st>>>(n, bcp, bir, nb1.as<uint8_t>(), nb2.as<uint8_t>());
+    HIPCHK(hipMemsetAsync(scal + 2, 0, 8, st));
+    k_mis_round<<<g, 256, 0, st>>>(n, fresh.as<uint8_t>(), nb1.as<uint8_t>(), nb2.as<uint8_t>(), cand.as<uint8_t>(),
+                                   mis.as<uint8_t>(), scal + 2);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(&left, scal + 2, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+  }
+  // parents, their draws, the aggregation of the unparented vertices, the MIS ranks (m1 = parent,
+  // flag = has-parent, r = MIS flags as int64 -> pos/misrank)
+  PoolBuf misrank;
+  misrank.pool = ctx->pool;
+  HIPCHK(misrank.reserve(8 * (n + 1)));
+  k_mis_parent<<<g, 256, 0, st>>>(n, bcp, bir, mis.as<uint8_t>(), m1.as<int64_t>(), flag.as<int64_t>(),
+                                  r.as<int64_t>());
+  HIPCHK(hipGetLastError());
+  CBGCHK(scan_counts_async(st, n, flag.as<int64_t>(), pos.as<int64_t>(), scal + 3, &tiles));
+  CBGCHK(scan_counts_async(st, n, r.as<int64_t>(), misrank.as<int64_t>(), scal + 4, &tiles));
+  k_mt_draw<<<1, 256, 0, st>>>(mt.as<uint32_t>(), scal + 3, draw.as<uint32_t>());
+  k_parent_keys<<<g, 256, 0, st>>>(n, flag.as<int64_t>(), pos.as<int64_t>(), draw.as<uint32_t>(), m2.as<uint64_t>());
+  k_nbr_min<<<g, 256, 0, st>>>(n, bcp, bir, m2.as<uint64_t>(), r.as<uint64_t>());
+  HIPCHK(hipGetLastError());
+  int64_t nagg = 0;
+  HIPCHK(hipMemcpyAsync(&nagg, scal + 4, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  // RandPerm of the aggregate columns: new column j is old column perm[j]; inv[perm[j]] = j
+  std::vector<int64_t> perm((size_t)nagg);
+  std::iota(perm.begin(), perm.end(), 0);
+  std::default_random_engine gen(perm_seed);
+  std::shuffle(perm.begin(), perm.end(), gen);
+  std::vector<int32_t> inv((size_t)nagg + 1);
+  for (int64_t j = 0; j < nagg; ++j) inv[(size_t)perm[(size_t)j]] = (int32_t)j;
+  PoolBuf dinv, agg, ccnt, rcp, members;
+  for (PoolBuf* b : {&dinv, &agg, &ccnt, &rcp, &members}) b->pool = ctx->pool;
+  HIPCHK(dinv.reserve(4 * (nagg + 1)));
+  HIPCHK(agg.reserve(4 * (n + 1)));
+  HIPCHK(ccnt.reserve(8 * (2 * nagg + 2)));
+  HIPCHK(rcp.reserve(8 * (nagg + 1)));
+  HIPCHK(members.reserve(4 * (n + 1)));
+  HIPCHK(hipMemcpyAsync(dinv.p, inv.data(), 4 * (nagg + 1), hipMemcpyHostToDevice, st));
+  unsigned long long* colcnt = ccnt.as<unsigned long long>();
+  unsigned long long* ccur = colcnt + nagg + 1;
+  HIPCHK(hipMemsetAsync(colcnt, 0, 8 * (nagg + 1), st));
+  k_restrict_cols<<<g, 256, 0, st>>>(n, m1.as<int64_t>(), r.as<uint64_t>(), misrank.as<int64_t>(), dinv.as<int32_t>(),
+                                     agg.as<int32_t>(), colcnt, scal + 5);
+  HIPCHK(hipGetLastError());
+  CBGCHK(scan_counts_async(st, nagg, (const int64_t*)colcnt, rcp.as<int64_t>(), scal + 6, &tiles));
+  if (nagg) HIPCHK(hipMemcpyAsync(ccur, rcp.p, 8 * nagg, hipMemcpyDeviceToDevice, st));
+  k_scatter_members<<<g, 256, 0, st>>>(n, agg.as<int32_t>(), ccur, members.as<int32_t>());
+  HIPCHK(hipGetLastError());
+  int64_t bad = 0;
+  HIPCHK(hipMemcpyAsync(&bad, scal + 5, 8, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));   // inv (host) is read; bad is known
+  if (bad) return CBG_EDEVICE;        // a vertex beyond distance 2 of the set: not a maximal MIS-2
+  CBGCHK(dedup_columns(ctx, n, nagg, n, rcp.as<int64_t>(), members.as<int32_t>(), nullptr, R));
+  R->multiplies = 0;
+  if (RT) {   // R^T (nagg x n): column v holds the single row agg(v)
+    std::unique_ptr<Owner> own(new Owner(ctx->pool));
+    HIPCHK(own->cp.reserve(8 * (n + 1)));
+    HIPCHK(own->ir.reserve(4 * (n + 1)));
+    HIPCHK(own->val.reserve(8 * (n + 1)));
+    k_rt<<<(int)grid_for(n + 1, 256, kMaxGrid * 4), 256, 0, st>>>(n, agg.as<int32_t>(), own->cp.as<int64_t>(),
+                                                                  own->ir.as<int32_t>(), own->val.as<double>());
+    HIPCHK(hipGetLastError());
+    memset(RT, 0, sizeof(*RT));
+    RT->nrow = nagg; RT->ncol = n; RT->nnz = n;
+    RT->colptr = own->cp.as<int64_t>(); RT->row = own->ir.as<int32_t>(); RT->val = own->val.p;
+    RT->val_type = CBG_F64;
+    RT->_owner = own.release();
+  }
+  HIPCHK(hipStreamSynchronize(st));
+  if (nagg_out) *nagg_out = nagg;
+  return CBG_OK;
+}
+
+// C = A^T (SpDCCols::Transpose, SpDCCols.cpp:845): per-row counts, scatter of (column, value) into the rows'
+// columns, then the duplicate-free row sort of dedup_columns.  PlusTimes<double> values (or a pattern).
+__global__ void k_row_counts(int64_t nnz, const int32_t* __restrict__ ir, unsigned long long* __restrict__ cnt) {
+  for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < nnz; p += (int64_t)gridDim.x * blockDim.x)
+    atomicAdd(&cnt[ir[p]], 1ull);
+}
+__global__ void k_transpose_fill(int64_t ncol, const int64_t* __restrict__ cp, const int32_t* __restrict__ ir,
+                                 const double* __restrict__ val, unsigned long long* __restrict__ cursor,
+                                 int32_t* __restrict__ orow, double* __restrict__ oval) {
+  for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < ncol; j += (int64_t)gridDim.x * blockDim.x)
+    for (int64_t p = cp[j]; p < cp[j + 1]; ++p) {
+      const unsigned long long o = atomicAdd(&cursor[ir[p]], 1ull);
+      orow[o] = (int32_t)j;
+      if (oval) oval[o] = val ? val[p] : 1.0;
+    }
+}
+
+extern "C" cbg_status cbg_transpose(cbg_ctx* ctx, const cbg_dcsc_view* Av, cbg_csc_result* C) {
+  if (!ctx || !Av || !C) return CBG_EINVAL;
+  if (Av->val && Av->val_type != CBG_F64) return CBG_EUNSUP;
+  HIPCHK(hipSetDevice(ctx->device));
+  hipStream_t st = ctx->stream;
+  DevBuf sb[5];
+  DevCsc<double> A;
+  CBGCHK(stage<double>(ctx, Av, sb, &A));
+  const int64_t m = A.nrow, n = A.ncol, nnz = A.nnz;
+  if (n >= INT32_MAX) return CBG_EUNSUP;
+  PoolBuf cnt, ocp, rows, vals, tiles, sc;
+  for (PoolBuf* b : {&cnt, &ocp, &rows, &vals, &tiles, &sc}) b->pool = ctx->pool;
+  HIPCHK(cnt.reserve(8 * (2 * m + 2)));
+  HIPCHK(ocp.reserve(8 * (m + 1)));
+  HIPCHK(rows.reserve(4 * (nnz + 1)));
+  HIPCHK(vals.reserve(8 * (nnz + 1)));
+  HIPCHK(sc.reserve(16));
+  unsigned long long* c = cnt.as<unsigned long long>();
+  unsigned long long* cur = c + m + 1;
+  HIPCHK(hipMemsetAsync(c, 0, 8 * (m + 1), st));
+  if (nnz) k_row_counts<<<(int)grid_for(nnz, 256, kMaxGrid * 4), 256, 0, st>>>(nnz, A.ir, c);
+  HIPCHK(hipGetLastError());
+  CBGCHK(scan_counts_async(st, m, (const int64_t*)c, ocp.as<int64_t>(), sc.as<int64_t>(), &tiles));
+  if (m) HIPCHK(hipMemcpyAsync(cur, ocp.p, 8 * m, hipMemcpyDeviceToDevice, st));
+  const bool has_val = A.val != nullptr;
+  if (n) k_transpose_fill<<<(int)grid_for(n, 256, kMaxGrid * 4), 256, 0, st>>>(n, A.cp, A.ir, A.val, cur,
+                                                                               rows.as<int32_t>(), vals.as<double>());
+  HIPCHK(hipGetLastError());
+  CBGCHK(dedup_columns(ctx, n, m, nnz, ocp.as<int64_t>(), rows.as<int32_t>(), has_val ? vals.as<double>() : nullptr, C));
+  C->multiplies = 0;
   return CBG_OK;
 }
 

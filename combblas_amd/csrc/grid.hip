@@ -466,8 +466,11 @@ cbg_status panel_rows_dt(cbg_ctx* ctx, cbg_dtype dt, const std::vector<Piece>& b
   }
 }
 
+// est != nullptr: count only (EstPerProcessNnzSUMMA) -- every stage runs the symbolic pass alone and est[0] / est[1]
+// accumulate its multiplies and nnz; no product is formed (staged schedule, parts stays empty)
 cbg_status summa_layer_impl(cbg_grid* G, const cbg_dcsc_view* Av, const cbg_dcsc_view* Bv, cbg_semiring sr,
-                            cbg_dtype dt, uint32_t flags, std::vector<Piece>* parts, cbg_grid_stats* st) {
+                            cbg_dtype dt, uint32_t flags, std::vector<Piece>* parts, cbg_grid_stats* st,
+                            int64_t* est = nullptr) {
   cbg_ctx* ctx = G->ctx;
   const size_t vs = dt_size(dt);
   Piece A0, B0;
@@ -520,12 +523,25 @@ cbg_status summa_layer_impl(cbg_grid* G, const cbg_dcsc_view* Av, const cbg_dcsc
       if (k != G->col) needA = std::max(needA, bytes_of(SA(r, k)));
       if (k != G->row) needB = std::max(needB, bytes_of(SB(r, k)));
     }
-  if ((flags & kPanels) && R == 1 && q > 1) {
+  bool panels = (flags & kPanels) && R == 1 && q > 1 && !est;
+  if (panels) {
+    // the panels hold the q received pieces of A and of B plus their concatenated copies; fall back to the
+    // staged schedule (two receive slots) when that does not fit in the free HBM with room for the product
+    int64_t need = 0;
+    for (int k = 0; k < q; ++k) need += 2 * (bytes_of(SA(0, k)) + bytes_of(SB(0, k)));
+    size_t freeb = 0, totalb = 0;
+    if (hipMemGetInfo(&freeb, &totalb) == hipSuccess && (double)need > 0.5 * (double)freeb) panels = false;
+    bool all_panels = true;   // every rank must take the same schedule (the collectives differ)
+    CBGCHK(all_ok(G, panels, &all_panels));
+    panels = all_panels;
+  }
+  if (panels) {
     // Panels: HBM holds the whole grid row of A and grid column of B (1/q of each operand), so the
     // layer's product is ONE local multiply of A(i, :) and B(:, j) -- the same bytes as the q stage
     // broadcasts, no stage products and no stage merge.  The inner blocks are concatenated in stage order,
     // so every duplicate combines in the order the staged merge would (Select2nd: first stage wins).
     std::vector<PoolBuf> bufA(q), bufB(q);
+    StreamFence fence(G->cs, ctx->stream);   // broadcasts into bufA/bufB end before the buffers return to the pool
     std::vector<Piece> pa(q), pb(q);
     for (int k = 0; k < q; ++k) {
       Piece a, b;
@@ -662,6 +678,20 @@ cbg_status summa_layer_impl(cbg_grid* G, const cbg_dcsc_view* Av, const cbg_dcsc
     const double t0 = now_ms();
     cbg_dcsc_view va = view_of(recvA[t], dt, recvA[t].val != nullptr);
     cbg_dcsc_view vb = view_of(recvB[t], dt, recvB[t].val != nullptr);
+    if (est) {   // symbolic pass only (estimateFLOP + estimateNNZ_Hash of the stage, ParFriends.h:1321-1322)
+      int64_t f = 0, z = 0;
+      CBGCHK(cbg_estimate(ctx, &va, &vb, &f, &z));
+      est[0] += f;
+      est[1] += z;
+      if (async) {
+        HIPCHK(hipEventRecord(G->ev_used[t & 1], cst));
+        G->used_rec[t & 1] = true;
+      }
+      if (st) { st->multiplies += f; st->local_ms += now_ms() - t0; ++st->stages; }
+      recvA[t] = Piece();
+      recvB[t] = Piece();
+      continue;
+    }
     cbg_csc_result C;
     int64_t m = 0;
     CBGCHK(cbg_spgemm_local(ctx, &va, &vb, sr, dt, CBG_SORTED_COLS, &C, &m));
@@ -764,6 +794,7 @@ cbg_status fiber_exchange(cbg_grid* G, const Piece& C, size_t vs, bool f64, std:
   const int64_t ir_bytes = (4 * rtot + 15) & ~15LL;
   // one owner holds the received rows+values (ir) and counts (val), pieces share it
   std::shared_ptr<Owner> rx(new Owner(ctx->pool));
+  StreamFence fence(cst, G->cs);
   HIPCHK(rx->ir.reserve(ir_bytes + vs * rtot + 16));
   HIPCHK(rx->val.reserve(8 * ((int64_t)L * myc + C.ncol + 2)));
   int64_t* rcnt = rx->val.as<int64_t>();
@@ -782,6 +813,7 @@ cbg_status fiber_exchange(cbg_grid* G, const Piece& C, size_t vs, bool f64, std:
     const int64_t stot = eb[L] - eb[0];
     PoolBuf s32, r32;
     s32.pool = r32.pool = ctx->pool;
+    StreamFence fence32(cst, G->cs);
     HIPCHK(s32.reserve(4 * (stot + 1)));
     HIPCHK(r32.reserve(4 * (rtot + 1)));
     if (stot) k_f64_to_f32<<<(int)grid_for(stot, 256, kMaxGrid), 256, 0, cst>>>(stot, (const double*)C.val + eb[0],
@@ -1021,6 +1053,19 @@ cbg_status cbg_summa_layer(cbg_grid* G, const cbg_dcsc_view* A, const cbg_dcsc_v
   *nparts = 0;
   for (auto& p : ps) CBGCHK(hand_out(G->ctx, p, dt, &parts[(*nparts)++]));   // stage products, stage order
   if (st) st->total_ms = now_ms() - t0;
+  return CBG_OK;
+}
+
+cbg_status cbg_summa_estimate(cbg_grid* G, const cbg_dcsc_view* A, const cbg_dcsc_view* B, int64_t* flops,
+                              int64_t* nnz) {
+  if (!G || !A || !B || !flops || !nnz) return CBG_EINVAL;
+  HIPCHK(hipSetDevice(G->ctx->device));
+  std::vector<Piece> ps;
+  int64_t est[2] = {0, 0};
+  const cbg_dtype dt = A->val ? A->val_type : (B->val ? B->val_type : CBG_F64);
+  CBGCHK(summa_layer_impl(G, A, B, CBG_SR_PLUS_TIMES, dt, 0u, &ps, nullptr, est));
+  *flops = est[0];
+  *nnz = est[1];
   return CBG_OK;
 }
 

@@ -112,6 +112,18 @@ struct PoolBuf {
   template <typename T> T* as() const { return (T*)p; }
 };
 
+// Synchronises the given streams when it goes out of scope.  Declared after the pool buffers that kernels or
+// RCCL calls still in flight may touch, it runs before their destructors hand them back to the pool, on the
+// error returns (HIPCHK / CBGCHK) as on the normal path.
+struct StreamFence {
+  hipStream_t a = nullptr, b = nullptr;
+  StreamFence(hipStream_t x, hipStream_t y = nullptr) : a(x), b(y) {}
+  ~StreamFence() {
+    if (a) (void)hipStreamSynchronize(a);
+    if (b) (void)hipStreamSynchronize(b);
+  }
+};
+
 struct Owner {                 // device storage behind a cbg_csc_result
   PoolBuf cp, ir, val;
   explicit Owner(const std::shared_ptr<Pool>& pl) { cp.pool = ir.pool = val.pool = pl; }

@@ -814,9 +814,11 @@ def EstPerProcessNnzSUMMA(A, B, hashEstimate=True):
     g, be = A.grid, A.backend
     if A.ncol != B.nrow:
         raise _abi.CbgError(_abi.EDIM, "EstPerProcessNnzSUMMA")
-    nnz = 0
-    for P in SUMMALayer(_PATTERN_SR(be), A, B):
-        nnz += P.nnz
+    _check_operands(A, B, "EstPerProcessNnzSUMMA")
+    if hasattr(be, "summa_estimate"):   # libcbgpu: broadcasts + symbolic pass per stage, nothing materialised
+        nnz = be.summa_estimate(g, A.block, B.block)[1]
+    else:                               # CPU test backend: the stage products' nnz
+        nnz = sum(P.nnz for P in _summa_partials(_PATTERN_SR(be), A, B, None, False))
     t = torch.tensor([nnz], dtype=torch.int64, device=be.comm_device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return int(t.item())
@@ -830,7 +832,7 @@ def _PATTERN_SR(be):
 def _phases_for_memory(A, B, phases, selectNum, recoverNum, perProcessMemory):
     """The phase count of MemEfficientSpGEMM3D's memory model (ParFriends.h:3243-3290): inputs (five copies
     of the largest layer piece), the layer's A*A estimate (two copies), the k-select buffers and the
-    post-selection output against perProcessMemory GB; the MAX over the fiber, never below `phases`."""
+    post-selection output against perProcessMemory GB; the MAX over the world, never below `phases`."""
     g, be = A.grid, A.backend
     p = g.q * g.q
     # bytes per stored nonzero in this implementation: int32 row + value (+ amortised colptr), the role of
@@ -849,7 +851,11 @@ def _phases_for_memory(A, B, phases, selectNum, recoverNum, perProcessMemory):
     remaining = perProcessMemory * 1e9 - input_mem - post_nnz * per_out * 2
     ksel_mem = ncl * k * (per_out - 8) * 3        # k-select buffers hold values only (sizeof(NUO) * 3)
     calc = int(-(-(asq_mem + ksel_mem) // remaining)) if remaining > 0 else -1
-    return max(phases, calc)
+    # B's local width differs across grid columns (the last block takes the remainder), so `calc` is
+    # MAX-reduced over the world: every rank must issue the same number of phases (the same collectives)
+    t = torch.tensor([max(phases, calc)], dtype=torch.int64, device=be.comm_device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return int(t.item())
 
 
 def MemEfficientSpGEMM(SR, A, B, phases, hardThreshold, selectNum, recoverNum, recoverPct, kselectVersion=1,
@@ -1185,6 +1191,15 @@ class GpuBackend:
             ctypes.pointer(r)[0] = parts[k]
             out.append(self._take(r))
         return out
+
+    def summa_estimate(self, grid, A, B):
+        """(multiplies, nnz) of this rank's unmerged stage products: symbolic passes only (cbg_summa_estimate)."""
+        ng = self.native_grid(grid)
+        va, vb = self._view(A), self._view(B)
+        f, z = ctypes.c_int64(0), ctypes.c_int64(0)
+        _abi.check(self.ctx._lib.cbg_summa_estimate(ng.ptr, ctypes.byref(va), ctypes.byref(vb), ctypes.byref(f),
+                                                    ctypes.byref(z)), "cbg_summa_estimate")
+        return int(f.value), int(z.value)
 
     def reduce_all(self, grid, parts, sr, stats=None):
         ng = self.native_grid(grid)

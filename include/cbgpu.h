@@ -230,7 +230,20 @@ cbg_status cbg_col_concat(cbg_ctx* ctx, const cbg_csc_result* parts, int32_t npa
  */
 cbg_status cbg_mis2_restriction(cbg_ctx* ctx, const cbg_dcsc_view* G, uint64_t seed, cbg_csc_result* R,
                                 cbg_csc_result* RT, int64_t* nagg);
+/*
+ * cbg_restriction_op: the reference's RestrictionOp (3DSpGEMM/RestrictionOp.h:196-291) of the square matrix A
+ *   (values ignored) at one rank, entry for entry: B = pattern(A) + pattern(A)^T without loops, MIS2 on B
+ *   (:116-193) with the MTRand stream of mt_seed, parents by MIS2verifySR, one draw per parented vertex,
+ *   Select2ndRandSR for the rest (equal draws: the larger neighbour), aggregate columns in set-vertex order
+ *   permuted by RandPerm (std::shuffle, std::default_random_engine(perm_seed); FullyDistVec.cpp:783-900).
+ *   The reference's DETERMINISTIC seeds are mt_seed = 1, perm_seed = 1383098845 (its output is deterministic
+ *   with one OpenMP thread only).  R (n x nagg, R(i, agg(i)) = 1) and, if RT is not NULL, R^T.
+ */
+cbg_status cbg_restriction_op(cbg_ctx* ctx, const cbg_dcsc_view* A, uint32_t mt_seed, uint32_t perm_seed,
+                              cbg_csc_result* R, cbg_csc_result* RT, int64_t* nagg);
 cbg_status cbg_galerkin_rap(cbg_ctx* ctx, const cbg_dcsc_view* A, const cbg_dcsc_view* R, cbg_csc_result* C);
+/* C = A^T (SpDCCols::Transpose, SpDCCols.cpp:845) on the device, rows sorted; f64 values or a pattern. */
+cbg_status cbg_transpose(cbg_ctx* ctx, const cbg_dcsc_view* A, cbg_csc_result* C);
 
 /*
  * ---------------------------------------------------------------------------------------------
@@ -316,6 +329,11 @@ cbg_status cbg_spgemm_grid(cbg_grid* grid, const cbg_dcsc_view* A, const cbg_dcs
 cbg_status cbg_summa_layer(cbg_grid* grid, const cbg_dcsc_view* A, const cbg_dcsc_view* B, cbg_semiring sr,
                            cbg_dtype out_type, uint32_t flags, cbg_csc_result* parts, int32_t* nparts,
                            cbg_grid_stats* stats);
+/* EstPerProcessNnzSUMMA (ParFriends.h:1242-1347): the layer SUMMA's broadcasts with only the symbolic pass of
+ * every stage product (estimateFLOP + estimateNNZ_Hash); *flops / *nnz are this rank's sums over the stages.
+ * No product is formed. */
+cbg_status cbg_summa_estimate(cbg_grid* grid, const cbg_dcsc_view* A, const cbg_dcsc_view* B, int64_t* flops,
+                              int64_t* nnz);
 /* Merge the stage products, then (L > 1) the fiber exchange + merge: the rank's colsplit C piece. */
 cbg_status cbg_reduce_all(cbg_grid* grid, const cbg_csc_result* parts, int32_t nparts, cbg_semiring sr,
                           cbg_dtype out_type, cbg_csc_result* C, cbg_grid_stats* stats);

@@ -527,3 +527,49 @@ def run_mcl_fixture_case(rank, world, port, backend_kind, cases, errq):
         import traceback
         errq.put(f"rank {rank}: {e!r}\n{traceback.format_exc()}")
         raise
+
+
+def run_galerkin_case(rank, world, port, backend_kind, cases, errq):
+    """Per-rank body of the distributed Galerkin product (BASELINE config 5; RestrictionOp.cpp:155-196): with the
+    reference's R (golden/galerkin.npz, made by refrestrict), R^T A and then (R^T A) R through the mandated layout
+    for `world` -- Mult_AnXBn_SUMMA3D and the 3DSpGEMM multiply the reference's Galerkin driver calls -- and every
+    rank's piece of both products against the reference's (refprobe LocalSpGEMMHash)."""
+    try:
+        init_group(rank, world, port, backend_kind)
+        L, q, _ = cbd.grid_for(world)
+        grid = cbd.CommGrid3D(L, q, q)
+        import combblas_amd as cb
+        be = cbd.GpuBackend(cb.Context(0)) if backend_kind.startswith("gpu") else ScipyBackend()
+        from helpers import load_fixture
+        z = load_fixture("galerkin")
+        n, nagg = (int(x) for x in z["R_shape"])
+        PT = _sr_obj("plus_times", "f64")
+        RT = cbd.SpParMat3D.from_global_csc(grid, nagg, n, z["RT_cp"], z["RT_ir"], z["RT_val"], True, be)
+        A = cbd.SpParMat3D.from_global_csc(grid, n, n, z["A_cp"], z["A_ir"], z["A_val"], False, be)
+        R = cbd.SpParMat3D.from_global_csc(grid, n, nagg, z["R_cp"], z["R_ir"], z["R_val"], False, be)
+        gRA = sp.csc_matrix((z["RA_val"], z["RA_ir"], z["RA_cp"]), shape=(nagg, n))
+        gC = sp.csc_matrix((z["C_val"], z["C_ir"], z["C_cp"]), shape=(nagg, nagg))
+        if not backend_kind.startswith("gpu"):
+            # scipy's product drops entries that cancel to 0.0; the reference (and libcbgpu) keep them
+            # (returnedSAID() is false), so the CPU stand-in is compared with the fixture's zeros removed
+            for M in (gRA, gC):
+                M.eliminate_zeros()
+        for name in cases:
+            mult = cbd.Mult_AnXBn_SUMMA3D if name == "SUMMA3D" else cbd.multiply
+            stats = {}
+            RA = mult(PT, RT, A, stats) if name == "SUMMA3D" else mult(PT, RT, A)
+            check_piece_exact_or_f64(RA, gRA, rank, f"galerkin/{name}/RtA", None)
+            C = mult(PT, RA, R)
+            check_piece_exact_or_f64(C, gC, rank, f"galerkin/{name}/RtAR", None)
+            if name == "SUMMA3D":
+                t = torch.tensor([stats.get("multiplies", 0)], dtype=torch.int64, device=be.comm_device)
+                dist.all_reduce(t)
+                assert int(t.item()) == int(z["RA_flops"]), (int(t.item()), int(z["RA_flops"]))
+            if backend_kind.startswith("gpu-rccl"):
+                assert be.native_grid(grid).info() == rccl_info(grid), be.native_grid(grid).info()
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:
+        import traceback
+        errq.put(f"rank {rank}: {e!r}\n{traceback.format_exc()}")
+        raise

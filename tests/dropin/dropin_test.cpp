@@ -198,8 +198,12 @@ int run3d(int q, int L, const std::string& fa, const std::string& fc, const std:
     for (auto* t : sl) delete t;
     delete S; delete R; delete D; delete DO;
   }
-  // Mult_AnXBn_SUMMA3D on SpParMat3D(A2D, L, colsplit) x SpParMat3D(A2D, L, rowsplit)
-  for (int f = 0; f < 2; ++f) {
+  // Mult_AnXBn_SUMMA3D on SpParMat3D(A2D, L, colsplit) x SpParMat3D(A2D, L, rowsplit).  The reference builds an
+  // SpParMat3D from a 2D SpParMat on a square CommGrid of all ranks (CommGrid.cpp:37-76), so this part runs
+  // where the world is a square (4 ranks: 2x2x1 and 1x1x4); 2 and 8 ranks cover the split-3D driver only.
+  const int world = q * q * L;
+  const int side = (int)std::lround(std::sqrt((double)world));
+  for (int f = 0; f < 2 && side * side == world; ++f) {
     typedef SpDCCols<I, double> DCC;
     typedef SpParMat<I, double, DCC> PM;
     typedef SpParMat3D<I, double, DCC> PM3;

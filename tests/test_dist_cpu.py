@@ -62,3 +62,10 @@ def test_memeff3d_phases_match_reference_gloo_cpu(world, port):
     (golden/mcl.npz) on every rank's piece, with the same branch counts."""
     from dist_support import run_mcl_fixture_case
     spawn_case(world, "scipy", [1, 2, 3, ("mem", 0.0025)], port, body=run_mcl_fixture_case)
+
+
+@pytest.mark.parametrize("world,port", [(2, 29661), (4, 29662), (8, 29663)])
+def test_galerkin_reference_restriction_gloo_cpu(world, port):
+    """R^T A then (R^T A) R with the reference's R on the 1x1x2 / 2x2 / 2x2x2 layouts (SUMMA3D and multiply)."""
+    from dist_support import run_galerkin_case
+    spawn_case(world, "scipy", ["SUMMA3D", "multiply"], port, body=run_galerkin_case)

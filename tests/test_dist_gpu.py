@@ -106,3 +106,13 @@ def test_reference_fixtures_staged_schedule_gloo_gpu(world, port, monkeypatch):
     from dist_support import run_fixture_case
     monkeypatch.setenv("CBG_GRID_STAGED", "1")
     spawn_case(world, "gpu", FIXTURE_CASES, port, body=run_fixture_case)
+
+
+@pytest.mark.parametrize("kind", ["gpu", "gpu-rccl-net"])
+@pytest.mark.parametrize("world,port", [(2, 29681), (4, 29682), (8, 29683)])
+def test_galerkin_reference_restriction_multirank_gpu(world, port, kind):
+    """BASELINE config 5 distributed: R^T A then (R^T A) R with the reference's R (refrestrict) through libcbgpu's
+    grid on the 1x1x2 / 2x2 / 2x2x2 layouts -- over the host-staged gloo transport and over RCCL (every rank its
+    own RCCL node) -- every rank's piece of both products equal to the reference's."""
+    from dist_support import run_galerkin_case
+    spawn_case(world, kind, ["SUMMA3D", "multiply"], port + (10 if kind != "gpu" else 0), body=run_galerkin_case)

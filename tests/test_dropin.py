@@ -85,7 +85,9 @@ def test_dropin_3dspgemm_and_summa3d_on_gpu(q, L, tmp_path):
     q x q x L MPI ranks sharing cuda:0, set up as test_mpipspgemm.cpp:101-153 does (ReadMat + SplitMat of
     bcsstk01), against the reference's multiply / SUMMALayer on the same split pieces and against MATLAB's
     C.mtx; and gpu::Mult_AnXBn_SUMMA3D against the reference's Mult_AnXBn_SUMMA3D on SpParMat3D operands
-    with L layers (bcsstk01 within 1e-12 of sum|a*b|, Graph500 s10 bit-exact), every rank's piece."""
+    with L layers (bcsstk01 within 1e-12 of sum|a*b|, Graph500 s10 bit-exact), every rank's piece, where the
+    world is a square (the reference's SpParMat3D is built from a 2D SpParMat on a square CommGrid: 2x2x1 and
+    1x1x4 here; 1x1x2 and 2x2x2 exercise the split-3D driver)."""
     mpirun = "/opt/conda/bin/mpirun"
     if not os.path.exists(BIN) or not os.path.exists(mpirun):
         pytest.skip("dropin_test or MPICH's mpirun not available")

@@ -200,7 +200,7 @@ def test_restriction_matches_host(gpu_ctx, kind, seed):
     else:   # isolated vertices (empty columns) each become their own aggregate
         G = _random_symmetric(3000, 1e-4, seed)
     nagg, rcp, rir, rval = aggregation_restriction(G.nrow, G.cp, G.ir, seed=seed)
-    R, RT = cb.RestrictionOp(up(gpu_ctx, G), seed=seed)
+    R, RT = cb.MIS2Restriction(up(gpu_ctx, G), seed=seed)
     Rh = host(R, G.nrow)
     assert R.getncol() == nagg
     assert np.array_equal(Rh.cp, rcp) and np.array_equal(Rh.ir, rir) and np.array_equal(Rh.val, rval)
@@ -226,7 +226,7 @@ def test_galerkin_rap_fused_vs_two_products(gpu_ctx, k, seed):
     (f64 within 1e-12 of sum|r a r|; weighted R rows exercise the value scaling)."""
     n, acp, air, aval = poisson3d(k)
     dA = up(gpu_ctx, Csc(n, n, acp, air, aval))
-    R, RT = cb.RestrictionOp(dA, seed=seed)
+    R, RT = cb.MIS2Restriction(dA, seed=seed)
     Rh = host(R, n)
     nagg = R.getncol()
     w = 0.5 + (np.arange(Rh.nnz) % 7) / 8.0           # a weighted aggregation (one nonzero per row)
@@ -242,19 +242,28 @@ def test_galerkin_rap_fused_vs_two_products(gpu_ctx, k, seed):
         assert_same_product(host(C, nagg), host(two, nagg), "f64", what="fused vs two products")
 
 
-def test_galerkin_rap_rejects_non_aggregation(gpu_ctx):
+def test_galerkin_rap_non_aggregation_takes_two_products(gpu_ctx):
+    """An R that is no aggregation (row 0 in two aggregates): the fused kernel declines (CBG_EUNSUP, checked
+    through the raw ABI) and GalerkinRAP runs the reference's two products with R^T made by cbg_transpose."""
+    import ctypes
+    from combblas_amd import _abi
     n = 50
     A = Csc(n, n, np.arange(n + 1), np.arange(n), np.ones(n))
-    # row 0 in two aggregates
     R = Csc(n, 2, np.array([0, 26, 51]), np.r_[np.arange(26), 0, np.arange(26, 50)], np.ones(51))
-    with pytest.raises(cb.CbgError) as ei:
-        cb.GalerkinRAP(up(gpu_ctx, A), up(gpu_ctx, R))
-    assert ei.value.status == 11
+    dA, dR = up(gpu_ctx, A), up(gpu_ctx, R)
+    res = _abi.CscResult()
+    st = gpu_ctx._lib.cbg_galerkin_rap(gpu_ctx._ptr, ctypes.byref(dA._view()), ctypes.byref(dR._view()),
+                                       ctypes.byref(res))
+    assert st == _abi.EUNSUP
+    C = cb.GalerkinRAP(dA, dR)
+    ORA, _, _ = oracle_spgemm(_transpose(R), A, "plus_times", "f64")
+    OC, _, _ = oracle_spgemm(ORA, R, "plus_times", "f64")
+    assert_same_product(host(C, 2), OC, "f64", what="two-product RtAR")
 
 
 def test_galerkin_rap_large_aggregate_falls_back(gpu_ctx):
-    """An aggregate gathering more than 512 entries of A: the fused kernel declines (CBG_EUNSUP) and,
-    given RT, GalerkinRAP runs the reference's two products."""
+    """An aggregate gathering more than 512 entries of A: the fused kernel declines (CBG_EUNSUP) and
+    GalerkinRAP runs the reference's two products (R^T given, or built by cbg_transpose)."""
     G = _random_symmetric(400, 0.02, 4)
     n = G.nrow
     A = Csc(n, n, G.cp, G.ir, np.linspace(0.5, 1.5, G.nnz))
@@ -264,11 +273,86 @@ def test_galerkin_rap_large_aggregate_falls_back(gpu_ctx):
     Rs.sort_indices()
     R = Csc(n, 8, Rs.indptr, Rs.indices, Rs.data)
     dA, dR, dRT = up(gpu_ctx, A), up(gpu_ctx, R), up(gpu_ctx, _transpose(R))
-    with pytest.raises(cb.CbgError) as ei:
-        cb.GalerkinRAP(dA, dR)
-    assert ei.value.status == 11
-    C = cb.GalerkinRAP(dA, dR, dRT)
     Rt = _transpose(R)
     ORA, _, _ = oracle_spgemm(Rt, A, "plus_times", "f64")
     OC, _, _ = oracle_spgemm(ORA, R, "plus_times", "f64")
-    assert_same_product(host(C, 8), OC, "f64", what="fallback RtAR")
+    for C in (cb.GalerkinRAP(dA, dR, dRT), cb.GalerkinRAP(dA, dR)):   # given R^T, and R^T built on the device
+        assert_same_product(host(C, 8), OC, "f64", what="fallback RtAR")
+
+
+# ------------------------------------------------------------------ the reference's RestrictionOp (f3)
+RESTRICTION_CASES = ["poisson6", "poisson12", "poisson80", "g500_s10", "unsym700"]
+
+
+def _restriction_input(z, name):
+    if name.startswith("poisson"):
+        n, cp, ir, val = poisson3d(int(name[len("poisson"):]))
+        return Csc(n, n, cp, ir, val)
+    n = len(z[f"{name}_agg"])
+    cp, ir = z[f"{name}_cp"], z[f"{name}_ir"]
+    return Csc(n, n, cp, ir, np.ones(len(ir)))
+
+
+@pytest.mark.parametrize("name", RESTRICTION_CASES)
+def test_restriction_op_matches_reference(gpu_ctx, name):
+    """cbg_restriction_op on the device = the reference's RestrictionOp (3DSpGEMM/RestrictionOp.h:196-291, run by
+    oracle/_ref/refrestrict at one rank, DETERMINISTIC seeds) entry for entry: the same MIS-2 set from the same
+    MTRand stream, the same Select2ndRandSR aggregation, the same RandPerm column order; RT = R^T.  Poisson
+    k = 6/12/80 (k = 80: 46343 aggregates, libstdc++'s one-swap-per-draw shuffle branch), the Graph500 s10
+    matrix (loops, unsymmetric) and an unsymmetric matrix with isolated vertices."""
+    z = load_fixture("restriction")
+    G = _restriction_input(z, name)
+    R, RT = cb.RestrictionOp(up(gpu_ctx, G))
+    nagg = int(z[f"{name}_nagg"])
+    assert R.getncol() == nagg and R.getnrow() == G.nrow
+    Rh = host(R, G.nrow)
+    agg = z[f"{name}_agg"].astype(np.int64)
+    order = np.lexsort((np.arange(G.nrow), agg))
+    cp = np.zeros(nagg + 1, np.int64)
+    np.cumsum(np.bincount(agg, minlength=nagg), out=cp[1:])
+    assert np.array_equal(Rh.cp, cp) and np.array_equal(Rh.ir, order) and np.all(Rh.val == 1.0)
+    RTh = host(RT, nagg)
+    T = _transpose(Rh)
+    assert np.array_equal(RTh.cp, T.cp) and np.array_equal(RTh.ir, T.ir) and np.array_equal(RTh.val, T.val)
+
+
+def test_restriction_op_seeds_change_the_aggregation(gpu_ctx):
+    """Other seeds give another (still valid) aggregation: one entry per row, every aggregate non-empty."""
+    n, cp, ir, val = poisson3d(12)
+    dA = up(gpu_ctx, Csc(n, n, cp, ir, val))
+    R1, _ = cb.RestrictionOp(dA)
+    R2, _ = cb.RestrictionOp(dA, mt_seed=7, perm_seed=11)
+    a, b = host(R1, n), host(R2, n)
+    assert b.nnz == n and np.all(np.diff(b.cp) > 0)
+    assert not (np.array_equal(a.cp, b.cp) and np.array_equal(a.ir, b.ir))
+
+
+@pytest.mark.parametrize("fused", [True, False])
+def test_galerkin_on_device_reference_restriction(gpu_ctx, fused):
+    """End to end on the device: R from cbg_restriction_op, then R^T A R (fused, or the reference's two products
+    with R^T built by cbg_transpose) equals the reference's R^T A R on the reference's R (golden/galerkin.npz,
+    made by refrestrict + refprobe's LocalSpGEMMHash)."""
+    z = load_fixture("galerkin")
+    n, nagg = (int(x) for x in z["R_shape"])
+    A = Csc(n, n, z["A_cp"], z["A_ir"], z["A_val"])
+    dA = up(gpu_ctx, A)
+    R, RT = cb.RestrictionOp(dA)
+    Rh = host(R, n)
+    assert np.array_equal(Rh.cp, z["R_cp"]) and np.array_equal(Rh.ir, z["R_ir"])
+    C = cb.GalerkinRAP(dA, R, fused=fused)
+    assert_same_product(host(C, nagg), Csc(nagg, nagg, z["C_cp"], z["C_ir"], z["C_val"]), "f64", what="RtAR")
+
+
+def test_transpose_matches_scipy(gpu_ctx):
+    M = _random_symmetric(900, 3e-3, 21)
+    import scipy.sparse as sp
+    S = sp.random(700, 900, density=0.01, format="csc", random_state=np.random.default_rng(5))
+    S.sort_indices()
+    A = Csc(700, 900, S.indptr, S.indices, S.data)
+    T = cb.Transpose(up(gpu_ctx, A))
+    Th = host(T, 700)
+    E = S.T.tocsc()
+    E.sort_indices()
+    assert T.getnrow() == 900 and T.getncol() == 700
+    assert np.array_equal(Th.cp, E.indptr) and np.array_equal(Th.ir, E.indices) and np.array_equal(Th.val, E.data)
+    assert M.nnz > 0
