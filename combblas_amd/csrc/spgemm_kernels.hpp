@@ -981,6 +981,9 @@ __global__ void __launch_bounds__(NT) k_sym_block(const int32_t* __restrict__ li
 #endif
 constexpr int kPartLog = CBG_PART_LOG;
 constexpr int kPartNT = CBG_PART_NT;
+#ifndef CBG_SYM_ROWS_WAVE
+#define CBG_SYM_ROWS_WAVE 0   // 1: k_sym_part emits its rows word-major per wave (measured slower, r03d)
+#endif
 #ifndef CBG_SYM_TESTOR
 #define CBG_SYM_TESTOR 1   // k_sym_part reads a bitmap word before setting a bit (0: no-return ds_or only)
 #endif
@@ -1101,6 +1104,31 @@ __global__ void __launch_bounds__(NT) k_sym_part(const PartItem* __restrict__ it
     __syncthreads();
     STAMP(28);
     const int64_t off = (int64_t)(uint32_t)misc[4] | ((int64_t)misc[5] << 32);
+#if CBG_SYM_ROWS_WAVE
+    if (off >= 0) {
+      // this part's sorted rows for the numeric pass, word-major per wave: at step s the wave's 64 lanes take
+      // 64 consecutive bitmap words, a wave scan of their popcounts places them, and each lane writes its word's
+      // rows -- the stores of one instruction fall in one short run of positions (coalesced), and a lane's
+      // serial work is one word (<= 32 rows), not its 16 words
+      const int l = lane_id();
+      const int w0 = (threadIdx.x / kWave) * kWave * WPT;
+      int64_t base = off + __shfl(ex, 0, kWave);   // rows of the words before the wave's (thread order = word order)
+      for (int s = 0; s < WPT; ++s) {
+        const int wi = w0 + s * kWave + l;
+        uint32_t wd = tab[wi];
+        const int c = __popc(wd);
+        const int inc = wave_incl_scan(c);
+        int64_t pos = base + inc - c;
+        const int32_t rb = r0 + 32 * wi;
+        while (wd) {
+          const int b = __ffs(wd) - 1;
+          wd &= wd - 1;
+          ho.rows[pos++] = rb + b;
+        }
+        base += __shfl(inc, kWave - 1, kWave);
+      }
+    }
+#else
     if (off >= 0) {   // this part's sorted rows for the numeric pass (each thread: its words' rows)
       int64_t pos = off + ex;
 #pragma unroll
@@ -1113,6 +1141,7 @@ __global__ void __launch_bounds__(NT) k_sym_part(const PartItem* __restrict__ it
         }
       }
     }
+#endif
     if (threadIdx.x == 0 && misc[0]) atomicAdd((unsigned long long*)&nnz[it.j], (unsigned long long)misc[0]);
     const int32_t sf = max(s0, sp.x >> spl.log), sl = min(s1 - 1, sp.y >> spl.log);
     int32_t* dst = ho.sub + (int64_t)it.h * ho.nsub;
