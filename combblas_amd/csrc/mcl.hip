@@ -23,6 +23,10 @@
 //                 largest order-preserving key, LDS histogram, wave-parallel digit search
 //   k_mcl_count   wave per column: kept entries -> scan -> colptr
 //   k_mcl_compact wave per column: ballot compaction in column order
+//   k_mcl_fused   (default) workgroup per column: the first three in one read of the values (LDS-staged
+//                 column, selection on the LDS copy); CBG_MCL_SPLIT=1 runs the three kernels instead.
+//                 (A wave-per-column variant holding the column in registers was measured slower: 436 VGPRs,
+//                 one wave per SIMD -- profiles/r03i_config4_prune_variants.txt.)
 #include "spgemm_host.hpp"
 
 namespace cbg {
@@ -103,18 +107,16 @@ __global__ void __launch_bounds__(256) k_mcl_stats(int64_t ncol, const int64_t* 
   }
 }
 
-// k-th largest value of val[a, b) (Kselect1 semantics); all NT threads of the block call it
-template <typename V, int NT>
-__device__ V block_kth(const V* __restrict__ val, int64_t a, int64_t b, int64_t k, unsigned* hist, V* red,
-                       unsigned long long* bc) {
+// k-th largest value of the n values ld(0..n-1) (Kselect1 semantics); all NT threads of the block call it
+template <typename V, int NT, class LD>
+__device__ V block_kth_ld(LD ld, int64_t n, int64_t k, unsigned* hist, V* red, unsigned long long* bc) {
   using KO = KeyOf<V>;
   using K = typename KO::K;
   constexpr int B = 8 * (int)sizeof(K);
-  const int64_t n = b - a;
   if (n == 0) return vmin_pos<V>();
   if (n < k) {   // fewer than k entries: the smallest one (last of the descending partial sort)
-    V m = val[a];
-    for (int64_t i = a + threadIdx.x; i < b; i += NT) m = min(m, val[i]);
+    V m = ld(0);
+    for (int64_t i = threadIdx.x; i < n; i += NT) m = min(m, ld(i));
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) m = min(m, __shfl_xor(m, d, kWave));
     if (lane_id() == 0) red[threadIdx.x / kWave] = m;
@@ -130,8 +132,8 @@ __device__ V block_kth(const V* __restrict__ val, int64_t a, int64_t b, int64_t 
     for (int i = threadIdx.x; i < 256; i += NT) hist[i] = 0;
     __syncthreads();
     const K himask = (shift + 8 >= B) ? (K)0 : ~(((K)1 << (shift + 8)) - 1);
-    for (int64_t i = a + threadIdx.x; i < b; i += NT) {
-      const K key = KO::key(val[i]);
+    for (int64_t i = threadIdx.x; i < n; i += NT) {
+      const K key = KO::key(ld(i));
       if ((key & himask) == prefix) atomicAdd(&hist[(key >> shift) & 255], 1u);
     }
     __syncthreads();
@@ -163,6 +165,104 @@ __device__ V block_kth(const V* __restrict__ val, int64_t a, int64_t b, int64_t 
     __syncthreads();
   }
   return KO::val(prefix);
+}
+
+template <typename V, int NT>
+__device__ V block_kth(const V* __restrict__ val, int64_t a, int64_t b, int64_t k, unsigned* hist, V* red,
+                       unsigned long long* bc) {
+  return block_kth_ld<V, NT>([&](int64_t i) { return val[a + i]; }, b - a, k, hist, red, bc);
+}
+
+// One pass over the column values for everything but the compaction: the column is staged in LDS (columns of
+// up to kMclCap entries; longer ones are read from HBM), wave 0 takes the statistics in k_mcl_stats' order, the
+// k-selections run on the LDS copy (k_mcl_select's radix select and recovery test), and the kept count of
+// k_mcl_count -- one read of the values instead of three, and the select passes hit LDS.
+constexpr int kMclCap = 4096;
+
+template <typename V, int NT>
+__global__ void __launch_bounds__(NT) k_mcl_fused(int64_t ncol, const int64_t* __restrict__ cp,
+                                                  const V* __restrict__ val, MclParams p, V* __restrict__ th,
+                                                  int64_t* __restrict__ cnt, unsigned long long* __restrict__ counters) {
+  __shared__ V lv[kMclCap];
+  __shared__ unsigned hist[256];
+  __shared__ V red[NT / kWave];
+  __shared__ int64_t rn[NT / kWave];
+  __shared__ unsigned long long bc[2];
+  __shared__ int smode;
+  for (int64_t j = blockIdx.x; j < ncol; j += gridDim.x) {
+    const int64_t a = cp[j], b = cp[j + 1], n = b - a;
+    const bool inl = n <= kMclCap;
+    if (inl) {   // 8 independent loads in flight per thread, then the LDS stores
+      for (int64_t i0 = threadIdx.x; i0 < n; i0 += 8 * NT) {
+        V r[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) r[u] = i0 + u * NT < n ? val[a + i0 + u * NT] : V(0);
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (i0 + u * NT < n) lv[i0 + u * NT] = r[u];
+      }
+    }
+    __syncthreads();
+    auto ld = [&](int64_t i) -> V { return inl ? lv[i] : val[a + i]; };
+    const V thr = (V)p.thr;
+    if (threadIdx.x < kWave) {   // column statistics, in k_mcl_stats' lane order
+      int64_t np = 0;
+      V sp = 0;
+      for (int64_t k = lane_id(); k < n; k += kWave) {
+        const V v = ld(k);
+        if (v > thr) { ++np; sp += v; }
+      }
+      np = wave_sum(np);
+      sp = wave_sum(sp);
+      if (lane_id() == 0) {
+        int m = kModeThr;
+        if (np < p.R && n > np && sp < (V)p.pct) m = kModeRecover;
+        else if (p.S > 0 && np > p.S) m = kModeSelect;
+        smode = m;
+        if (m != kModeThr) atomicAdd(&counters[m], 1ull);
+      }
+    }
+    __syncthreads();
+    const int m = smode;
+    V t = thr;
+    if (m == kModeRecover) {
+      t = block_kth_ld<V, NT>(ld, n, p.R, hist, red, bc);
+    } else if (m == kModeSelect) {
+      t = block_kth_ld<V, NT>(ld, n, p.S, hist, red, bc);
+      if (p.R > 0) {   // recovery after selection (ParFriends.h:290-333), k_mcl_select's order
+        int64_t n1 = 0;
+        V s1 = 0;
+        for (int64_t i = threadIdx.x; i < n; i += NT) {
+          const V v = ld(i);
+          if (v >= t) { ++n1; s1 += v; }
+        }
+        n1 = wave_sum(n1);
+        s1 = wave_sum(s1);
+        if (lane_id() == 0) { rn[threadIdx.x / kWave] = n1; red[threadIdx.x / kWave] = s1; }
+        __syncthreads();
+        int64_t N1 = 0;
+        V S1 = 0;
+        for (int w = 0; w < NT / kWave; ++w) { N1 += rn[w]; S1 += red[w]; }
+        __syncthreads();
+        if (N1 < p.R && S1 < (V)p.pct) {
+          t = block_kth_ld<V, NT>(ld, n, p.R, hist, red, bc);
+          if (threadIdx.x == 0) atomicAdd(&counters[3], 1ull);
+        }
+      }
+    }
+    int64_t c = 0;   // kept entries (v >= t)
+    for (int64_t i = threadIdx.x; i < n; i += NT) c += ld(i) >= t;
+    c = wave_sum(c);
+    if (lane_id() == 0) rn[threadIdx.x / kWave] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int64_t C = 0;
+      for (int w = 0; w < NT / kWave; ++w) C += rn[w];
+      cnt[j] = C;
+      th[j] = t;
+    }
+    __syncthreads();
+  }
 }
 
 template <typename V, int NT>
@@ -238,18 +338,26 @@ __global__ void __launch_bounds__(256) k_mcl_compact(int64_t ncol, const int64_t
     const int64_t a = cp[j], b = cp[j + 1];
     const V t = th[j];
     int64_t o = ocp[j];
-    for (int64_t k0 = a; k0 < b; k0 += kWave) {
-      const int64_t k = k0 + l;
-      V v = 0;
-      bool keep = false;
-      if (k < b) { v = val[k]; keep = v >= t; }
-      const unsigned long long m = __ballot(keep);
-      if (keep) {
-        const int64_t d = o + __popcll(m & below);
-        oir[d] = ir[k];
-        oval[d] = v;
+    for (int64_t k0 = a; k0 < b; k0 += 4 * kWave) {   // four chunks' loads in flight, then their compaction
+      V v[4];
+      int32_t r[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int64_t k = k0 + u * kWave + l;
+        v[u] = k < b ? val[k] : V(0);
+        r[u] = k < b ? ir[k] : 0;
       }
-      o += __popcll(m);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const bool keep = k0 + u * kWave + l < b && v[u] >= t;
+        const unsigned long long m = __ballot(keep);
+        if (keep) {
+          const int64_t d = o + __popcll(m & below);
+          oir[d] = r[u];
+          oval[d] = v[u];
+        }
+        o += __popcll(m);
+      }
     }
   }
 }
@@ -309,11 +417,17 @@ cbg_status mcl_prune_impl(cbg_ctx* ctx, const cbg_csc_result* in, const MclParam
   HIPCHK(hipMemsetAsync(sc, 0, 64, st));
   const V* val = (const V*)in->val;
   const int gw = (int)grid_for(N, 4, kMaxGrid * 2);
-  if (N > 0) {
+  static const bool split_passes = [] { const char* e = std::getenv("CBG_MCL_SPLIT"); return e && e[0] == '1'; }();
+  if (N > 0 && split_passes) {   // the three-pass form (stats, select of the listed columns, count)
     k_mcl_stats<V><<<gw, 256, 0, st>>>(N, in->colptr, val, p, th.as<V>(), mode.as<int32_t>(), list.as<int32_t>(), sc);
     k_mcl_select<V, 256><<<(int)grid_for(N, 1, kMaxGrid * 2), 256, 0, st>>>(
         list.as<int32_t>(), sc, in->colptr, val, p, th.as<V>(), mode.as<int32_t>(), sc);
     k_mcl_count<V><<<gw, 256, 0, st>>>(N, in->colptr, val, th.as<V>(), cnt.as<int64_t>());
+  } else if (N > 0) {
+    k_mcl_fused<V, 256><<<(int)grid_for(N, 1, kMaxGrid * 8), 256, 0, st>>>(N, in->colptr, val, p, th.as<V>(),
+                                                                          cnt.as<int64_t>(), sc);
+  }
+  if (N > 0) {
     const int64_t ntiles = (N + kScanTile - 1) / kScanTile;
     HIPCHK(tiles.reserve(sizeof(int64_t) * (ntiles + 1)));
     k_scan_tiles<<<(int)ntiles, 256, 0, st>>>(N, cnt.as<int64_t>(), tiles.as<int64_t>());
