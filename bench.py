@@ -247,11 +247,13 @@ def bench_dist(args, world, rank, local_rank):
             os.environ.update({"NCCL_HOSTID": f"cbg-bench-rank-{rank}", "NCCL_SOCKET_IFNAME": "lo",
                                "NCCL_IB_DISABLE": "1", "CBG_GRID_TRANSPORT": "rccl"})
         dist.init_process_group("gloo")
-    L, q, _ = cbd.grid_for(world)
-    grid = cbd.CommGrid3D(L, q, q)
     ctx = cb.Context(dev)
     be = cbd.GpuBackend(ctx)
     n = 1 << args.scale
+    if args.layout == "1d":
+        return bench_1d(args, world, rank, ctx, be, n, backend)
+    L, q, _ = cbd.grid_for(world)
+    grid = cbd.CommGrid3D(L, q, q)
     t0 = time.perf_counter()
     # every rank builds only its own pieces, on its GPU (SpParMat3D.from_rmat -> cbg_rmat_block)
     A = cbd.SpParMat3D.from_rmat(grid, args.scale, args.edgefactor, args.seed, True, be)
@@ -268,7 +270,8 @@ def bench_dist(args, world, rank, local_rank):
         C = cbd.Mult_AnXBn_SUMMA3D(SR, A, B, st)
         nz = C.block.nnz
         del C
-        for k in ("bcast_ms", "local_ms", "merge_ms", "fiber_ms", "total_ms", "bcast_bytes", "fiber_bytes"):
+        for k in ("bcast_ms", "local_ms", "merge_ms", "fiber_ms", "total_ms", "bcast_bytes", "fiber_bytes",
+                  "fiber_xfer_ms"):
             phases[k] = phases.get(k, 0) + st.get(k, 0)
         return st.get("multiplies", 0), nz
 
@@ -320,6 +323,101 @@ def bench_dist(args, world, rank, local_rank):
     dist.destroy_process_group()
 
 
+def bench_1d(args, world, rank, ctx, be, n, backend):
+    """SURVEY §8(e)'s stated comparison (not the mandated layouts): a 1D column split.  Rank r builds its column
+    block A(:, J_r) on its GPU; every step all-gathers the blocks (A replicated: one RCCL all-gather of counts,
+    rows and values) and multiplies A * A(:, J_r) locally -- C(:, J_r) complete, no merge, no fiber exchange."""
+    import torch
+    import torch.distributed as dist
+    import combblas_amd as cb
+    from combblas_amd import dist as cbd
+    c0, c1 = cbd.block_range(n, world, rank)
+    t0 = time.perf_counter()
+    mine = be.rmat_block(args.scale, args.edgefactor, args.seed, 0, n, c0, c1)   # rows 0..n-1, columns J_r
+    torch.cuda.synchronize()
+    build_s = time.perf_counter() - t0
+    cd = be.comm_device
+    widths = [cbd.block_range(n, world, r)[1] - cbd.block_range(n, world, r)[0] for r in range(world)]
+    nz = torch.tensor([mine.nnz], dtype=torch.int64, device=cd)
+    nzs = [torch.zeros(1, dtype=torch.int64, device=cd) for _ in range(world)]
+    dist.all_gather(nzs, nz)
+    nzs = [int(x.item()) for x in nzs]
+    mx = max(nzs)
+    SR = cb.PlusTimesSRing("f64")
+    phases = {}
+
+    def gather_a():
+        cnt = torch.diff(mine.cp).to(cd)
+        ir = torch.zeros(mx, dtype=torch.int32, device=cd)
+        val = torch.zeros(mx, dtype=torch.float64, device=cd)
+        ir[:mine.nnz] = mine.ir.to(cd)
+        val[:mine.nnz] = mine.val.to(cd)
+        wmax = max(widths)
+        cntp = torch.zeros(wmax, dtype=torch.int64, device=cd)
+        cntp[:cnt.numel()] = cnt
+        outs = []
+        for t, proto in ((cntp, wmax), (ir, mx), (val, mx)):
+            g = torch.empty(world * proto, dtype=t.dtype, device=cd)
+            dist.all_gather_into_tensor(g, t)
+            outs.append(g)
+        cnts = torch.cat([outs[0][r * wmax:r * wmax + widths[r]] for r in range(world)])
+        irs = torch.cat([outs[1][r * mx:r * mx + nzs[r]] for r in range(world)])
+        vals = torch.cat([outs[2][r * mx:r * mx + nzs[r]] for r in range(world)])
+        cp = torch.zeros(n + 1, dtype=torch.int64, device=cd)
+        torch.cumsum(cnts, 0, out=cp[1:])
+        return cbd.Block(n, n, cp.to(be.device), irs.to(be.device), vals.to(be.device))
+
+    def step():
+        ta = time.perf_counter()
+        Afull = gather_a()
+        torch.cuda.synchronize()
+        tb = time.perf_counter()
+        st = {}
+        C = be.multiply(Afull, mine, SR, st)
+        z = C.nnz
+        del C, Afull
+        torch.cuda.synchronize()
+        phases["allgather_ms"] = phases.get("allgather_ms", 0) + 1e3 * (tb - ta)
+        phases["local_ms"] = phases.get("local_ms", 0) + 1e3 * (time.perf_counter() - tb)
+        return st.get("multiplies", 0), z
+
+    for _ in range(max(args.warmup, 1)):
+        step()
+    phases.clear()
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    mults = nnzc = 0
+    for _ in range(args.steps):
+        m, z = step()
+        mults += m
+        nnzc += z
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], dtype=torch.float64, device=cd)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    s = torch.tensor([mults, nnzc], dtype=torch.float64, device=cd)
+    dist.all_reduce(s)
+    elapsed, mults, nnzc = float(t.item()), float(s[0].item()), float(s[1].item())
+    if rank == 0:
+        cfg = workload(args.scale, args.edgefactor, f"1D column split over {world} ranks, A replicated by an "
+                       f"all-gather ({backend}); SURVEY 8(e) comparison, not the mandated layout")
+        nnza = sum(nzs)
+        cfg.update({"nnz_A": nnza, "multiplies": int(mults / args.steps), "nnz_C": int(nnzc / args.steps)})
+        print(json.dumps({"metric": METRIC, "value": mults / elapsed, "unit": "multiplies/s", "n_gpus": world,
+                          "steps": args.steps, "warmup": args.warmup, "ms_per_step": 1000.0 * elapsed / args.steps,
+                          "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+                          "data": "synthetic", "config": cfg,
+                          "effective_GBps": balg_bytes(mults / args.steps, nnzc / args.steps, nnza, n)
+                          / (elapsed / args.steps) / 1e9,
+                          "rank0_phases_per_step": {k: round(v / args.steps, 3) for k, v in phases.items()},
+                          "input": {"rank0_device_build_s": round(build_s, 4)}}), flush=True)
+    dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -329,6 +427,8 @@ def main():
     ap.add_argument("--edgefactor", type=int, default=16)
     ap.add_argument("--seed", type=int, default=0xDECAFBAD, help="Graph500 user seed (the reference's SEED)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--layout", choices=["3d", "1d"], default="3d",
+                    help="N > 1: the mandated 1x1x2 / 2x2 / 2x2x2 layouts (default) or SURVEY 8(e)'s 1D comparison")
     ap.add_argument("--cpu-mults", type=float, default=1.5e9, help="multiplies in the CPU baseline sample")
     args = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))

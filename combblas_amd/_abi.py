@@ -52,7 +52,8 @@ class MclStats(ctypes.Structure):
 class GridStats(ctypes.Structure):
     _fields_ = [("multiplies", ctypes.c_int64), ("bcast_bytes", ctypes.c_int64), ("fiber_bytes", ctypes.c_int64),
                 ("bcast_ms", ctypes.c_double), ("local_ms", ctypes.c_double), ("merge_ms", ctypes.c_double),
-                ("fiber_ms", ctypes.c_double), ("total_ms", ctypes.c_double), ("stages", ctypes.c_int32)]
+                ("fiber_ms", ctypes.c_double), ("total_ms", ctypes.c_double), ("fiber_xfer_ms", ctypes.c_double),
+                ("stages", ctypes.c_int32)]
 
 
 # cbg_transport callbacks (include/cbgpu.h)

@@ -130,6 +130,7 @@ struct Piece {
   std::shared_ptr<Owner> own;    // storage of cp/ir/val (or of cp only, see keep)
   std::shared_ptr<Owner> keep;   // shared storage the arrays point into (fiber receive buffers)
   int32_t k = 0, r = 0;          // stage (inner block) and half of the product: merge order
+  bool reduced = false;          // already reduced over the fiber (fiber_pipeline)
 };
 
 }  // namespace
@@ -466,6 +467,12 @@ cbg_status panel_rows_dt(cbg_ctx* ctx, cbg_dtype dt, const std::vector<Piece>& b
   }
 }
 
+cbg_status fiber_pipeline(cbg_grid* G, const cbg_dcsc_view& va, const cbg_dcsc_view& vb, cbg_semiring sr,
+                          cbg_dtype dt, Piece* out, cbg_grid_stats* st);
+// Internal flag: L = 2, plain product -- the layer product runs in two column halves with the fiber exchange
+// of the other layer's half overlapping the own half (fiber_pipeline); parts then holds the reduced piece.
+constexpr uint32_t kFiberPipe = 1u << 29;
+
 // est != nullptr: count only (EstPerProcessNnzSUMMA) -- every stage runs the symbolic pass alone and est[0] / est[1]
 // accumulate its multiplies and nnz; no product is formed (staged schedule, parts stays empty)
 cbg_status summa_layer_impl(cbg_grid* G, const cbg_dcsc_view* Av, const cbg_dcsc_view* Bv, cbg_semiring sr,
@@ -598,12 +605,19 @@ cbg_status summa_layer_impl(cbg_grid* G, const cbg_dcsc_view* Av, const cbg_dcsc
     pb.clear();
     cbg_dcsc_view va = view_of(AP, dt, AP.val != nullptr);
     cbg_dcsc_view vb = view_of(BP, dt, BP.val != nullptr);
-    cbg_csc_result C;
-    int64_t m = 0;
-    CBGCHK(cbg_spgemm_local(ctx, &va, &vb, sr, dt, CBG_SORTED_COLS, &C, &m));
-    if (st) { st->multiplies += m; st->local_ms += now_ms() - t0; st->stages += q; }
-    Piece P = piece_of_result(C);
-    parts->push_back(P);
+    if (flags & kFiberPipe) {   // product + fiber reduction, overlapped
+      Piece P;
+      CBGCHK(fiber_pipeline(G, va, vb, sr, dt, &P, st));
+      if (st) st->stages += q;
+      parts->push_back(P);
+    } else {
+      cbg_csc_result C;
+      int64_t m = 0;
+      CBGCHK(cbg_spgemm_local(ctx, &va, &vb, sr, dt, CBG_SORTED_COLS, &C, &m));
+      if (st) { st->multiplies += m; st->local_ms += now_ms() - t0; st->stages += q; }
+      Piece P = piece_of_result(C);
+      parts->push_back(P);
+    }
     HIPCHK(hipStreamSynchronize(G->cs));
     HIPCHK(hipStreamSynchronize(ctx->stream));   // panels and receive buffers go back to the pool on return
     float ms = 0.f;
@@ -665,6 +679,15 @@ cbg_status summa_layer_impl(cbg_grid* G, const cbg_dcsc_view* Av, const cbg_dcsc
     return CBG_OK;
   };
   hipStream_t cst = ctx->stream;
+  if ((flags & kFiberPipe) && S == 1 && !est) {   // one stage (q = 1): the own pieces, product + fiber overlapped
+    cbg_dcsc_view va = view_of(Ah[0], dt, Ah[0].val != nullptr);
+    cbg_dcsc_view vb = view_of(Bh[0], dt, Bh[0].val != nullptr);
+    Piece P;
+    CBGCHK(fiber_pipeline(G, va, vb, sr, dt, &P, st));
+    if (st) ++st->stages;
+    parts->push_back(P);
+    return CBG_OK;
+  }
   const bool async = G->rccl && q > 1;
   if (async) CBGCHK(issue(0));
   std::vector<Piece> acc;   // running merge (Overlap)
@@ -862,6 +885,190 @@ cbg_status fiber_exchange(cbg_grid* G, const Piece& C, size_t vs, bool f64, std:
   return CBG_OK;
 }
 
+// L = 2, plain product (reduce_all_impl's exchange-after-product, overlapped): the columns of the other layer's
+// part (block_range of the local columns, as fiber_exchange cuts them) are multiplied first; their counts, rows
+// and values leave for the other layer as one grouped ncclSend/ncclRecv on the communication stream while the own
+// part multiplies on the compute stream; then the received partial and the own one are merged.  The same two
+// pieces and the same two-way merge as the unpipelined path, so the product is identical.  Values travel as f32
+// when both sides' messages survive the round trip (fiber_exchange's rule).  With a caller transport the
+// exchange is synchronous (no overlap, same result).
+cbg_status fiber_pipeline(cbg_grid* G, const cbg_dcsc_view& va, const cbg_dcsc_view& vb, cbg_semiring sr,
+                          cbg_dtype dt, Piece* out, cbg_grid_stats* st) {
+  cbg_ctx* ctx = G->ctx;
+  hipStream_t cst = ctx->stream;
+  const size_t vs = dt_size(dt);
+  const int me = G->layer, other = 1 - me;
+  const int64_t ncol = vb.ncol;
+  const int64_t cb[3] = {0, ncol / 2, ncol};
+  PoolBuf cpo, cpm, scnt, s32, r32, tiles, scal;
+  for (PoolBuf* b : {&cpo, &cpm, &scnt, &s32, &r32, &tiles, &scal}) b->pool = ctx->pool;
+  std::shared_ptr<Owner> rx(new Owner(ctx->pool));
+  StreamFence fence(cst, G->cs);   // transfers into / out of the buffers above end before they return to the pool
+  // column-range views of B: rebased colptr, rows and values from cp[c0]
+  int64_t e[4] = {0, 0, 0, 0};
+  for (int m = 0; m < 2; ++m) {
+    HIPCHK(hipMemcpyAsync(&e[2 * m], (const int64_t*)vb.cp + cb[m], 8, hipMemcpyDeviceToHost, cst));
+    HIPCHK(hipMemcpyAsync(&e[2 * m + 1], (const int64_t*)vb.cp + cb[m + 1], 8, hipMemcpyDeviceToHost, cst));
+  }
+  HIPCHK(hipStreamSynchronize(cst));
+  auto col_view = [&](int m, PoolBuf& cpbuf, cbg_dcsc_view* v) -> cbg_status {
+    const int64_t c0 = cb[m], n = cb[m + 1] - cb[m], e0 = e[2 * m], e1 = e[2 * m + 1];
+    HIPCHK(cpbuf.reserve(8 * (n + 1)));
+    k_cp_rebase<<<(int)grid_for(n + 1, 256, kMaxGrid), 256, 0, cst>>>(n, (const int64_t*)vb.cp, c0, cpbuf.as<int64_t>());
+    HIPCHK(hipGetLastError());
+    *v = vb;
+    v->ncol = n; v->nzc = n; v->nnz = e1 - e0;
+    v->cp = cpbuf.p;
+    v->ir = (const int32_t*)vb.ir + e0;
+    v->val = vb.val ? (const void*)((const char*)vb.val + vs * e0) : nullptr;
+    return CBG_OK;
+  };
+  cbg_dcsc_view vo, vm;
+  CBGCHK(col_view(other, cpo, &vo));
+  CBGCHK(col_view(me, cpm, &vm));
+  // 1. the other layer's columns
+  double t0 = now_ms();
+  cbg_csc_result Ro;
+  int64_t mo = 0;
+  CBGCHK(cbg_spgemm_local(ctx, &va, &vo, sr, dt, CBG_SORTED_COLS, &Ro, &mo));
+  Piece Po = piece_of_result(Ro);
+  double t_local = now_ms() - t0;
+  // 2. column counts, the f32 verdict and the sizes (host-synchronous, 8 bytes each way)
+  t0 = now_ms();
+  const int64_t myc = cb[me + 1] - cb[me], oc = Po.ncol;
+  HIPCHK(scnt.reserve(8 * (oc + 1)));
+  if (oc) k_col_counts<<<(int)grid_for(oc, 256, kMaxGrid), 256, 0, cst>>>(oc, Po.cp, scnt.as<int64_t>());
+  HIPCHK(hipGetLastError());
+  bool narrow = dt == CBG_F64 && Po.val != nullptr && vs == 8;
+  if (narrow) {
+    const char* env = std::getenv("CBG_FIBER_NARROW");
+    narrow = !(env && env[0] == '0');
+  }
+  HIPCHK(G->small.reserve(64));
+  int64_t* dsn = G->small.as<int64_t>();   // [0..1] sent flags, [2..3] received, [4] inexact count
+  if (narrow) {
+    HIPCHK(hipMemsetAsync(dsn + 4, 0, 8, cst));
+    if (Po.nnz) k_f32_inexact<<<(int)grid_for(Po.nnz, 256, kMaxGrid), 256, 0, cst>>>(
+        Po.nnz, (const double*)Po.val, (unsigned long long*)(dsn + 4));
+    int64_t nb = 0;
+    HIPCHK(hipMemcpyAsync(&nb, dsn + 4, 8, hipMemcpyDeviceToHost, cst));
+    HIPCHK(hipStreamSynchronize(cst));
+    narrow = nb == 0;
+  }
+  const int64_t kNarrowBit = 1LL << 62;
+  int64_t sflag[2] = {0, 0}, rflag[2] = {0, 0};
+  sflag[other] = Po.nnz | (narrow ? kNarrowBit : 0);
+  HIPCHK(hipMemcpyAsync(dsn, sflag, 16, hipMemcpyHostToDevice, cst));
+  const int64_t eight[2] = {8, 8};
+  CBGCHK(t_alltoallv(G, CBG_GROUP_FIBER, dsn, eight, dsn + 2, eight));
+  HIPCHK(hipMemcpyAsync(rflag, dsn + 2, 16, hipMemcpyDeviceToHost, cst));
+  HIPCHK(hipStreamSynchronize(cst));
+  const bool all_narrow = narrow && (rflag[other] & kNarrowBit);
+  const int64_t rnnz = rflag[other] & ~kNarrowBit;
+  // 3. receive storage (rows, then values; the counts behind them) and the exchange
+  const int64_t ir_bytes = (4 * rnnz + 15) & ~15LL;
+  HIPCHK(rx->ir.reserve(ir_bytes + vs * rnnz + 16));
+  HIPCHK(rx->val.reserve(8 * (myc + 1)));
+  char* rbase = rx->ir.as<char>();
+  int64_t* rcnt = rx->val.as<int64_t>();
+  const void* sval = Po.val;
+  void* rval = Po.val ? (void*)(rbase + ir_bytes) : nullptr;
+  const int64_t wire = all_narrow ? 4 : (int64_t)vs;
+  if (all_narrow) {
+    HIPCHK(s32.reserve(4 * (Po.nnz + 1)));
+    HIPCHK(r32.reserve(4 * (rnnz + 1)));
+    if (Po.nnz) k_f64_to_f32<<<(int)grid_for(Po.nnz, 256, kMaxGrid), 256, 0, cst>>>(Po.nnz, (const double*)Po.val,
+                                                                                   s32.as<float>());
+    HIPCHK(hipGetLastError());
+    sval = s32.p;
+    rval = r32.p;
+  }
+  const bool has_val = Po.val != nullptr;
+  const double t_setup = now_ms() - t0;
+  if (st) for (int m = 0; m < 2; ++m) if (m == other) st->fiber_bytes += (4 + (has_val ? wire : 0)) * Po.nnz + 8 * oc;
+  const bool async = G->rccl;
+  if (async) {
+    HIPCHK(hipEventRecord(G->ev_t[0], cst));   // counts and narrowed values are ready
+    HIPCHK(hipStreamWaitEvent(G->cs, G->ev_t[0], 0));
+    HIPCHK(hipEventRecord(G->ev_t[1], G->cs));
+    ncclComm_t f = G->comm[CBG_GROUP_FIBER];
+    NCCLCHK(ncclGroupStart());
+    if (oc) NCCLCHK(ncclSend(scnt.p, (size_t)(8 * oc), ncclInt8, other, f, G->cs));
+    if (myc) NCCLCHK(ncclRecv(rcnt, (size_t)(8 * myc), ncclInt8, other, f, G->cs));
+    if (Po.nnz) NCCLCHK(ncclSend(Po.ir, (size_t)(4 * Po.nnz), ncclInt8, other, f, G->cs));
+    if (rnnz) NCCLCHK(ncclRecv(rbase, (size_t)(4 * rnnz), ncclInt8, other, f, G->cs));
+    if (has_val && Po.nnz) NCCLCHK(ncclSend(sval, (size_t)(wire * Po.nnz), ncclInt8, other, f, G->cs));
+    if (has_val && rnnz) NCCLCHK(ncclRecv(rval, (size_t)(wire * rnnz), ncclInt8, other, f, G->cs));
+    NCCLCHK(ncclGroupEnd());
+    HIPCHK(hipEventRecord(G->ev_t[2], G->cs));
+  } else {   // caller transport: synchronous segments (member `other` only)
+    int64_t sb[2] = {0, 0}, rb[2] = {0, 0};
+    sb[other] = 8 * oc; rb[other] = 8 * myc;
+    CBGCHK(t_alltoallv(G, CBG_GROUP_FIBER, scnt.p, sb, rcnt, rb));
+    sb[other] = 4 * Po.nnz; rb[other] = 4 * rnnz;
+    CBGCHK(t_alltoallv(G, CBG_GROUP_FIBER, Po.ir, sb, rbase, rb));
+    if (has_val) {
+      sb[other] = wire * Po.nnz; rb[other] = wire * rnnz;
+      CBGCHK(t_alltoallv(G, CBG_GROUP_FIBER, sval, sb, rval, rb));
+    }
+  }
+  // 4. the own columns, while the exchange runs on the communication stream
+  t0 = now_ms();
+  cbg_csc_result Rm;
+  int64_t mm = 0;
+  CBGCHK(cbg_spgemm_local(ctx, &va, &vm, sr, dt, CBG_SORTED_COLS, &Rm, &mm));
+  Piece Pm = piece_of_result(Rm);
+  t_local += now_ms() - t0;
+  // 5. join, the received piece (colptr from its counts; f32 values widened), the merge in layer order
+  t0 = now_ms();
+  float xfer_ms = 0.f;
+  if (async) {
+    HIPCHK(hipStreamWaitEvent(cst, G->ev_t[2], 0));
+    HIPCHK(hipEventSynchronize(G->ev_t[2]));
+    (void)hipEventElapsedTime(&xfer_ms, G->ev_t[1], G->ev_t[2]);
+  }
+  if (all_narrow && has_val && rnnz)
+    k_f32_to_f64<<<(int)grid_for(rnnz, 256, kMaxGrid), 256, 0, cst>>>(rnnz, r32.as<float>(), (double*)(rbase + ir_bytes));
+  std::shared_ptr<Owner> co(new Owner(ctx->pool));
+  HIPCHK(co->cp.reserve(8 * (myc + 1)));
+  const int64_t ntiles = (myc + kScanTile - 1) / kScanTile;
+  HIPCHK(tiles.reserve(8 * (ntiles + 1)));
+  HIPCHK(scal.reserve(16));
+  if (myc > 0) {
+    k_scan_tiles<<<(int)ntiles, 256, 0, cst>>>(myc, rcnt, tiles.as<int64_t>());
+    k_scan_sums<<<1, 1024, 0, cst>>>(ntiles, tiles.as<int64_t>(), scal.as<int64_t>());
+    k_scan_apply<<<(int)ntiles, 256, 0, cst>>>(myc, rcnt, tiles.as<int64_t>(), co->cp.as<int64_t>());
+  } else {
+    HIPCHK(hipMemsetAsync(co->cp.p, 0, 8, cst));
+  }
+  HIPCHK(hipGetLastError());
+  Piece Pr;
+  Pr.nrow = Pm.nrow; Pr.ncol = myc; Pr.nnz = rnnz;
+  Pr.cp = co->cp.as<int64_t>();
+  Pr.ir = (const int32_t*)rbase;
+  Pr.val = has_val ? (const void*)(rbase + ir_bytes) : nullptr;
+  Pr.own = co;
+  Pr.keep = rx;
+  Po = Piece();   // the sent partial is no longer needed (the exchange has completed)
+  const double t_wait = now_ms() - t0;
+  t0 = now_ms();
+  std::vector<cbg_csc_result> two;
+  if (me == 0) two = {result_of(Pm, dt), result_of(Pr, dt)};
+  else two = {result_of(Pr, dt), result_of(Pm, dt)};
+  cbg_csc_result M;
+  CBGCHK(merge_parts(ctx, two, sr, dt, &M));
+  *out = piece_of_result(M);
+  out->reduced = true;
+  if (st) {
+    st->multiplies += mo + mm;
+    st->local_ms += t_local;
+    st->fiber_ms += t_setup + t_wait;   // exposed exchange time (the transfer itself overlaps the own product)
+    st->merge_ms += now_ms() - t0;
+    st->fiber_xfer_ms += xfer_ms;
+  }
+  return CBG_OK;
+}
+
 // hand a piece out as a library result (move its storage when it owns it alone, else copy)
 cbg_status hand_out(cbg_ctx* ctx, Piece& C, cbg_dtype dt, cbg_csc_result* out) {
   if (C.own && C.own.use_count() == 1 && !C.keep && C.cp == C.own->cp.as<int64_t>() &&
@@ -963,6 +1170,7 @@ cbg_status grid_common(cbg_ctx* ctx, int32_t world, int32_t rank, int32_t layers
     HIPCHK(hipEventCreateWithFlags(&G->ev_comm[i], hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&G->ev_used[i], hipEventDisableTiming));
   }
+  for (int i = 0; i < 4; ++i) HIPCHK(hipEventCreate(&G->ev_t[i]));   // fiber pipeline: fences + transfer timing
   *out = G;
   return CBG_OK;
 }
@@ -1022,6 +1230,8 @@ cbg_status cbg_grid_destroy(cbg_grid* G) {
     if (G->ev_comm[i]) (void)hipEventDestroy(G->ev_comm[i]);
     if (G->ev_used[i]) (void)hipEventDestroy(G->ev_used[i]);
   }
+  for (int i = 0; i < 4; ++i)
+    if (G->ev_t[i]) (void)hipEventDestroy(G->ev_t[i]);
   if (G->cs) (void)hipStreamDestroy(G->cs);
   delete G;
   return CBG_OK;
@@ -1097,8 +1307,16 @@ cbg_status cbg_spgemm_grid(cbg_grid* G, const cbg_dcsc_view* A, const cbg_dcsc_v
   // staged schedules, and so does Select2nd on L > 1 layers, whose fiber merge order is (stage, layer)
   const bool panels = !(flags & (CBG_HALVES | CBG_RUNNING_MERGE)) && !(sr == CBG_SR_SELECT2ND && G->L > 1) &&
                       std::getenv("CBG_GRID_STAGED") == nullptr;
-  CBGCHK(summa_layer_impl(G, A, B, sr, dt, flags | (panels ? kPanels : 0u), &ps, st));
-  CBGCHK(reduce_all_impl(G, ps, sr, dt, C, st));
+  // two layers, one product per layer (panels, or one stage): the fiber exchange overlaps the product
+  static const bool pipe_env = [] { const char* e = std::getenv("CBG_FIBER_PIPE"); return !(e && e[0] == '0'); }();
+  const bool pipe = pipe_env && G->L == 2 && !(flags & (CBG_HALVES | CBG_RUNNING_MERGE)) && sr != CBG_SR_SELECT2ND &&
+                    (panels || G->q == 1);
+  CBGCHK(summa_layer_impl(G, A, B, sr, dt, flags | (panels ? kPanels : 0u) | (pipe ? kFiberPipe : 0u), &ps, st));
+  if (ps.size() == 1 && ps[0].reduced) {   // the pipeline returned the reduced piece
+    CBGCHK(hand_out(G->ctx, ps[0], dt, C));
+  } else {
+    CBGCHK(reduce_all_impl(G, ps, sr, dt, C, st));
+  }
   if (st) st->total_ms = now_ms() - t0;
   return CBG_OK;
 }

@@ -423,8 +423,8 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
   // subwindow geometry of the row space (heavy-column units)
   // SUBW >= 2^13: k_sym_part's per-part subwindow counters assume it, and a single-subwindow unit
   // must fit k_num_heavy's dense table (2^CBG_HEAVY_LOGT rows)
-  static_assert(CBG_HEAVY_LOGT >= 13, "k_num_heavy table must cover a 2^13-row subwindow");
-  int32_t slog = 13;
+  static_assert(CBG_HEAVY_LOGT >= 12, "k_num_heavy table of at least 2^12 rows");
+  int32_t slog = kSubLogMin;
   while (((M - 1) >> slog) + 1 > kMaxSub) ++slog;
   const int32_t nsub = (int32_t)(((M - 1) >> slog) + 1);
 
@@ -656,7 +656,9 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
         HIPCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device));
         ctx->ncu = ncu > 0 ? ncu : 256;
       }
-      const int grid = (int)std::min<int64_t>(ctx->ncu, nitems * kItemUnits);
+      // persistent: as many workgroups as the LDS lets every CU hold (160 KB per CU)
+      const int per_cu = std::max<int>(1, (int)((160u << 10) / num_heavy_known_lds<SRT, V, CBG_KNOWN_LOGT, CBG_KNOWN_NT>()));
+      const int grid = (int)std::min<int64_t>((int64_t)ctx->ncu * per_cu, nitems * kItemUnits);
       e = launch_num_heavy_known<CBG_KNOWN_LOGT, CBG_KNOWN_NT, SRT, V>(st, grid, ctx->items.as<KnownUnit>(), sc + 12,
                                                                      A, B, spl, ou);
       if (e == hipSuccess)

@@ -97,6 +97,9 @@ constexpr int64_t kHeavy = 4096;   // nnz(C(:,j)) above which a column is split 
 #ifndef CBG_UNIT_CAP
 #define CBG_UNIT_CAP (3 << (CBG_HEAVY_LOGT - 2))   // rank mode holds up to T outputs; 3/4 T measured best
 #endif
+// smallest subwindow: 2^13 rows, or the heavy table's 2^CBG_HEAVY_LOGT when that is smaller (a one-subwindow unit
+// must fit k_num_heavy's dense table)
+constexpr int kSubLogMin = CBG_HEAVY_LOGT < 13 ? CBG_HEAVY_LOGT : 13;
 constexpr int64_t kUnitCap = CBG_UNIT_CAP;   // max outputs of a multi-subwindow unit (load <= kUnitCap/T)
 constexpr int kSplitMin = 16;      // A columns at least this long get split-table rows
 constexpr int kMaxSub = 2048;      // max subwindows per column (SUBW chosen so nrow/SUBW <= kMaxSub)
@@ -1016,7 +1019,7 @@ __global__ void k_part_items(const int32_t* __restrict__ list, int64_t count, in
 template <int NT>
 constexpr size_t sym_part_lds() {
   return (size_t)(1 << (kPartLog - 5)) * 4 + (size_t)NT * 21 + (size_t)(NT / kWave + 1) * 8 +
-         (size_t)((1 << (kPartLog - 13)) + 8) * 4 + 64;
+         (size_t)((1 << (kPartLog - kSubLogMin)) + 8) * 4 + 64;
 }
 
 template <int NT>
@@ -1027,14 +1030,14 @@ __global__ void __launch_bounds__(NT) k_sym_part(const PartItem* __restrict__ it
                                                  HeavyOut ho) {
   constexpr int T = 1 << (kPartLog - 5);   // bitmap words
   constexpr int WPT = T / NT;              // words per thread in the subwindow count (<= SUBW / 32)
-  static_assert(WPT * 32 <= (1 << 13), "a thread's words must lie in one subwindow");
+  static_assert(WPT * 32 <= (1 << kSubLogMin), "a thread's words must lie in one subwindow");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   int64_t* qb = (int64_t*)smem;                    // NT
   int64_t* off = qb + NT;                          // NT
   int64_t* scr = off + NT;                         // NT/64 + 1
   uint32_t* tab = (uint32_t*)(scr + NT / kWave + 1);// T
-  int32_t* scnt = (int32_t*)(tab + T);             // part subwindows (<= 2^(kPartLog-13))
-  int* misc = scnt + (1 << (kPartLog - 13));       // [0] total
+  int32_t* scnt = (int32_t*)(tab + T);             // part subwindows (<= 2^(kPartLog-kSubLogMin))
+  int* misc = scnt + (1 << (kPartLog - kSubLogMin));   // [0] total
   int32_t* lens = misc + 8;                        // NT
   uint8_t* bvs = (uint8_t*)(lens + NT);            // NT
   const SegBuf<uint8_t> sb{qb, off, bvs, scr, lens};

@@ -1059,7 +1059,8 @@ def _stats_update(stats, st):
     if stats is None:
         return
     stats["multiplies"] = stats.get("multiplies", 0) + int(st.multiplies)
-    for k in ("bcast_bytes", "fiber_bytes", "bcast_ms", "local_ms", "merge_ms", "fiber_ms", "total_ms"):
+    for k in ("bcast_bytes", "fiber_bytes", "bcast_ms", "local_ms", "merge_ms", "fiber_ms", "total_ms",
+              "fiber_xfer_ms"):
         stats[k] = stats.get(k, 0) + getattr(st, k)
     stats["stages"] = stats.get("stages", 0) + int(st.stages)
 

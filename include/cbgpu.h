@@ -301,6 +301,7 @@ typedef struct {
   int64_t multiplies;          /* this rank's local multiplies */
   int64_t bcast_bytes, fiber_bytes;
   double bcast_ms, local_ms, merge_ms, fiber_ms, total_ms;
+  double fiber_xfer_ms;        /* two layers: the fiber transfer on the communication stream (overlaps local_ms) */
   int32_t stages;
 } cbg_grid_stats;
 
