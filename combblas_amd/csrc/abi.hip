@@ -35,6 +35,7 @@ cbg_status cbg_init(int device, cbg_ctx** out) {
   c->own_stream = true;
   for (auto& e : c->ev)
     if (hipEventCreate(&e) != hipSuccess) { delete c; return CBG_EDEVICE; }
+  if (hipHostMalloc(&c->pin, kPinBytes, hipHostMallocDefault) != hipSuccess) { delete c; return CBG_EDEVICE; }
   *out = c;
   return CBG_OK;
 }
@@ -44,6 +45,7 @@ cbg_status cbg_destroy(cbg_ctx* c) {
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
   for (auto& e : c->ev) if (e) (void)hipEventDestroy(e);
+  if (c->pin) (void)hipHostFree(c->pin);
   if (c->own_stream) (void)hipStreamDestroy(c->stream);
   delete c;
   return CBG_OK;

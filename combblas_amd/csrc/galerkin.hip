@@ -242,9 +242,9 @@ __global__ void k_rap_compact(int64_t nagg, const int64_t* __restrict__ rcp, con
 
 // ---------------------------------------------------------------- the reference's RestrictionOp
 // MTRand (psort-1.0/include/psort/MersenneTwister.h:137-147, 179-196, 283-314) = MT19937 with init_genrand
-// seeding.  The state (624 words + read index) lives in HBM between launches; one 256-lane workgroup
-// draws the next *count values of the stream: each reload is the three data-parallel spans of the twist
-// ([0,227) reads old words, [227,454) and [454,623) read words the previous span rewrote) staged in LDS.
+// seeding.  The state (624 words + read index) lives in HBM between launches; one workgroup draws the next
+// *count values of the stream: each reload is the three data-parallel spans of the twist ([0,227) reads old
+// words, [227,454) and [454,624) read words the previous span rewrote) staged in LDS.
 constexpr int kMtN = 624;
 
 __global__ void k_mt_seed(uint32_t seed, uint32_t* __restrict__ st) {
@@ -269,40 +269,40 @@ __device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
   return y ^ (y >> 18);
 }
 
+// Two LDS copies of the state: a reload writes the new words into the other copy, so a span never
+// overwrites words it still reads -- three barriers per 624 draws (one per dependent span); tempering reads
+// the new copy while the next reload writes the old one.
 __global__ void __launch_bounds__(256) k_mt_draw(uint32_t* __restrict__ st, const int64_t* __restrict__ count,
                                                  uint32_t* __restrict__ out) {
-  __shared__ uint32_t s[kMtN];
+  __shared__ uint32_t buf[2][kMtN];
   const int t = threadIdx.x;
-  for (int i = t; i < kMtN; i += 256) s[i] = st[i];
+  int cur = 0;
+  for (int i = t; i < kMtN; i += 256) buf[0][i] = st[i];
   uint32_t idx = st[kMtN];
   const int64_t n = *count;
   __syncthreads();
   for (int64_t done = 0; done < n;) {
     if (idx == kMtN) {
-      uint32_t v = 0;
-      if (t < 227) v = mt_twist(s[t + 397], s[t], s[t + 1]);
+      const uint32_t* X = buf[cur];
+      uint32_t* Y = buf[cur ^ 1];
+      if (t < 227) Y[t] = mt_twist(X[t + 397], X[t], X[t + 1]);
       __syncthreads();
-      if (t < 227) s[t] = v;
+      if (t < 227) Y[t + 227] = mt_twist(Y[t], X[t + 227], X[t + 228]);
       __syncthreads();
-      if (t < 227) v = mt_twist(s[t], s[t + 227], s[t + 228]);
+      if (t < 169) Y[t + 454] = mt_twist(Y[t + 227], X[t + 454], X[t + 455]);
+      else if (t == 169) Y[623] = mt_twist(Y[396], X[623], Y[0]);
       __syncthreads();
-      if (t < 227) s[t + 227] = v;
-      __syncthreads();
-      if (t < 169) v = mt_twist(s[t + 227], s[t + 454], s[t + 455]);
-      __syncthreads();
-      if (t < 169) s[t + 454] = v;
-      __syncthreads();
-      if (t == 0) s[623] = mt_twist(s[396], s[623], s[0]);
-      __syncthreads();
+      cur ^= 1;
       idx = 0;
     }
+    const uint32_t* Y = buf[cur];
     const int64_t take = min<int64_t>(kMtN - idx, n - done);
-    for (int64_t k = t; k < take; k += 256) out[done + k] = mt_temper(s[idx + k]);
+    for (int64_t k = t; k < take; k += 256) out[done + k] = mt_temper(Y[idx + k]);
     idx += (uint32_t)take;
     done += take;
   }
   __syncthreads();
-  for (int i = t; i < kMtN; i += 256) st[i] = s[i];
+  for (int i = t; i < kMtN; i += 256) st[i] = buf[cur][i];
   if (t == 0) st[kMtN] = idx;
 }
 

@@ -148,9 +148,17 @@ struct cbg_ctx {
   DevBuf hrows, hmode, hpoff, urows;   // symbolic -> numeric row handoff of heavy columns
   DevBuf oitems;                       // heavy items the rows-known kernel does not take
   DevBuf gal[8];                       // fused Galerkin product scratch (galerkin.hip)
+  void* pin = nullptr;                 // 16 KB of pinned host memory: small read-backs (bin counts, scalars)
   int ncu = 0;                         // compute units (persistent grids)
   int row_handoff = -1;                // -1: read CBG_ROW_HANDOFF once (default on)
 };
+
+// pinned read-back slots (byte offsets into ctx->pin); a D2H copy into pageable memory goes through a staging
+// buffer and costs tens of microseconds per host sync on small products
+constexpr size_t kPinSymHist = 0, kPinScalars = 1024, kPinNumHist = 1280, kPinTotals = 2432, kPinErr = 2496,
+                 kPinMerge = 2624, kPinBytes = 16384;
+template <typename T>
+inline T* pinned(cbg_ctx* c, size_t off) { return (T*)((char*)c->pin + off); }
 
 inline hipError_t launch_cfg_lds(const void* fn, size_t lds) {
   if (lds > 64 * 1024) return hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -460,7 +468,7 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
   // 2. symbolic binning + kernels
   Classes cs;
   BinParams sbp{kSymWave, kSymBlock, 64, 1, kLaneMax};
-  unsigned long long hh[64];
+  unsigned long long* hh = pinned<unsigned long long>(ctx, kPinSymHist);   // 64 entries
   HIPCHK(hipMemsetAsync(hist, 0, sizeof(unsigned long long) * 64, st));
   bin_count(st, N, flop, span, nullptr, sbp, hist, list);
   HIPCHK(hipMemcpyAsync(hh, hist, sizeof(unsigned long long) * 32, hipMemcpyDeviceToHost, st));
@@ -559,7 +567,7 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
   k_scan_sums<<<1, 1024, 0, st>>>(ntiles, ctx->scan_tiles.as<int64_t>(), (int64_t*)(sc + 1));
   k_scan_apply<<<(int)ntiles, 256, 0, st>>>(N, nnz, ctx->scan_tiles.as<int64_t>(), colptr);
   HIPCHK(hipGetLastError());
-  unsigned long long hsc[4];
+  unsigned long long* hsc = pinned<unsigned long long>(ctx, kPinScalars);   // 4 entries
   HIPCHK(hipMemcpyAsync(hsc, sc, 32, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
   HIPCHK(hipEventRecord(ctx->ev[4], st));
@@ -617,9 +625,11 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
   BinParams nbp{kNumWave, kNumBlock, 64, 0, kLaneMax};
   HIPCHK(hipMemsetAsync(hist, 0, sizeof(unsigned long long) * 128, st));
   bin_count(st, N, nnz, span, flop, nbp, hist, list);
-  unsigned long long hn[128], tots[2] = {0, 0};
+  unsigned long long* hn = pinned<unsigned long long>(ctx, kPinNumHist);    // 128 entries
+  unsigned long long* tots = pinned<unsigned long long>(ctx, kPinTotals);   // 2 entries
+  tots[0] = tots[1] = 0;
   HIPCHK(hipMemcpyAsync(hn, hist, sizeof(unsigned long long) * 128, hipMemcpyDeviceToHost, st));
-  if (H > 0) HIPCHK(hipMemcpyAsync(tots, sc + 8, sizeof(tots), hipMemcpyDeviceToHost, st));
+  if (H > 0) HIPCHK(hipMemcpyAsync(tots, sc + 8, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
   const int64_t segtot = (int64_t)tots[0], nitems = (int64_t)tots[1];
   if (H > 0) {
@@ -687,9 +697,10 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
     HIPCHK(hipGetLastError());
   }
   HIPCHK(hipEventRecord(ctx->ev[5], st));
-  int herr[8];
-  unsigned long long hknown = 0;
-  HIPCHK(hipMemcpyAsync(herr, si, sizeof(herr), hipMemcpyDeviceToHost, st));
+  int* herr = pinned<int>(ctx, kPinErr);   // 8 ints, then the rows-known unit count
+  unsigned long long& hknown = *pinned<unsigned long long>(ctx, kPinErr + 32);
+  hknown = 0;
+  HIPCHK(hipMemcpyAsync(herr, si, 8 * sizeof(int), hipMemcpyDeviceToHost, st));
   if (H > 0) HIPCHK(hipMemcpyAsync(&hknown, sc + 12, sizeof(hknown), hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
   float t;
@@ -913,7 +924,7 @@ cbg_status merge2_sr(cbg_ctx* ctx, const cbg_csc_result* parts, cbg_csc_result* 
     HIPCHK(hipMemsetAsync(own->cp.p, 0, 8, st));
   }
   HIPCHK(hipGetLastError());
-  unsigned long long h[3] = {0, 0, 0};   // duplicate pairs, nnz(C), columns out of row order
+  unsigned long long* h = pinned<unsigned long long>(ctx, kPinMerge);   // duplicate pairs, nnz(C), columns out of order
   HIPCHK(hipMemcpyAsync(h, sc, 24, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
   if (h[2]) return CBG_EINVAL;   // a partial is not row-sorted: the caller takes the hash merge

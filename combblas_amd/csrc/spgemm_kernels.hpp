@@ -391,6 +391,7 @@ __global__ void __launch_bounds__(256) k_bin(int64_t n, const int64_t* __restric
 // into a private LDS slice, counts (symbolic) or accumulates, sorts and writes (numeric).  A wave
 // per such column spent its time on table set-up and scans for a handful of multiplies.
 constexpr int kLaneStride = kLaneMax + 1;   // odd stride: the 64 lanes' slices start in distinct banks
+constexpr int kLaneBatch = 8;               // B nonzeros whose loads a lane issues together
 
 __global__ void __launch_bounds__(256) k_sym_lane(const int32_t* __restrict__ list, int64_t count,
                                                   const int64_t* __restrict__ Acp, const int32_t* __restrict__ Air,
@@ -401,11 +402,27 @@ __global__ void __launch_bounds__(256) k_sym_lane(const int32_t* __restrict__ li
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < count; i += (int64_t)gridDim.x * blockDim.x) {
     const int32_t j = list[i];
     int m = 0;
-    const int64_t be = Bcp[j + 1];
-    for (int64_t b = Bcp[j]; b < be; ++b) {
-      const int32_t k = Bir[b];
-      const int64_t a1 = Acp[k + 1];
-      for (int64_t q = Acp[k]; q < a1 && m < kLaneMax; ++q) rows[m++] = Air[q];
+    const int64_t bs = Bcp[j], be = Bcp[j + 1];
+    for (int64_t b0 = bs; b0 < be; b0 += kLaneBatch) {   // batched independent loads, as k_num_lane
+      int32_t k[kLaneBatch];
+      int64_t a0[kLaneBatch], a1[kLaneBatch];
+      int32_t r0[kLaneBatch];
+#pragma unroll
+      for (int t = 0; t < kLaneBatch; ++t) k[t] = b0 + t < be ? Bir[b0 + t] : 0;
+#pragma unroll
+      for (int t = 0; t < kLaneBatch; ++t) {
+        const bool ok = b0 + t < be;
+        a0[t] = ok ? Acp[k[t]] : 0;
+        a1[t] = ok ? Acp[k[t] + 1] : 0;
+      }
+#pragma unroll
+      for (int t = 0; t < kLaneBatch; ++t) r0[t] = a1[t] > a0[t] ? Air[a0[t]] : 0;
+#pragma unroll
+      for (int t = 0; t < kLaneBatch; ++t) {
+        if (a1[t] <= a0[t] || m >= kLaneMax) continue;
+        rows[m++] = r0[t];
+        for (int64_t q = a0[t] + 1; q < a1[t] && m < kLaneMax; ++q) rows[m++] = Air[q];
+      }
     }
     int d = 0;   // an entry counts when no earlier entry has its row
     for (int x = 0; x < m; ++x) {
@@ -1458,26 +1475,49 @@ __global__ void __launch_bounds__(256) k_num_lane(const int32_t* __restrict__ li
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < count; i += (int64_t)gridDim.x * blockDim.x) {
     const int32_t j = list[i];
     int m = 0;
-    const int64_t be = B.cp[j + 1];
-    // (B nonzero, A entry) in storage order: the first contributor of a row is the first inserted
-    for (int64_t b = B.cp[j]; b < be; ++b) {
-      const int32_t k = B.ir[b];
-      const V bv = load_val(B.val, b);
-      const int64_t a1 = A.cp[k + 1];
-      for (int64_t q = A.cp[k]; q < a1; ++q) {
-        const int32_t r = A.ir[q];
-        const Acc x = SRT::mul(load_val(A.val, q), bv, q, b);
-        int y = 0;
-        while (y < m && rows[y] != r) ++y;
-        if (y == m) {
-          if (m == kLaneMax) continue;   // cannot happen: flop <= kLaneMax
-          rows[m] = r;
-          accs[m] = SRT::identity();
-          ++m;
-        } else if (SRT::kAddIsError) {
-          aerr = true;
-        }
-        SRT::acc(&accs[y], x);
+    const int64_t bs = B.cp[j], be = B.cp[j + 1];
+    auto insert = [&](int32_t r, const Acc& x) {
+      int y = 0;
+      while (y < m && rows[y] != r) ++y;
+      if (y == m) {
+        if (m == kLaneMax) return;   // cannot happen: flop <= kLaneMax
+        rows[m] = r;
+        accs[m] = SRT::identity();
+        ++m;
+      } else if (SRT::kAddIsError) {
+        aerr = true;
+      }
+      SRT::acc(&accs[y], x);
+    };
+    // (B nonzero, A entry) in storage order: the first contributor of a row is the first inserted.  The B
+    // nonzeros go kLaneBatch at a time: their rows, A ranges and the first A entry of every range are loaded
+    // with independent loads before the inserts (a serial B -> A.cp -> A.ir chain per nonzero otherwise)
+    for (int64_t b0 = bs; b0 < be; b0 += kLaneBatch) {
+      int32_t k[kLaneBatch];
+      int64_t a0[kLaneBatch], a1[kLaneBatch];
+      int32_t r0[kLaneBatch];
+      V av0[kLaneBatch], bv[kLaneBatch];
+#pragma unroll
+      for (int t = 0; t < kLaneBatch; ++t) k[t] = b0 + t < be ? B.ir[b0 + t] : 0;
+#pragma unroll
+      for (int t = 0; t < kLaneBatch; ++t) {
+        const bool ok = b0 + t < be;
+        a0[t] = ok ? A.cp[k[t]] : 0;
+        a1[t] = ok ? A.cp[k[t] + 1] : 0;
+        bv[t] = ok ? load_val(B.val, b0 + t) : V(0);
+      }
+#pragma unroll
+      for (int t = 0; t < kLaneBatch; ++t) {
+        const bool ok = a1[t] > a0[t];
+        r0[t] = ok ? A.ir[a0[t]] : 0;
+        av0[t] = ok ? load_val(A.val, a0[t]) : V(0);
+      }
+#pragma unroll
+      for (int t = 0; t < kLaneBatch; ++t) {
+        if (a1[t] <= a0[t]) continue;
+        const int64_t b = b0 + t;
+        insert(r0[t], SRT::mul(av0[t], bv[t], a0[t], b));
+        for (int64_t q = a0[t] + 1; q < a1[t]; ++q) insert(A.ir[q], SRT::mul(load_val(A.val, q), bv[t], q, b));
       }
     }
     for (int x = 1; x < m; ++x) {   // insertion sort by row (m <= kLaneMax)
