@@ -147,6 +147,7 @@ struct cbg_ctx {
   DevBuf nunits, segsz, segoff, useg, icnt, itemoff, items, parts, wide_win;
   DevBuf hrows, hmode, hpoff, urows;   // symbolic -> numeric row handoff of heavy columns
   DevBuf oitems;                       // heavy items the rows-known kernel does not take
+  DevBuf aos;                          // A's rows and values interleaved (k_num_heavy_known gathers)
   DevBuf gal[8];                       // fused Galerkin product scratch (galerkin.hip)
   void* pin = nullptr;                 // 16 KB of pinned host memory: small read-backs (bin counts, scalars)
   int ncu = 0;                         // compute units (persistent grids)
@@ -335,10 +336,15 @@ hipError_t launch_num_heavy(hipStream_t st, int grid, const HeavyItem* items, co
 }
 template <int LOGT, int NT, class SRT, typename V>
 hipError_t launch_num_heavy_known(hipStream_t st, int grid, const KnownUnit* ku, const unsigned long long* nku,
-                                  const DevCsc<V>& A, const DevCsc<V>& B, const Split& spl, const NumOut<V>& o) {
+                                  const DevCsc<V>& A, const DevCsc<V>& B, const Split& spl, const NumOut<V>& o,
+                                  const RowVal<V>* arv = nullptr) {
   if (grid <= 0) return hipSuccess;
   const size_t lds = num_heavy_known_lds<SRT, V, LOGT, NT>();
-  if (A.val) {
+  if (A.val && arv) {
+    hipError_t e = launch_cfg_lds((const void*)k_num_heavy_known<SRT, V, LOGT, NT, true, true>, lds);
+    if (e != hipSuccess) return e;
+    k_num_heavy_known<SRT, V, LOGT, NT, true, true><<<grid, NT, lds, st>>>(ku, nku, A, B, spl, o, arv);
+  } else if (A.val) {
     hipError_t e = launch_cfg_lds((const void*)k_num_heavy_known<SRT, V, LOGT, NT, true>, lds);
     if (e != hipSuccess) return e;
     k_num_heavy_known<SRT, V, LOGT, NT, true><<<grid, NT, lds, st>>>(ku, nku, A, B, spl, o);
@@ -669,8 +675,23 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
       // persistent: as many workgroups as the LDS lets every CU hold (160 KB per CU)
       const int per_cu = std::max<int>(1, (int)((160u << 10) / num_heavy_known_lds<SRT, V, CBG_KNOWN_LOGT, CBG_KNOWN_NT>()));
       const int grid = (int)std::min<int64_t>((int64_t)ctx->ncu * per_cu, nitems * kItemUnits);
+      // CBG_AOS=1: A's rows and values interleaved for the rows-known kernel's gathers (one 16-byte load per
+      // multiply).  Off by default: measured slower at s20 (heavy 34.3 vs 32.8 ms) and even at s21 (108.1 vs
+      // 107.1 ms) -- the extra 4 bytes per gathered entry cost more than the halved load count saves
+      const RowVal<V>* arv = nullptr;
+      static const bool aos_env = [] { const char* x = std::getenv("CBG_AOS"); return x && x[0] == '1'; }();
+      if (aos_env && A.val && sizeof(V) >= 4 && e == hipSuccess) {
+        const size_t need = sizeof(RowVal<V>) * (size_t)(A.nnz + 1);
+        size_t fr = 0, tot = 0;
+        if (need <= ctx->aos.n || (hipMemGetInfo(&fr, &tot) == hipSuccess && need < fr / 4)) {
+          HIPCHK(ctx->aos.reserve(need));
+          k_pack_rowval<V><<<(int)grid_for(A.nnz, 256, kMaxGrid * 4), 256, 0, st>>>(A.nnz, A.ir, A.val,
+                                                                                   ctx->aos.as<RowVal<V>>());
+          arv = ctx->aos.as<RowVal<V>>();
+        }
+      }
       e = launch_num_heavy_known<CBG_KNOWN_LOGT, CBG_KNOWN_NT, SRT, V>(st, grid, ctx->items.as<KnownUnit>(), sc + 12,
-                                                                     A, B, spl, ou);
+                                                                     A, B, spl, ou, arv);
       if (e == hipSuccess)
         e = launch_num_heavy<CBG_HEAVY_LOGT, CBG_HEAVY_NT, SRT, V>(st, grid, ctx->oitems.as<HeavyItem>(), sc + 13,
                                                                  ctx->heavy_cols.as<int32_t>(), units, nsub, A, B, span,

@@ -2226,10 +2226,29 @@ __device__ __forceinline__ int64_t known_row_src(const KnownUnit& H, int i) {
 #define CBG_GROUP_KNOWN 2
 #endif
 
-template <class SRT, typename V, int LOGT, int NT, bool AV>
+// A's (row, value) pairs interleaved for the heavy gathers: one 16-byte (8-byte for 4-byte values) load per
+// multiply instead of a row load and a value load
+template <typename V> struct alignas(sizeof(V) == 8 ? 16 : 8) RowVal {
+  int32_t r;
+  int32_t pad_[sizeof(V) == 8 ? 1 : 0];
+  V v;
+};
+template <typename V>
+__global__ void k_pack_rowval(int64_t nnz, const int32_t* __restrict__ ir, const V* __restrict__ val,
+                              RowVal<V>* __restrict__ out) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nnz; i += (int64_t)gridDim.x * blockDim.x) {
+    RowVal<V> e;
+    e.r = ir[i];
+    e.v = val[i];
+    out[i] = e;
+  }
+}
+
+template <class SRT, typename V, int LOGT, int NT, bool AV, bool AOS = false>
 __global__ void __launch_bounds__(NT) k_num_heavy_known(const KnownUnit* __restrict__ ku,
                                                         const unsigned long long* __restrict__ nku, DevCsc<V> A,
-                                                        DevCsc<V> B, Split spl, NumOut<V> out) {
+                                                        DevCsc<V> B, Split spl, NumOut<V> out,
+                                                        const RowVal<V>* __restrict__ arv = nullptr) {
   using Acc = typename SRT::Acc;
   constexpr int T = 1 << LOGT;
   constexpr int RPT = known_rpt<NT>();   // rows per thread (cnt <= RPT*NT)
@@ -2349,7 +2368,25 @@ __global__ void __launch_bounds__(NT) k_num_heavy_known(const KnownUnit* __restr
       STAMP(3);
       expand_staged_slots<NT, CBG_UNROLL_KNOWN, CBG_GROUP_KNOWN, V>(
           sb, tid, F, H.bs + c, (int)min<int64_t>(NT, H.nb - c),
-          [&](int64_t q) { return NumItem<V>{A.ir[q], AV ? A.val[q] : V(1)}; },   // AV: no pointer test per load
+          [&](int64_t q) {   // AV: no pointer test per load; AOS: one load for the row and the value
+            if constexpr (AOS && sizeof(V) == 8) {   // one dwordx4: (row, pad, value)
+              typedef int v4i __attribute__((ext_vector_type(4)));
+              const v4i w = *(const v4i*)(arv + q);
+              const long long b = ((long long)(unsigned)w.w << 32) | (unsigned)w.z;
+              V v;
+              __builtin_memcpy(&v, &b, 8);
+              return NumItem<V>{w.x, v};
+            } else if constexpr (AOS) {              // one dwordx2: (row, value)
+              typedef int v2i __attribute__((ext_vector_type(2)));
+              const v2i w = *(const v2i*)(arv + q);
+              const int wy = w.y;
+              V v;
+              __builtin_memcpy(&v, &wy, sizeof(V) < 4 ? sizeof(V) : 4);
+              return NumItem<V>{w.x, v};
+            } else {
+              return NumItem<V>{A.ir[q], AV ? A.val[q] : V(1)};
+            }
+          },
           [&](const NumItem<V>& it) -> int {
             const uint32_t o = (uint32_t)(it.r - lo);
             const bool ok = o <= (uint32_t)(hi - lo);
