@@ -1001,6 +1001,9 @@ __global__ void __launch_bounds__(NT) k_sym_block(const int32_t* __restrict__ li
 #endif
 constexpr int kPartLog = CBG_PART_LOG;
 constexpr int kPartNT = CBG_PART_NT;
+#ifndef CBG_SYM_SHORT_SEARCH
+#define CBG_SYM_SHORT_SEARCH 1   // k_sym_part narrows a short A column to the part's rows by binary search
+#endif
 #ifndef CBG_SYM_ROWS_WAVE
 #define CBG_SYM_ROWS_WAVE 0   // 1: k_sym_part emits its rows word-major per wave (measured slower, r03d)
 #endif
@@ -1080,6 +1083,9 @@ __global__ void __launch_bounds__(NT) k_sym_part(const PartItem* __restrict__ it
         const int32_t* t = spl.tab + (int64_t)spl.idx[k] * (spl.nsub + 1);
         a0 = c0 + t[s0];
         a1 = c0 + t[s1];
+      } else if (CBG_SYM_SHORT_SEARCH) {   // short column: its rows inside the part by binary search
+        a0 = lower_bound_rows(Air, c0, c1, r0);
+        a1 = lower_bound_rows(Air, a0, c1, (int64_t)r0 + (1 << kPartLog));
       } else {
         a0 = c0;
         a1 = c1;
@@ -1420,11 +1426,20 @@ __global__ void __launch_bounds__(256) k_unit_segs(const int32_t* __restrict__ c
         out[(int64_t)u * nb] = UnitSeg{c0 + t[un.s0], c0 + t[un.s1]};
       }
     } else {
+      // a short column (rows ascend, fewer than kSplitMin): its entries inside the unit's rows by binary search,
+      // so the numeric sweep gathers only the unit's own multiplies
       const int32_t rf = c1 > c0 ? Air[c0] : 0, rl = c1 > c0 ? Air[c1 - 1] : -1;
       for (int u = 0; u < nu; ++u) {
         const Unit un = U[u];
-        const bool hit = c1 > c0 && rl >= ((int64_t)un.s0 << sp.log) && rf < ((int64_t)un.s1 << sp.log);
-        out[(int64_t)u * nb] = hit ? UnitSeg{c0, c1} : UnitSeg{c0, c0};
+        const int64_t lo = (int64_t)un.s0 << sp.log, hi = (int64_t)un.s1 << sp.log;
+        const bool hit = c1 > c0 && rl >= lo && rf < hi;
+        if (!hit) {
+          out[(int64_t)u * nb] = UnitSeg{c0, c0};
+        } else {
+          const int64_t a0 = rf >= lo ? c0 : lower_bound_rows(Air, c0, c1, lo);
+          const int64_t a1 = rl < hi ? c1 : lower_bound_rows(Air, a0, c1, hi);
+          out[(int64_t)u * nb] = UnitSeg{a0, a1};
+        }
       }
     }
   }

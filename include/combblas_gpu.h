@@ -15,7 +15,8 @@
  *   combblas::gpu::Mult_AnXBn_SUMMA3D<SR, NUO, UDERO>(A3D, B3D)          ParFriends.h:2918-3208
  *   combblas::gpu::multiply(splitA, splitB, CMG, isBT, threaded)           3DSpGEMM/Multiplier.h:10-61
  *   combblas::gpu::SUMMALayer(splitA, splitB, C, CMG, isBT, threaded)      3DSpGEMM/SUMMALayer.h:24-97
- *     (the 3DSpGEMM pair is declared when 3DSpGEMM/CCGrid.h is included before this header)
+ *   combblas::gpu::RestrictionOp(CMG, localmat, R, RT)                    3DSpGEMM/RestrictionOp.h:196-291
+ *     (the 3DSpGEMM ones are declared when 3DSpGEMM/CCGrid.h is included before this header)
  *
  * The distributed ones run the whole SUMMA (stage broadcasts, local products, merges, fiber
  * exchange) inside libcbgpu on the device (cbg_spgemm_grid) over the SpParMat's own MPI
@@ -495,6 +496,106 @@ SpDCCols<IT, NT>* multiply(SpDCCols<IT, NT>& splitA, SpDCCols<IT, NT>& splitB, C
   SpDCCols<IT, NT>* D = new SpDCCols<IT, NT>(*t, false);
   delete t;
   return D;
+}
+
+// RestrictionOp (3DSpGEMM/RestrictionOp.h:196-291): layer 0 builds R and R^T of the layer's matrix.  The layer's
+// pieces are gathered on its rank 0, the device computes the reference's ONE-rank R there (cbg_restriction_op:
+// MIS2 on the MTRand stream, Select2ndRandSR, RandPerm; the reference's DETERMINISTIC seeds by default) and every
+// rank of layer 0 receives its block of R (n x nagg) and R^T in the SpParMat block distribution of the layer grid
+// (RestrictionOp.h:287-288 keep Rop.seq()).  The reference's own R depends on its rank count (each rank draws its
+// part of the stream), so at one rank per layer the two are equal entry for entry; on a q x q layer this returns
+// the one-rank R.  Values are 1.
+template <typename IT, typename NT>
+void RestrictionOp(CCGrid& CMG, SpDCCols<IT, NT>* localmat, SpDCCols<IT, NT>*& R, SpDCCols<IT, NT>*& RT,
+                   uint32_t mt_seed = 1, uint32_t perm_seed = 1383098845) {
+  if (CMG.layer_grid != 0) return;
+  MPI_Comm lw = CMG.layerWorld;
+  int lr = 0, ls = 1;
+  MPI_Comm_rank(lw, &lr);
+  MPI_Comm_size(lw, &ls);
+  const int q = CMG.GridCols, bi = lr / q, bj = lr % q;
+  // the layer matrix's size and this piece's offsets (colWorld orders the grid column by row, rowWorld the grid
+  // row by column)
+  int64_t m = localmat->getnrow(), n = localmat->getncol(), M = 0, N = 0, roff = 0, coff = 0;
+  MPI_Allreduce(&m, &M, 1, MPI_INT64_T, MPI_SUM, CMG.colWorld);
+  MPI_Allreduce(&n, &N, 1, MPI_INT64_T, MPI_SUM, CMG.rowWorld);
+  MPI_Exscan(&m, &roff, 1, MPI_INT64_T, MPI_SUM, CMG.colWorld);
+  MPI_Exscan(&n, &coff, 1, MPI_INT64_T, MPI_SUM, CMG.rowWorld);
+  if (bi == 0) roff = 0;
+  if (bj == 0) coff = 0;
+  if (M != N) throw std::runtime_error("RestrictionOp: square matrix required (3002)");
+  // the pattern's global (row, col) pairs on the layer's rank 0
+  std::vector<int64_t> mine;
+  {
+    SpTuples<IT, NT> T(*localmat);
+    mine.resize(2 * (size_t)T.getnnz());
+    for (int64_t k = 0; k < T.getnnz(); ++k) {
+      mine[2 * k] = (int64_t)T.rowindex(k) + roff;
+      mine[2 * k + 1] = (int64_t)T.colindex(k) + coff;
+    }
+  }
+  int cnt = (int)mine.size();
+  std::vector<int> cnts(ls), displs(ls + 1, 0);
+  MPI_Gather(&cnt, 1, MPI_INT, cnts.data(), 1, MPI_INT, 0, lw);
+  for (int r = 0; r < ls; ++r) displs[r + 1] = displs[r] + cnts[r];
+  std::vector<int64_t> all(lr == 0 ? (size_t)displs[ls] : 0);
+  MPI_Gatherv(mine.data(), cnt, MPI_INT64_T, all.data(), cnts.data(), displs.data(), MPI_INT64_T, 0, lw);
+  int64_t nagg = 0;
+  std::vector<int64_t> agg;   // aggregate (column of R) of every vertex, on rank 0
+  if (lr == 0) {
+    const int64_t nnz = (int64_t)all.size() / 2;
+    std::vector<int64_t> cp((size_t)N + 1, 0);
+    for (int64_t k = 0; k < nnz; ++k) cp[(size_t)all[2 * k + 1] + 1]++;
+    for (int64_t c = 0; c < N; ++c) cp[(size_t)c + 1] += cp[(size_t)c];
+    std::vector<int32_t> ir((size_t)nnz + 1);
+    std::vector<int64_t> cur(cp.begin(), cp.end() - 1);
+    for (int64_t k = 0; k < nnz; ++k) ir[(size_t)cur[(size_t)all[2 * k + 1]]++] = (int32_t)all[2 * k];
+    for (int64_t c = 0; c < N; ++c) std::sort(ir.begin() + cp[(size_t)c], ir.begin() + cp[(size_t)c + 1]);
+    cbg_dcsc_view v{};
+    v.nrow = M; v.ncol = N; v.nnz = nnz; v.nzc = N;
+    v.cp = cp.data(); v.jc = nullptr; v.ir = ir.data(); v.idx_bytes = 4; v.ptr_bytes = 8;
+    v.val = nullptr; v.val_type = CBG_F64; v.on_device = 0;
+    cbg_csc_result Rd{}, RTd{};
+    check(cbg_restriction_op(context(), &v, mt_seed, perm_seed, &Rd, &RTd, &nagg), "cbg_restriction_op");
+    // R^T has one entry per column: its rows are the aggregates of the vertices
+    std::vector<int64_t> tcp((size_t)M + 1);
+    std::vector<int32_t> trow((size_t)M + 1);
+    std::vector<double> tval((size_t)M + 1);
+    check(cbg_result_to_host(context(), &RTd, tcp.data(), trow.data(), tval.data()), "cbg_result_to_host");
+    cbg_result_free(context(), &Rd);
+    cbg_result_free(context(), &RTd);
+    agg.assign(trow.begin(), trow.begin() + M);
+  }
+  MPI_Bcast(&nagg, 1, MPI_INT64_T, 0, lw);
+  agg.resize((size_t)M);
+  MPI_Bcast(agg.data(), (int)M, MPI_INT64_T, 0, lw);
+  // blocks of the SpParMat distribution on the q x q layer grid: n / q per block, the last takes the remainder
+  auto blk = [q](int64_t len, int b, int64_t* lo, int64_t* hi) {
+    *lo = (len / q) * b;
+    *hi = b == q - 1 ? len : (len / q) * (b + 1);
+  };
+  int64_t r0, r1, c0, c1;
+  blk(M, bi, &r0, &r1);      // R: rows = vertices, cols = aggregates
+  blk(nagg, bj, &c0, &c1);
+  std::vector<std::tuple<IT, IT, NT>> tr, tt;
+  for (int64_t v = r0; v < r1; ++v)
+    if (agg[(size_t)v] >= c0 && agg[(size_t)v] < c1)
+      tr.emplace_back((IT)(v - r0), (IT)(agg[(size_t)v] - c0), (NT)1);
+  int64_t t0, t1, u0, u1;
+  blk(nagg, bi, &t0, &t1);   // R^T: rows = aggregates, cols = vertices
+  blk(M, bj, &u0, &u1);
+  for (int64_t v = u0; v < u1; ++v)
+    if (agg[(size_t)v] >= t0 && agg[(size_t)v] < t1)
+      tt.emplace_back((IT)(agg[(size_t)v] - t0), (IT)(v - u0), (NT)1);
+  auto build = [](std::vector<std::tuple<IT, IT, NT>>& t, int64_t nr, int64_t nc) {
+    std::tuple<IT, IT, NT>* a = new std::tuple<IT, IT, NT>[t.size() > 0 ? t.size() : 1];
+    std::copy(t.begin(), t.end(), a);
+    SpTuples<IT, NT> T((IT)t.size(), (IT)nr, (IT)nc, a, false, false);
+    T.SortColBased();
+    return new SpDCCols<IT, NT>(T, false);
+  };
+  R = build(tr, r1 - r0, c1 - c0);
+  RT = build(tt, t1 - t0, u1 - u0);
 }
 #endif  // _CC_GRID_
 

@@ -13,6 +13,7 @@
 // Exit 0 = all equal (or, with --expect-no-gpu, the device path threw a device error).
 //
 // 3D mode (mpirun -np q*q*L):  dropin_test --3d <q> <L> <A.mtx> <C.mtx> <G.mtx>
+// restriction (mpirun -np q*q): dropin_test --restrict <q> <A.mtx> <agg.txt>
 //   * the split-3D driver of 3DSpGEMM exactly as test_mpipspgemm.cpp:101-153 sets it up (CCGrid, ReadMat
 //     unpermuted, SplitMat): gpu::multiply (column and outer/isBT modes) and gpu::SUMMALayer against the
 //     reference's multiply / SUMMALayer on the same split pieces, and against controlC (C.mtx = MATLAB A*A);
@@ -234,8 +235,79 @@ int run3d(int q, int L, const std::string& fa, const std::string& fc, const std:
   return any;
 }
 
+// gpu::RestrictionOp (3DSpGEMM/RestrictionOp.h:196-291) on a q x q layer: every rank's R and R^T blocks against the
+// reference's one-rank R (aggregate of every vertex, from oracle/_ref/refrestrict via tests/golden/restriction.npz)
+int run_restrict(int q, const std::string& fa, const std::string& fagg) {
+  int rc = 0;
+  typedef SpDCCols<I, double> DCC;
+  CCGrid CMG(1, q);
+  std::shared_ptr<CommGrid> lg(new CommGrid(CMG.layerWorld, 0, 0));
+  SpParMat<I, double, DCC> A(lg);
+  A.ParallelReadMM(fa, true, maximum<double>());
+  DCC* local = new DCC(*A.seqptr());
+  DCC *R = nullptr, *RT = nullptr;
+  gpu::RestrictionOp(CMG, local, R, RT);
+  std::vector<int64_t> agg;
+  {
+    FILE* f = fopen(fagg.c_str(), "r");
+    long long x;
+    while (f && fscanf(f, "%lld", &x) == 1) agg.push_back(x);
+    if (f) fclose(f);
+  }
+  const int64_t M = (int64_t)agg.size(), nagg = agg.empty() ? 0 : *std::max_element(agg.begin(), agg.end()) + 1;
+  int lr = 0;
+  MPI_Comm_rank(CMG.layerWorld, &lr);
+  const int bi = lr / q, bj = lr % q;
+  auto blk = [q](int64_t len, int b, int64_t* lo, int64_t* hi) {
+    *lo = (len / q) * b;
+    *hi = b == q - 1 ? len : (len / q) * (b + 1);
+  };
+  int64_t r0, r1, c0, c1, t0, t1, u0, u1;
+  blk(M, bi, &r0, &r1);
+  blk(nagg, bj, &c0, &c1);
+  blk(nagg, bi, &t0, &t1);
+  blk(M, bj, &u0, &u1);
+  if (R->getnrow() != r1 - r0 || R->getncol() != c1 - c0 || RT->getnrow() != t1 - t0 || RT->getncol() != u1 - u0) {
+    printf("restrict: block shapes differ\n");
+    rc = 1;
+  }
+  int64_t want_r = 0, want_t = 0;
+  for (int64_t v = r0; v < r1; ++v) want_r += agg[(size_t)v] >= c0 && agg[(size_t)v] < c1;
+  for (int64_t v = u0; v < u1; ++v) want_t += agg[(size_t)v] >= t0 && agg[(size_t)v] < t1;
+  SpTuples<I, double> TR(*R), TT(*RT);
+  int64_t off = 0;
+  for (int64_t k = 0; k < TR.getnnz(); ++k)
+    off += agg[(size_t)(TR.rowindex(k) + r0)] != TR.colindex(k) + c0 || TR.numvalue(k) != 1.0;
+  for (int64_t k = 0; k < TT.getnnz(); ++k) off += agg[(size_t)(TT.colindex(k) + u0)] != TT.rowindex(k) + t0;
+  if (off || TR.getnnz() != want_r || TT.getnnz() != want_t) {
+    printf("restrict: rank %d: %lld entries off, nnz R %lld (want %lld), R^T %lld (want %lld)\n", lr, (long long)off,
+           (long long)TR.getnnz(), (long long)want_r, (long long)TT.getnnz(), (long long)want_t);
+    rc = 1;
+  } else {
+    printf("gpu::RestrictionOp rank %d: R block %lld entries, R^T block %lld, equal to the reference's R\n", lr,
+           (long long)TR.getnnz(), (long long)TT.getnnz());
+  }
+  delete R;
+  delete RT;
+  delete local;
+  int any = 0;
+  MPI_Allreduce(&rc, &any, 1, MPI_INT, MPI_MAX, MPI_COMM_WORLD);
+  return any;
+}
+
 int main(int argc, char** argv) {
   MPI_Init(&argc, &argv);
+  if (argc == 5 && std::string(argv[1]) == "--restrict") {
+    int rc = 1;
+    try {
+      rc = run_restrict(atoi(argv[2]), argv[3], argv[4]);
+    } catch (std::exception& e) {
+      printf("restrict: %s\n", e.what());
+    }
+    MPI_Finalize();
+    printf(rc == 0 ? "DROPINR OK\n" : "DROPINR FAILED\n");
+    return rc;
+  }
   if (argc == 7 && std::string(argv[1]) == "--3d") {
     int rc = 1;
     try {

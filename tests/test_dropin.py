@@ -96,3 +96,32 @@ def test_dropin_3dspgemm_and_summa3d_on_gpu(q, L, tmp_path):
     r = subprocess.run([mpirun, "-np", str(world), BIN, "--3d", str(q), str(L), fa, fc, fg], capture_output=True,
                        text=True, timeout=300)
     assert r.returncode == 0 and r.stdout.count("DROPIN3D OK") == world, r.stdout + r.stderr
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("q", [1, 2])
+@pytest.mark.parametrize("name", ["poisson12", "g500_s10"])
+def test_dropin_restriction_op_on_gpu(q, name, tmp_path):
+    """gpu::RestrictionOp (3DSpGEMM/RestrictionOp.h:196-291) on a CCGrid layer of q x q MPI ranks: the layer's pieces
+    go to the device on the layer's rank 0, and every rank's R and R^T blocks (SpParMat distribution of the layer
+    grid) must hold the reference's one-rank R -- oracle/_ref/refrestrict's output in golden/restriction.npz."""
+    mpirun = "/opt/conda/bin/mpirun"
+    if not os.path.exists(BIN) or not os.path.exists(mpirun):
+        pytest.skip("dropin_test or MPICH's mpirun not available")
+    import numpy as np
+    z = np.load(os.path.join(HERE, "golden", "restriction.npz"))
+    if name.startswith("poisson"):
+        import sys
+        sys.path.insert(0, os.path.dirname(HERE))
+        from combblas_amd.inputs import poisson3d
+        n, cp, ir, val = poisson3d(int(name[len("poisson"):]))
+    else:
+        cp, ir = z[f"{name}_cp"], z[f"{name}_ir"]
+        n = len(z[f"{name}_agg"])
+        val = np.ones(len(ir))
+    fa, fg = str(tmp_path / "A.mtx"), str(tmp_path / "agg.txt")
+    _write_mtx(fa, n, n, cp, ir, val)
+    np.savetxt(fg, z[f"{name}_agg"].astype(np.int64), fmt="%d")
+    r = subprocess.run([mpirun, "-np", str(q * q), BIN, "--restrict", str(q), fa, fg], capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0 and r.stdout.count("DROPINR OK") == q * q, r.stdout + r.stderr
