@@ -1001,8 +1001,11 @@ __global__ void __launch_bounds__(NT) k_sym_block(const int32_t* __restrict__ li
 #endif
 constexpr int kPartLog = CBG_PART_LOG;
 constexpr int kPartNT = CBG_PART_NT;
+#ifndef CBG_KNOWN_OTF
+#define CBG_KNOWN_OTF 1   // k_num_heavy_known computes its unit segments from the split table (no k_unit_segs store)
+#endif
 #ifndef CBG_SYM_SHORT_SEARCH
-#define CBG_SYM_SHORT_SEARCH 1   // k_sym_part narrows a short A column to the part's rows by binary search
+#define CBG_SYM_SHORT_SEARCH 0   // 1: k_sym_part narrows a short A column to the part's rows by binary search (r03s: +0.8 ms)
 #endif
 #ifndef CBG_SYM_ROWS_WAVE
 #define CBG_SYM_ROWS_WAVE 0   // 1: k_sym_part emits its rows word-major per wave (measured slower, r03d)
@@ -1403,11 +1406,16 @@ __global__ void k_build_units(int H, const int32_t* __restrict__ cols, const int
 // mostly from cache, instead of a dependent lookup chain per (unit, b) inside the numeric kernel).
 // Short A columns are given whole (rows outside a unit are dropped at insert time) unless their row
 // range misses the unit entirely.
+template <class SRT, int LOGT, int NT>
+__device__ __forceinline__ bool heavy_unit_known(const Unit& un, int2 usp, const UnitRows& ur);
+
+template <class SRT, int LOGT, int NT>
 __global__ void __launch_bounds__(256) k_unit_segs(const int32_t* __restrict__ cols, const int32_t* __restrict__ nunits,
                                                    const int64_t* __restrict__ segoff, Unit* __restrict__ units,
                                                    int32_t nsub, const int64_t* __restrict__ Acp,
                                                    const int32_t* __restrict__ Air, const int64_t* __restrict__ Bcp,
-                                                   const int32_t* __restrict__ Bir, Split sp, UnitSeg* __restrict__ seg) {
+                                                   const int32_t* __restrict__ Bir, Split sp, UnitSeg* __restrict__ seg,
+                                                   const int2* __restrict__ uspan) {
   const int h = blockIdx.x;
   const int32_t j = cols[h];
   const int nu = nunits[h];
@@ -1415,6 +1423,22 @@ __global__ void __launch_bounds__(256) k_unit_segs(const int32_t* __restrict__ c
   const int64_t base = segoff[h];
   Unit* U = units + (int64_t)h * nsub;
   for (int u = threadIdx.x; u < nu; u += blockDim.x) U[u].segbase = base + (int64_t)u * nb;
+#if CBG_KNOWN_OTF
+  // units the rows-known kernel takes compute their segments on the fly: when every unit of the column is
+  // one of them, nothing is stored
+  __shared__ int s_other;
+  if (threadIdx.x == 0) s_other = 0;
+  __syncthreads();
+  if (sp.urows) {
+    for (int u = threadIdx.x; u < nu; u += blockDim.x)
+      if (!heavy_unit_known<SRT, LOGT, NT>(U[u], uspan[(int64_t)h * nsub + u], sp.urows[(int64_t)h * nsub + u]))
+        s_other = 1;
+  } else if (threadIdx.x == 0) {
+    s_other = 1;
+  }
+  __syncthreads();
+  if (!s_other) return;
+#endif
   for (int64_t i = threadIdx.x; i < nb; i += blockDim.x) {
     const int32_t k = Bir[bs + i];
     const int64_t c0 = Acp[k], c1 = Acp[k + 1];
@@ -2309,9 +2333,27 @@ __global__ void __launch_bounds__(NT) k_num_heavy_known(const KnownUnit* __restr
     a0 = a1 = 0;
     bv = V(0);
     if (i < H.nb) {
+#if CBG_KNOWN_OTF
+      // the segment of this B nonzero inside the unit's rows, from the split table (what k_unit_segs would have
+      // stored, narrowed to the unit's row span [lo, hi]; prefetched a chunk ahead, so the extra levels of
+      // loads overlap the current sweep)
+      const int32_t k = B.ir[H.bs + i];
+      const int64_t c0 = A.cp[k], c1 = A.cp[k + 1];
+      if (c1 - c0 >= kSplitMin) {
+        const int32_t* t = spl.tab + (int64_t)spl.idx[k] * (spl.nsub + 1);
+        a0 = c0 + t[H.lo >> spl.log];
+        a1 = c0 + t[(H.hi >> spl.log) + 1];
+      } else if (c1 > c0 && A.ir[c1 - 1] >= H.lo && A.ir[c0] <= H.hi) {
+        a0 = c0;
+        a1 = c1;
+      } else {
+        a0 = a1 = c0;
+      }
+#else
       const UnitSeg g = spl.useg[H.segbase + i];
       a0 = g.a0;
       a1 = g.a1;
+#endif
       bv = load_val(B.val, H.bs + i);
     }
   };
