@@ -1002,7 +1002,7 @@ __global__ void __launch_bounds__(NT) k_sym_block(const int32_t* __restrict__ li
 constexpr int kPartLog = CBG_PART_LOG;
 constexpr int kPartNT = CBG_PART_NT;
 #ifndef CBG_KNOWN_OTF
-#define CBG_KNOWN_OTF 1   // k_num_heavy_known computes its unit segments from the split table (no k_unit_segs store)
+#define CBG_KNOWN_OTF 0   // 1: k_num_heavy_known computes its unit segments from the split table (r03t: heavy +8 ms)
 #endif
 #ifndef CBG_SYM_SHORT_SEARCH
 #define CBG_SYM_SHORT_SEARCH 0   // 1: k_sym_part narrows a short A column to the part's rows by binary search (r03s: +0.8 ms)
