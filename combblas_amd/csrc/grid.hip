@@ -143,6 +143,17 @@ struct cbg_grid {
   cbg_transport cb{};
   hipStream_t cs = nullptr;          // communication stream
   hipEvent_t ev_comm[2] = {}, ev_used[2] = {}, ev_t[4] = {};
+  std::vector<hipEvent_t> ev_stage;  // timing events of the schedules, created once and reused by every call
+  hipError_t stage_event(size_t i, hipEvent_t* e) {
+    while (ev_stage.size() <= i) {
+      hipEvent_t x;
+      hipError_t r = hipEventCreate(&x);
+      if (r != hipSuccess) return r;
+      ev_stage.push_back(x);
+    }
+    *e = ev_stage[i];
+    return hipSuccess;
+  }
   bool used_rec[2] = {false, false};
   DevBuf slotA[2], slotB[2], small, xsend, xrecv, xcnt;
 
@@ -580,9 +591,9 @@ cbg_status summa_layer_impl(cbg_grid* G, const cbg_dcsc_view* Av, const cbg_dcsc
       pb[k] = b;
     }
     hipEvent_t e0, e1, ready;
-    HIPCHK(hipEventCreate(&e0));
-    HIPCHK(hipEventCreate(&e1));
-    HIPCHK(hipEventCreate(&ready));
+    HIPCHK(G->stage_event(0, &e0));
+    HIPCHK(G->stage_event(1, &e1));
+    HIPCHK(G->stage_event(2, &ready));
     HIPCHK(hipEventRecord(ready, ctx->stream));   // the own pieces are complete before they are sent
     HIPCHK(hipStreamWaitEvent(G->cs, ready, 0));
     HIPCHK(hipEventRecord(e0, G->cs));
@@ -623,9 +634,6 @@ cbg_status summa_layer_impl(cbg_grid* G, const cbg_dcsc_view* Av, const cbg_dcsc
     float ms = 0.f;
     (void)hipEventElapsedTime(&ms, e0, e1);
     if (st) st->bcast_ms += ms;
-    (void)hipEventDestroy(e0);
-    (void)hipEventDestroy(e1);
-    (void)hipEventDestroy(ready);
     return CBG_OK;
   }
   if (q > 1)
@@ -659,8 +667,8 @@ cbg_status summa_layer_impl(cbg_grid* G, const cbg_dcsc_view* Av, const cbg_dcsc
     }
     if (q > 1) {
       hipEvent_t e0, e1;
-      HIPCHK(hipEventCreate(&e0));
-      HIPCHK(hipEventCreate(&e1));
+      HIPCHK(G->stage_event(2 * (size_t)t, &e0));
+      HIPCHK(G->stage_event(2 * (size_t)t + 1, &e1));
       if (G->rccl && G->used_rec[slot]) HIPCHK(hipStreamWaitEvent(G->cs, G->ev_used[slot], 0));
       HIPCHK(hipEventRecord(e0, G->cs));
       void* ab[3] = {(void*)a.cp, (void*)a.ir, (void*)a.val};
@@ -754,8 +762,6 @@ cbg_status summa_layer_impl(cbg_grid* G, const cbg_dcsc_view* Av, const cbg_dcsc
     float ms = 0.f;
     (void)hipEventElapsedTime(&ms, e.first, e.second);
     if (st) st->bcast_ms += ms;
-    (void)hipEventDestroy(e.first);
-    (void)hipEventDestroy(e.second);
   }
   return CBG_OK;
 }
@@ -1232,6 +1238,7 @@ cbg_status cbg_grid_destroy(cbg_grid* G) {
   }
   for (int i = 0; i < 4; ++i)
     if (G->ev_t[i]) (void)hipEventDestroy(G->ev_t[i]);
+  for (hipEvent_t e : G->ev_stage) (void)hipEventDestroy(e);
   if (G->cs) (void)hipStreamDestroy(G->cs);
   delete G;
   return CBG_OK;
