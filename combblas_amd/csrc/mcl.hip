@@ -24,7 +24,9 @@
 //   k_mcl_count   wave per column: kept entries -> scan -> colptr
 //   k_mcl_compact wave per column: ballot compaction in column order
 //   k_mcl_fused   (default) workgroup per column: the first three in one read of the values (LDS-staged
-//                 column, selection on the LDS copy); CBG_MCL_SPLIT=1 runs the three kernels instead.
+//                 column; both k-th values from one 10-bit histogram below the column's common key prefix,
+//                 block_kth2); CBG_MCL_RADIX=1 keeps the 8-bit radix passes in the fused kernel
+//                 (k_mcl_fused_radix), CBG_MCL_SPLIT=1 runs the three kernels instead.
 //                 (A wave-per-column variant holding the column in registers was measured slower: 436 VGPRs,
 //                 one wave per SIMD -- profiles/r03i_config4_prune_variants.txt.)
 #include "spgemm_host.hpp"
@@ -173,16 +175,231 @@ __device__ V block_kth(const V* __restrict__ val, int64_t a, int64_t b, int64_t 
   return block_kth_ld<V, NT>([&](int64_t i) { return val[a + i]; }, b - a, k, hist, red, bc);
 }
 
+// Both k-th largest values of one column from ONE histogram (k_mcl_fused's selection): the keys' common
+// prefix comes from the column's key range (kmin..kmax, taken in the statistics pass), one kSelBits-bit digit
+// below it buckets the column, a block suffix scan finds the bucket of each target, the (few) keys of those
+// buckets are gathered into LDS lists and wave q ranks list q exactly.  Six barriers instead of block_kth's
+// four per 8-bit digit; a list that overflows kSelList falls back to block_kth_ld for that target.
+// Preconditions: 1 <= k0 <= n; k1 == 0 (no second target) or 1 <= k1 <= n.
+constexpr int kSelBits = 10, kSelBins = 1 << kSelBits, kSelList = 128;
+
+template <typename K> struct SelScratch {
+  unsigned hist[kSelBins];
+  K list[2][kSelList];
+  unsigned lcnt[2], wtot[8];
+  int dig[2];
+  int64_t kr[2];
+  K res[2];
+};
+
+template <typename V, int NT, class LD>
+__device__ void block_kth2(LD ld, int64_t n, int64_t k0, int64_t k1, typename KeyOf<V>::K kmin,
+                           typename KeyOf<V>::K kmax, SelScratch<typename KeyOf<V>::K>& s, V* red,
+                           unsigned long long* bc, V& t0, V& t1) {
+  using KO = KeyOf<V>;
+  using K = typename KO::K;
+  constexpr int B = 8 * (int)sizeof(K);
+  constexpr int PB = kSelBins / NT;   // thread t owns bins PB*t .. PB*t+PB-1
+  static_assert(PB * NT == kSelBins && PB >= 1 && NT / kWave <= 8, "bins split evenly over the threads");
+  if (kmin == kmax) { t0 = t1 = KO::val(kmax); return; }
+  const K dx = kmin ^ kmax;
+  const int vb = B - (sizeof(K) == 8 ? __builtin_clzll((unsigned long long)dx) : __builtin_clz((unsigned)dx));
+  const int shift = vb > kSelBits ? vb - kSelBits : 0;
+  const int tid = threadIdx.x, w = tid / kWave, l = lane_id();
+  for (int i = tid; i < kSelBins; i += NT) s.hist[i] = 0;
+  if (tid < 2) s.lcnt[tid] = 0;
+  __syncthreads();
+  for (int64_t i = tid; i < n; i += NT) atomicAdd(&s.hist[(KO::key(ld(i)) >> shift) & (kSelBins - 1)], 1u);
+  __syncthreads();
+  unsigned h[PB], own = 0;
+#pragma unroll
+  for (int u = 0; u < PB; ++u) { h[u] = s.hist[PB * tid + u]; own += h[u]; }
+  unsigned incl = own;   // inclusive suffix over the wave's lanes >= l
+#pragma unroll
+  for (int d = 1; d < kWave; d <<= 1) {
+    const unsigned t = __shfl_down(incl, d, kWave);
+    if (l + d < kWave) incl += t;
+  }
+  if (l == 0) s.wtot[w] = incl;
+  __syncthreads();
+  for (int v = w + 1; v < NT / kWave; ++v) incl += s.wtot[v];
+  const unsigned above = incl - own;   // entries in bins > PB*t+PB-1
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int64_t kq = q ? k1 : k0;
+    if (kq > 0 && (int64_t)above < kq && (int64_t)incl >= kq) {   // exactly one thread holds target q
+      int64_t c = (int64_t)above;
+      int dg = PB * tid;
+#pragma unroll
+      for (int u = PB - 1; u >= 0; --u) {   // highest bin first: the k-th largest
+        if (c + h[u] >= kq) { dg = PB * tid + u; break; }
+        c += h[u];
+      }
+      s.dig[q] = dg;
+      s.kr[q] = kq - c;
+    }
+  }
+  __syncthreads();
+  const int d0 = s.dig[0], d1 = k1 > 0 ? s.dig[1] : -1;
+  for (int64_t i = tid; i < n; i += NT) {
+    const K key = KO::key(ld(i));
+    const int dg = (int)((key >> shift) & (kSelBins - 1));
+    if (dg == d0) { const unsigned at = atomicAdd(&s.lcnt[0], 1u); if (at < kSelList) s.list[0][at] = key; }
+    if (dg == d1) { const unsigned at = atomicAdd(&s.lcnt[1], 1u); if (at < kSelList) s.list[1][at] = key; }
+  }
+  __syncthreads();
+  if (w < 2 && (w == 0 || k1 > 0)) {   // wave q ranks list q: the key with gt < kr <= ge is the answer
+    const unsigned m = s.lcnt[w];
+    if (m <= (unsigned)kSelList) {
+      const int64_t kr = s.kr[w];
+#pragma unroll
+      for (int h = 0; h < kSelList / kWave; ++h) {
+        const unsigned e = l + h * kWave;
+        if (e < m) {
+          const K x = s.list[w][e];
+          int64_t gt = 0, ge = 0;
+          for (unsigned y = 0; y < m; ++y) {
+            const K z = s.list[w][y];
+            gt += z > x;
+            ge += z >= x;
+          }
+          if (gt < kr && ge >= kr) s.res[w] = x;   // equal keys write the same value
+        }
+      }
+    }
+  }
+  __syncthreads();
+  const bool of0 = s.lcnt[0] > (unsigned)kSelList, of1 = k1 > 0 && s.lcnt[1] > (unsigned)kSelList;
+  t0 = KO::val(s.res[0]);
+  t1 = k1 > 0 ? KO::val(s.res[1]) : V(0);
+  __syncthreads();
+  if (of0) t0 = block_kth_ld<V, NT>(ld, n, k0, s.hist, red, bc);
+  if (of1) t1 = block_kth_ld<V, NT>(ld, n, k1, s.hist, red, bc);
+}
+
 // One pass over the column values for everything but the compaction: the column is staged in LDS (columns of
-// up to kMclCap entries; longer ones are read from HBM), wave 0 takes the statistics in k_mcl_stats' order, the
-// k-selections run on the LDS copy (k_mcl_select's radix select and recovery test), and the kept count of
-// k_mcl_count -- one read of the values instead of three, and the select passes hit LDS.
+// up to kMclCap entries; longer ones are read from HBM), all waves take the statistics (nP, sP, the kept count at
+// thr and the key range), block_kth2 finds the select and the recover targets from one histogram, and one more
+// pass gives the recovery-after-selection test and the kept count for both candidate thresholds -- one read of
+// the values instead of k_mcl_stats + k_mcl_select + k_mcl_count's three.  (k_mcl_fused_radix, behind
+// CBG_MCL_RADIX=1, is the same kernel with k_mcl_select's 8-bit radix passes and wave-0 statistics.)
 constexpr int kMclCap = 4096;
 
 template <typename V, int NT>
+__device__ __forceinline__ void stage_column(V* lv, const V* __restrict__ val, int64_t a, int64_t n) {
+  for (int64_t i0 = threadIdx.x; i0 < n; i0 += 8 * NT) {   // 8 independent loads in flight, then the stores
+    V r[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) r[u] = i0 + u * NT < n ? val[a + i0 + u * NT] : V(0);
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (i0 + u * NT < n) lv[i0 + u * NT] = r[u];
+  }
+}
+
+template <typename V, int NT, int CAP>
 __global__ void __launch_bounds__(NT) k_mcl_fused(int64_t ncol, const int64_t* __restrict__ cp,
                                                   const V* __restrict__ val, MclParams p, V* __restrict__ th,
                                                   int64_t* __restrict__ cnt, unsigned long long* __restrict__ counters) {
+  using KO = KeyOf<V>;
+  using K = typename KO::K;
+  constexpr int NW = NT / kWave;
+  __shared__ V lv[CAP];
+  __shared__ SelScratch<K> ss;
+  __shared__ V red[NW], wsp[NW];
+  __shared__ int64_t wnp[NW], wge[NW], wn1[NW], wnr[NW];   // second-pass sums in their own slots: no barrier
+  __shared__ K wkmn[NW], wkmx[NW];
+  __shared__ unsigned long long bc[2];
+  const int w = threadIdx.x / kWave;
+  for (int64_t j = blockIdx.x; j < ncol; j += gridDim.x) {
+    const int64_t a = cp[j], b = cp[j + 1], n = b - a;
+    const bool inl = n <= CAP;
+    if (inl) stage_column<V, NT>(lv, val, a, n);
+    __syncthreads();
+    auto ld = [&](int64_t i) -> V { return inl ? lv[i] : val[a + i]; };
+    const V thr = (V)p.thr;
+    {   // column statistics over all waves: nP = |v > thr|, sP, |v >= thr| (the kept count at thr), key range
+      int64_t np = 0, nge = 0;
+      V sp = 0;
+      K kmn = ~K(0), kmx = 0;
+      for (int64_t i = threadIdx.x; i < n; i += NT) {
+        const V v = ld(i);
+        if (v > thr) { ++np; sp += v; }
+        nge += v >= thr;
+        const K key = KO::key(v);
+        kmn = min(kmn, key);
+        kmx = max(kmx, key);
+      }
+      np = wave_sum(np);
+      nge = wave_sum(nge);
+      sp = wave_sum(sp);
+#pragma unroll
+      for (int d = 32; d >= 1; d >>= 1) {
+        kmn = min(kmn, (K)__shfl_xor(kmn, d, kWave));
+        kmx = max(kmx, (K)__shfl_xor(kmx, d, kWave));
+      }
+      if (lane_id() == 0) { wnp[w] = np; wge[w] = nge; wsp[w] = sp; wkmn[w] = kmn; wkmx[w] = kmx; }
+    }
+    __syncthreads();
+    int64_t NP = 0, C = 0;
+    V SP = 0;
+    K kmn = ~K(0), kmx = 0;
+    for (int v = 0; v < NW; ++v) {
+      NP += wnp[v]; C += wge[v]; SP += wsp[v];
+      kmn = min(kmn, wkmn[v]);
+      kmx = max(kmx, wkmx[v]);
+    }
+    int m = kModeThr;
+    if (NP < p.R && n > NP && SP < (V)p.pct) m = kModeRecover;
+    else if (p.S > 0 && NP > p.S) m = kModeSelect;
+    if (threadIdx.x == 0 && m != kModeThr) atomicAdd(&counters[m], 1ull);
+    V t = thr;
+    if (m != kModeThr) {
+      // Kselect1 targets: kth(S) for select, kth(R) for recover or recovery after selection; k > n -> the
+      // column minimum (n >= 1 here: nP > S >= 1 or nU > nP)
+      const V vmin = KO::val(kmn);
+      const int64_t kR = p.R > 0 && p.R <= n ? p.R : 0;
+      V r0 = vmin, r1 = vmin;
+      if (m == kModeSelect) block_kth2<V, NT>(ld, n, p.S, kR, kmn, kmx, ss, red, bc, r0, r1);   // S < nP <= n
+      else if (kR > 0) block_kth2<V, NT>(ld, n, kR, 0, kmn, kmx, ss, red, bc, r1, r0);
+      const V tS = r0, tR = r1;
+      // one pass: the kept count at the final threshold, and for selection the recovery test
+      // (ParFriends.h:290-333: n1 = |v >= tS|, s1 = sum{v >= tS}; n1 < R && s1 < pct -> tR)
+      const bool sel = m == kModeSelect;
+      int64_t n1 = 0, nr = 0;
+      V s1 = 0;
+      for (int64_t i = threadIdx.x; i < n; i += NT) {
+        const V v = ld(i);
+        if (sel && v >= tS) { ++n1; s1 += v; }
+        nr += v >= tR;
+      }
+      n1 = wave_sum(n1);
+      nr = wave_sum(nr);
+      s1 = wave_sum(s1);
+      if (lane_id() == 0) { wn1[w] = n1; wnr[w] = nr; red[w] = s1; }
+      __syncthreads();
+      int64_t N1 = 0, NR = 0;
+      V S1 = 0;
+      for (int v = 0; v < NW; ++v) { N1 += wn1[v]; NR += wnr[v]; S1 += red[v]; }
+      if (!sel) {
+        t = tR; C = NR;
+      } else if (p.R > 0 && N1 < p.R && S1 < (V)p.pct) {
+        t = tR; C = NR;
+        if (threadIdx.x == 0) atomicAdd(&counters[3], 1ull);
+      } else {
+        t = tS; C = N1;
+      }
+    }
+    if (threadIdx.x == 0) { cnt[j] = C; th[j] = t; }
+    __syncthreads();
+  }
+}
+
+template <typename V, int NT>
+__global__ void __launch_bounds__(NT) k_mcl_fused_radix(int64_t ncol, const int64_t* __restrict__ cp,
+                                                        const V* __restrict__ val, MclParams p, V* __restrict__ th,
+                                                        int64_t* __restrict__ cnt,
+                                                        unsigned long long* __restrict__ counters) {
   __shared__ V lv[kMclCap];
   __shared__ unsigned hist[256];
   __shared__ V red[NT / kWave];
@@ -192,16 +409,7 @@ __global__ void __launch_bounds__(NT) k_mcl_fused(int64_t ncol, const int64_t* _
   for (int64_t j = blockIdx.x; j < ncol; j += gridDim.x) {
     const int64_t a = cp[j], b = cp[j + 1], n = b - a;
     const bool inl = n <= kMclCap;
-    if (inl) {   // 8 independent loads in flight per thread, then the LDS stores
-      for (int64_t i0 = threadIdx.x; i0 < n; i0 += 8 * NT) {
-        V r[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) r[u] = i0 + u * NT < n ? val[a + i0 + u * NT] : V(0);
-#pragma unroll
-        for (int u = 0; u < 8; ++u)
-          if (i0 + u * NT < n) lv[i0 + u * NT] = r[u];
-      }
-    }
+    if (inl) stage_column<V, NT>(lv, val, a, n);
     __syncthreads();
     auto ld = [&](int64_t i) -> V { return inl ? lv[i] : val[a + i]; };
     const V thr = (V)p.thr;
@@ -424,8 +632,12 @@ cbg_status mcl_prune_impl(cbg_ctx* ctx, const cbg_csc_result* in, const MclParam
         list.as<int32_t>(), sc, in->colptr, val, p, th.as<V>(), mode.as<int32_t>(), sc);
     k_mcl_count<V><<<gw, 256, 0, st>>>(N, in->colptr, val, th.as<V>(), cnt.as<int64_t>());
   } else if (N > 0) {
-    k_mcl_fused<V, 256><<<(int)grid_for(N, 1, kMaxGrid * 8), 256, 0, st>>>(N, in->colptr, val, p, th.as<V>(),
-                                                                          cnt.as<int64_t>(), sc);
+    static const bool radix = [] { const char* e = std::getenv("CBG_MCL_RADIX"); return e && e[0] == '1'; }();
+    const int g = (int)grid_for(N, 1, kMaxGrid * 8);
+    if (radix)
+      k_mcl_fused_radix<V, 256><<<g, 256, 0, st>>>(N, in->colptr, val, p, th.as<V>(), cnt.as<int64_t>(), sc);
+    else
+      k_mcl_fused<V, 256, kMclCap><<<g, 256, 0, st>>>(N, in->colptr, val, p, th.as<V>(), cnt.as<int64_t>(), sc);
   }
   if (N > 0) {
     const int64_t ntiles = (N + kScanTile - 1) / kScanTile;

@@ -109,6 +109,33 @@ def test_prune_edge_cases(gpu_ctx):
         assert (st["recovered"], st["selected"], st["recovered_after_select"]) == ost
 
 
+def test_prune_selection_adversarial(gpu_ctx):
+    """Columns that stress k_mcl_fused's one-histogram selection (block_kth2): one repeated value (empty key
+    range), a few values with thousands of ties (gathered bucket lists overflow -> radix fallback), a column
+    longer than the LDS stage (values read from HBM), values a few ulps apart (every bucket exact), mixed
+    signs, and a tie block straddling the k-th position."""
+    rng = np.random.default_rng(7)
+    cols = [np.full(3000, 0.25),
+            rng.choice([0.1, 0.2, 0.3, 0.4, 0.5], 3000),
+            rng.lognormal(-6, 2, 5000),
+            0.5 + np.arange(2000) * np.spacing(0.5),
+            rng.normal(0, 1, 2500),
+            np.concatenate([np.full(1200, 0.3), rng.uniform(0, 0.29, 300)]),
+            rng.lognormal(-4, 1, 1300)]
+    cols = [rng.permutation(c) for c in cols]
+    cp = np.cumsum([0] + [len(c) for c in cols]).astype(np.int64)
+    ir = np.concatenate([np.sort(rng.choice(6000, len(c), replace=False)) for c in cols]).astype(np.int32)
+    val = np.concatenate(cols).astype(np.float64)
+    M = Csc(6000, len(cols), cp, ir, val)
+    for params in [(1e-4, 1100, 1400, 0.9), (1e-4, 1000, 0, 0.9), (0.6, 100, 2600, 0.99), (1e-9, 1250, 1250, 1.0),
+                   (1e-9, 100, 2600, 1e6), (1e-9, 100, 1200, 1e6)]:
+        D = up(gpu_ctx, M)
+        st = cb.MCLPruneRecoverySelect(D, *params)
+        O, ost = oracle_mcl_prune(M, *params)
+        assert_same_product(host(D, 6000), O, "f64", rtol=0.0, what=f"adversarial {params}")
+        assert (st["recovered"], st["selected"], st["recovered_after_select"]) == ost
+
+
 def test_prune_f32_and_empty(gpu_ctx):
     n, cp, ir, val = protein_like_graph(3000, seed=2, cmax=200)
     A32 = Csc(n, n, cp, ir, val.astype(np.float32))
