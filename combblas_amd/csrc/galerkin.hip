@@ -157,7 +157,7 @@ __global__ void k_member_len(int64_t nnzr, const int32_t* __restrict__ rir, cons
 // R(i,I) A(i,j) R(j,J), bitonic-sorted, and every run of one row is summed in position order
 // (deterministic); count pass -> cnt[J], fill pass -> sorted (row, value) at ccp[J].  Aggregates with
 // more than kRapCap entries are counted in *overflow (the caller falls back to two SpGEMMs).
-constexpr int kRapCap = 512;
+constexpr int kRapCap = 512, kRapMem = 256;
 
 __global__ void __launch_bounds__(64) k_rap_agg(int64_t nagg, const int64_t* __restrict__ rcp,
                                                 const int32_t* __restrict__ rir, const int64_t* __restrict__ acp,
@@ -168,6 +168,9 @@ __global__ void __launch_bounds__(64) k_rap_agg(int64_t nagg, const int64_t* __r
                                                 unsigned long long* __restrict__ overflow) {
   __shared__ uint64_t key[kRapCap];
   __shared__ double val[kRapCap];
+  __shared__ int32_t s_mo[kRapMem + 1];   // members' entry offsets (relative to the aggregate's first entry)
+  __shared__ int64_t s_q0[kRapMem];       // members' A column starts
+  __shared__ double s_rvj[kRapMem];       // R(j, J)
   const int lane = threadIdx.x;
   for (int64_t J = blockIdx.x; J < nagg; J += gridDim.x) {
     const int64_t p0 = rcp[J], p1 = rcp[J + 1];
@@ -179,7 +182,31 @@ __global__ void __launch_bounds__(64) k_rap_agg(int64_t nagg, const int64_t* __r
     }
     int N = 64;
     while (N < t) N <<= 1;
-    for (int e = lane; e < N; e += 64) {
+    const int64_t nm = p1 - p0;
+    if (nm <= kRapMem) {   // members staged: one level of member loads, then the entry -> member search in LDS
+      for (int64_t m = lane; m < nm; m += 64) {
+        const int32_t j = rir[p0 + m];
+        s_mo[m] = (int32_t)(moff[p0 + m] - base);
+        s_q0[m] = acp[j];
+        s_rvj[m] = rv[j];
+      }
+      __syncthreads();
+      for (int e = lane; e < N; e += 64) {
+        if (e < t) {
+          int lo = 0, hi = (int)nm - 1;   // last member m with s_mo[m] <= e
+          while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (s_mo[mid] <= e) lo = mid; else hi = mid - 1;
+          }
+          const int64_t q = s_q0[lo] + (e - s_mo[lo]);
+          const int32_t i = air[q];
+          key[e] = ((uint64_t)(uint32_t)agg[i] << 32) | (uint32_t)e;
+          val[e] = rv[i] * (aval ? aval[q] : 1.0) * s_rvj[lo];
+        } else {
+          key[e] = ~0ull;
+        }
+      }
+    } else for (int e = lane; e < N; e += 64) {
       if (e < t) {
         int64_t lo = p0, hi = p1 - 1;   // the member holding entry e: last p with moff[p] - base <= e
         while (lo < hi) {
