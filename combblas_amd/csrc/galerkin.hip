@@ -157,7 +157,7 @@ __global__ void k_member_len(int64_t nnzr, const int32_t* __restrict__ rir, cons
 // R(i,I) A(i,j) R(j,J), bitonic-sorted, and every run of one row is summed in position order
 // (deterministic); count pass -> cnt[J], fill pass -> sorted (row, value) at ccp[J].  Aggregates with
 // more than kRapCap entries are counted in *overflow (the caller falls back to two SpGEMMs).
-constexpr int kRapCap = 512, kRapMem = 256;
+constexpr int kRapCap = 512, kRapMem = 64;
 
 __global__ void __launch_bounds__(64) k_rap_agg(int64_t nagg, const int64_t* __restrict__ rcp,
                                                 const int32_t* __restrict__ rir, const int64_t* __restrict__ acp,
