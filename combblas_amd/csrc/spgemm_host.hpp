@@ -271,6 +271,8 @@ inline cbg_status bin_fill(hipStream_t st, int64_t n, const int64_t* cnt, const 
   cl->off.assign(32, 0);
   unsigned long long acc = 0;
   for (int c = 0; c < ncls; ++c) { cl->off[c] = acc; acc += cl->hist[c]; }
+  cl->off[kLane8Class] = acc;
+  acc += cl->hist[kLane8Class];
   cl->off[kLaneClass] = acc;
   HIPCHK(hipMemcpyAsync(hist_dev + 32, cl->off.data(), sizeof(unsigned long long) * 32, hipMemcpyHostToDevice, st));
   const int64_t g = (n + 256 * kBinPer - 1) / (256 * kBinPer);
@@ -375,8 +377,11 @@ hipError_t launch_numeric_classes(hipStream_t st, const Classes& cl, const int32
   auto L = [&](int c) { return list + cl.off[c]; };
   auto n = [&](int c) { return (int64_t)cl.hist[c]; };
   if constexpr (!UNIT) {
+    if (n(kLane8Class))
+      k_num_lane<SRT, V, kLaneSmall><<<(int)grid_for(n(kLane8Class), 256, kMaxGrid * 4), 256, 0, st>>>(
+          L(kLane8Class), n(kLane8Class), A, B, colptr, o);
     if (n(kLaneClass))
-      k_num_lane<SRT, V><<<(int)grid_for(n(kLaneClass), 256, kMaxGrid * 4), 256, 0, st>>>(L(kLaneClass), n(kLaneClass),
+      k_num_lane<SRT, V, kLaneMax><<<(int)grid_for(n(kLaneClass), 256, kMaxGrid * 4), 256, 0, st>>>(L(kLaneClass), n(kLaneClass),
                                                                                           A, B, colptr, o);
   }
   if (n(1)) launch_num_wave<6, SRT, V, UNIT>(st, L(1), n(1), units, A, B, span, colptr, spl, o);
@@ -465,7 +470,15 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
       *fb_ovf_n = si + 6;
   HIPCHK(hipMemsetAsync(sc, 0, 128, st));
   HIPCHK(hipMemsetAsync(nnz, 0, sizeof(int64_t) * N, st));
-  k_col_stats<<<(int)grid_for(N * 16, 256, kMaxGrid), 256, 0, st>>>(N, A.cp, A.ir, B.cp, B.ir, flop, span, sc);
+  {
+    const int64_t avg = N > 0 ? (B.nnz + N - 1) / N : 0;   // lanes per column ~ the mean B column length
+    if (avg <= 4)
+      k_col_stats<4><<<(int)grid_for(N * 4, 256, kMaxGrid), 256, 0, st>>>(N, A.cp, A.ir, B.cp, B.ir, flop, span, sc);
+    else if (avg <= 8)
+      k_col_stats<8><<<(int)grid_for(N * 8, 256, kMaxGrid), 256, 0, st>>>(N, A.cp, A.ir, B.cp, B.ir, flop, span, sc);
+    else
+      k_col_stats<16><<<(int)grid_for(N * 16, 256, kMaxGrid), 256, 0, st>>>(N, A.cp, A.ir, B.cp, B.ir, flop, span, sc);
+  }
   k_split_assign<<<(int)grid_for(A.ncol, 256, kMaxGrid), 256, 0, st>>>(A.ncol, A.cp, ctx->split_idx.as<int32_t>(),
                                                                         ctx->long_cols.as<int32_t>(), nlong);
   HIPCHK(hipGetLastError());

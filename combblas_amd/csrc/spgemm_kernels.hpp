@@ -252,23 +252,27 @@ __device__ __forceinline__ void unit_bounds(const int64_t* __restrict__ Acp, con
 // ============================================================================ 1. column statistics
 // flop[j] = sum_{k in B(:,j)} nnz(A(:,k))   (estimateFLOP, mtSpGEMM.h:1117-1135)
 // span[j] = [min, max] row index any of those A columns holds (A columns are row-sorted).
-// 16 lanes per column.
+// LPC lanes per column (4, 8 or 16: the host picks the power of two nearest nnz(B)/ncol, so short columns do
+// not idle most of a 16-lane group).
+template <int LPC>
 __global__ void __launch_bounds__(256) k_col_stats(int64_t ncol, const int64_t* __restrict__ Acp,
                                                    const int32_t* __restrict__ Air,
                                                    const int64_t* __restrict__ Bcp,
                                                    const int32_t* __restrict__ Bir,
                                                    int64_t* __restrict__ flop, int2* __restrict__ span,
                                                    unsigned long long* __restrict__ total) {
-  // 16 lanes per column, grid-stride over column groups; the block totals are added once per block
-  // (one global atomic per block: a same-address atomic per 16 columns serialised at the L2)
-  const int sub = threadIdx.x & 15;
+  // LPC lanes per column, grid-stride over column groups; the block totals are added once per block
+  // (one global atomic per block: a same-address atomic per column group serialised at the L2)
+  constexpr int LOG = LPC == 4 ? 2 : LPC == 8 ? 3 : 4;
+  static_assert(LPC == 4 || LPC == 8 || LPC == 16, "4, 8 or 16 lanes per column");
+  const int sub = threadIdx.x & (LPC - 1);
   int64_t wf = 0, hb = 0;
-  for (int64_t j = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 4; j < ncol;
-       j += ((int64_t)gridDim.x * blockDim.x) >> 4) {
+  for (int64_t j = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> LOG; j < ncol;
+       j += ((int64_t)gridDim.x * blockDim.x) >> LOG) {
     int64_t f = 0;
     int lo = INT32_MAX, hi = -1;
     const int64_t e = Bcp[j + 1];
-    for (int64_t p = Bcp[j] + sub; p < e; p += 16) {
+    for (int64_t p = Bcp[j] + sub; p < e; p += LPC) {
       const int32_t k = Bir[p];
       const int64_t a0 = Acp[k], a1 = Acp[k + 1];
       if (a1 > a0) {
@@ -278,10 +282,10 @@ __global__ void __launch_bounds__(256) k_col_stats(int64_t ncol, const int64_t* 
       }
     }
 #pragma unroll
-    for (int d = 8; d > 0; d >>= 1) {
-      f += __shfl_xor(f, d, 16);
-      lo = min(lo, __shfl_xor(lo, d, 16));
-      hi = max(hi, __shfl_xor(hi, d, 16));
+    for (int d = LPC / 2; d > 0; d >>= 1) {
+      f += __shfl_xor(f, d, LPC);
+      lo = min(lo, __shfl_xor(lo, d, LPC));
+      hi = max(hi, __shfl_xor(hi, d, LPC));
     }
     if (sub == 0) {
       flop[j] = f;
@@ -318,6 +322,8 @@ struct BinParams {
 };
 constexpr int kLaneClass = 30;   // list class of the one-lane-per-column kernels (hist[30])
 constexpr int kLaneMax = 16;     // their per-lane table size: flop <= kLaneMax
+constexpr int kLane8Class = 29;  // numeric binning: flop <= kLaneSmall (half the per-lane LDS, twice the lanes per CU)
+constexpr int kLaneSmall = 8;
 
 __device__ __forceinline__ int class_of(int64_t need, const BinParams& bp) {
   if (need <= 0) return 0;
@@ -364,15 +370,16 @@ __global__ void __launch_bounds__(256) k_bin(int64_t n, const int64_t* __restric
     if (j < n) {
       const int64_t cj = cnt[j];
       const int64_t fj = flop ? flop[j] : cj;
-      const int c = (bp.lane_max > 0 && cj > 0 && fj <= bp.lane_max) ? kLaneClass
-                                                                   : class_of(need_of(cj, span[j], bp.sym), bp);
+      const int c = (bp.lane_max > 0 && cj > 0 && fj <= bp.lane_max)
+                        ? (!bp.sym && fj <= kLaneSmall ? kLane8Class : kLaneClass)
+                        : class_of(need_of(cj, span[j], bp.sym), bp);
       cls[r] = c;
       rank[r] = atomicAdd(&s_h[c], 1u);
       if (pass == 0 && cj > heavy) atomicAdd(&s_h[31], 1u);
     }
   }
   __syncthreads();
-  const bool used = threadIdx.x < ncls || threadIdx.x == kLaneClass;
+  const bool used = threadIdx.x < ncls || threadIdx.x == kLaneClass || threadIdx.x == kLane8Class;
   if (pass == 0) {
     if ((used || threadIdx.x == 31) && s_h[threadIdx.x])
       atomicAdd(&hist[threadIdx.x], (unsigned long long)s_h[threadIdx.x]);
@@ -1494,15 +1501,17 @@ struct NumOut {
   int32_t* ovf_list;      // items whose order-preserving hash overflowed (columns, or unit ids)
 };
 
-// numeric pass of the one-lane columns (kLaneClass, see k_sym_lane)
-template <class SRT, typename V>
+// numeric pass of the one-lane columns (kLaneClass / kLane8Class, see k_sym_lane): LMAX table entries per lane
+// (its LDS slice bounds the lanes a CU holds: 16 -> 3 workgroups of 256 per CU for f64, 8 -> 5)
+template <class SRT, typename V, int LMAX>
 __global__ void __launch_bounds__(256) k_num_lane(const int32_t* __restrict__ list, int64_t count, DevCsc<V> A,
                                                   DevCsc<V> B, const int64_t* __restrict__ colptr, NumOut<V> out) {
   using Acc = typename SRT::Acc;
-  __shared__ int32_t s_rows[256 * kLaneStride];
-  __shared__ Acc s_acc[256 * kLaneStride];
-  int32_t* rows = s_rows + threadIdx.x * kLaneStride;
-  Acc* accs = s_acc + threadIdx.x * kLaneStride;
+  constexpr int STRIDE = LMAX + 1;   // odd stride: the 64 lanes' slices start in distinct banks
+  __shared__ int32_t s_rows[256 * STRIDE];
+  __shared__ Acc s_acc[256 * STRIDE];
+  int32_t* rows = s_rows + threadIdx.x * STRIDE;
+  Acc* accs = s_acc + threadIdx.x * STRIDE;
   bool aerr = false;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < count; i += (int64_t)gridDim.x * blockDim.x) {
     const int32_t j = list[i];
@@ -1512,7 +1521,7 @@ __global__ void __launch_bounds__(256) k_num_lane(const int32_t* __restrict__ li
       int y = 0;
       while (y < m && rows[y] != r) ++y;
       if (y == m) {
-        if (m == kLaneMax) return;   // cannot happen: flop <= kLaneMax
+        if (m == LMAX) return;   // cannot happen: flop <= LMAX
         rows[m] = r;
         accs[m] = SRT::identity();
         ++m;
