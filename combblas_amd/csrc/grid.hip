@@ -112,6 +112,29 @@ __global__ void k_f32_inexact(int64_t n, const double* __restrict__ v, unsigned 
   c = (unsigned long long)wave_sum64((int64_t)c);
   if (lane_id() == 0 && c) atomicAdd(bad, c);
 }
+// one pass for both narrowings: bad[0] counts values that do not survive f32, bad[1] values that are not an integer
+// in [0, 65535] (those travel as u16: a quarter of the f64 bytes -- multiplicity-valued products such as R-MAT A*A)
+__global__ void k_narrow_check(int64_t n, const double* __restrict__ v, unsigned long long* __restrict__ bad) {
+  unsigned long long c32 = 0, c16 = 0;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const double x = v[i];
+    c32 += __double_as_longlong((double)(float)x) != __double_as_longlong(x);
+    const bool in16 = x >= 0.0 && x <= 65535.0;   // false for NaN
+    c16 += !(in16 && __double_as_longlong((double)(unsigned short)x) == __double_as_longlong(x));
+  }
+  c32 = (unsigned long long)wave_sum64((int64_t)c32);
+  c16 = (unsigned long long)wave_sum64((int64_t)c16);
+  if (lane_id() == 0 && c32) atomicAdd(bad, c32);
+  if (lane_id() == 0 && c16) atomicAdd(bad + 1, c16);
+}
+__global__ void k_f64_to_u16(int64_t n, const double* __restrict__ in, unsigned short* __restrict__ out) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = (unsigned short)in[i];
+}
+__global__ void k_u16_to_f64(int64_t n, const unsigned short* __restrict__ in, double* __restrict__ out) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = (double)in[i];
+}
 __global__ void k_f64_to_f32(int64_t n, const double* __restrict__ in, float* __restrict__ out) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
     out[i] = (float)in[i];
@@ -895,9 +918,11 @@ cbg_status fiber_exchange(cbg_grid* G, const Piece& C, size_t vs, bool f64, std:
 // part (block_range of the local columns, as fiber_exchange cuts them) are multiplied first; their counts, rows
 // and values leave for the other layer as one grouped ncclSend/ncclRecv on the communication stream while the own
 // part multiplies on the compute stream; then the received partial and the own one are merged.  The same two
-// pieces and the same two-way merge as the unpipelined path, so the product is identical.  Values travel as f32
-// when both sides' messages survive the round trip (fiber_exchange's rule).  With a caller transport the
-// exchange is synchronous (no overlap, same result).
+// pieces and the same two-way merge as the unpipelined path, so the product is identical.  Each direction's values
+// travel in the narrowest lossless format of its whole message: u16 when every value is an integer in [0, 65535]
+// (multiplicities: R-MAT A*A), else f32 when every value survives the f32 round trip bit for bit, else f64 --
+// announced in the count exchange (bits 61, 62).  With a caller transport the exchange is synchronous (no
+// overlap, same result).
 cbg_status fiber_pipeline(cbg_grid* G, const cbg_dcsc_view& va, const cbg_dcsc_view& vb, cbg_semiring sr,
                           cbg_dtype dt, Piece* out, cbg_grid_stats* st) {
   cbg_ctx* ctx = G->ctx;
@@ -951,26 +976,29 @@ cbg_status fiber_pipeline(cbg_grid* G, const cbg_dcsc_view& va, const cbg_dcsc_v
     narrow = !(env && env[0] == '0');
   }
   HIPCHK(G->small.reserve(64));
-  int64_t* dsn = G->small.as<int64_t>();   // [0..1] sent flags, [2..3] received, [4] inexact count
+  int64_t* dsn = G->small.as<int64_t>();   // [0..1] sent flags, [2..3] received, [4..5] inexact counts
+  // wire format of this rank's values (each direction its own, announced with the counts): 2 = u16 (integers
+  // 0..65535), 1 = f32 (bit-exact round trip), 0 = native
+  int lvl = 0;
   if (narrow) {
-    HIPCHK(hipMemsetAsync(dsn + 4, 0, 8, cst));
-    if (Po.nnz) k_f32_inexact<<<(int)grid_for(Po.nnz, 256, kMaxGrid), 256, 0, cst>>>(
+    HIPCHK(hipMemsetAsync(dsn + 4, 0, 16, cst));
+    if (Po.nnz) k_narrow_check<<<(int)grid_for(Po.nnz, 256, kMaxGrid), 256, 0, cst>>>(
         Po.nnz, (const double*)Po.val, (unsigned long long*)(dsn + 4));
-    int64_t nb = 0;
-    HIPCHK(hipMemcpyAsync(&nb, dsn + 4, 8, hipMemcpyDeviceToHost, cst));
+    int64_t nb[2] = {0, 0};
+    HIPCHK(hipMemcpyAsync(nb, dsn + 4, 16, hipMemcpyDeviceToHost, cst));
     HIPCHK(hipStreamSynchronize(cst));
-    narrow = nb == 0;
+    lvl = nb[1] == 0 ? 2 : nb[0] == 0 ? 1 : 0;
   }
-  const int64_t kNarrowBit = 1LL << 62;
+  const int64_t kNarrowBit = 1LL << 62, kU16Bit = 1LL << 61;
   int64_t sflag[2] = {0, 0}, rflag[2] = {0, 0};
-  sflag[other] = Po.nnz | (narrow ? kNarrowBit : 0);
+  sflag[other] = Po.nnz | (lvl >= 1 ? kNarrowBit : 0) | (lvl == 2 ? kU16Bit : 0);
   HIPCHK(hipMemcpyAsync(dsn, sflag, 16, hipMemcpyHostToDevice, cst));
   const int64_t eight[2] = {8, 8};
   CBGCHK(t_alltoallv(G, CBG_GROUP_FIBER, dsn, eight, dsn + 2, eight));
   HIPCHK(hipMemcpyAsync(rflag, dsn + 2, 16, hipMemcpyDeviceToHost, cst));
   HIPCHK(hipStreamSynchronize(cst));
-  const bool all_narrow = narrow && (rflag[other] & kNarrowBit);
-  const int64_t rnnz = rflag[other] & ~kNarrowBit;
+  const int rlvl = (rflag[other] & kU16Bit) ? 2 : (rflag[other] & kNarrowBit) ? 1 : 0;
+  const int64_t rnnz = rflag[other] & ~(kNarrowBit | kU16Bit);
   // 3. receive storage (rows, then values; the counts behind them) and the exchange
   const int64_t ir_bytes = (4 * rnnz + 15) & ~15LL;
   HIPCHK(rx->ir.reserve(ir_bytes + vs * rnnz + 16));
@@ -979,14 +1007,21 @@ cbg_status fiber_pipeline(cbg_grid* G, const cbg_dcsc_view& va, const cbg_dcsc_v
   int64_t* rcnt = rx->val.as<int64_t>();
   const void* sval = Po.val;
   void* rval = Po.val ? (void*)(rbase + ir_bytes) : nullptr;
-  const int64_t wire = all_narrow ? 4 : (int64_t)vs;
-  if (all_narrow) {
-    HIPCHK(s32.reserve(4 * (Po.nnz + 1)));
-    HIPCHK(r32.reserve(4 * (rnnz + 1)));
-    if (Po.nnz) k_f64_to_f32<<<(int)grid_for(Po.nnz, 256, kMaxGrid), 256, 0, cst>>>(Po.nnz, (const double*)Po.val,
-                                                                                   s32.as<float>());
+  auto wire_of = [&](int l) { return l == 2 ? (int64_t)2 : l == 1 ? (int64_t)4 : (int64_t)vs; };
+  const int64_t wire = wire_of(lvl), wire_r = wire_of(rlvl);
+  if (lvl >= 1) {
+    HIPCHK(s32.reserve(wire * Po.nnz + 16));
+    if (Po.nnz && lvl == 2)
+      k_f64_to_u16<<<(int)grid_for(Po.nnz, 256, kMaxGrid), 256, 0, cst>>>(Po.nnz, (const double*)Po.val,
+                                                                          s32.as<unsigned short>());
+    else if (Po.nnz)
+      k_f64_to_f32<<<(int)grid_for(Po.nnz, 256, kMaxGrid), 256, 0, cst>>>(Po.nnz, (const double*)Po.val,
+                                                                          s32.as<float>());
     HIPCHK(hipGetLastError());
     sval = s32.p;
+  }
+  if (rlvl >= 1) {
+    HIPCHK(r32.reserve(wire_r * rnnz + 16));
     rval = r32.p;
   }
   const bool has_val = Po.val != nullptr;
@@ -1004,7 +1039,7 @@ cbg_status fiber_pipeline(cbg_grid* G, const cbg_dcsc_view& va, const cbg_dcsc_v
     if (Po.nnz) NCCLCHK(ncclSend(Po.ir, (size_t)(4 * Po.nnz), ncclInt8, other, f, G->cs));
     if (rnnz) NCCLCHK(ncclRecv(rbase, (size_t)(4 * rnnz), ncclInt8, other, f, G->cs));
     if (has_val && Po.nnz) NCCLCHK(ncclSend(sval, (size_t)(wire * Po.nnz), ncclInt8, other, f, G->cs));
-    if (has_val && rnnz) NCCLCHK(ncclRecv(rval, (size_t)(wire * rnnz), ncclInt8, other, f, G->cs));
+    if (has_val && rnnz) NCCLCHK(ncclRecv(rval, (size_t)(wire_r * rnnz), ncclInt8, other, f, G->cs));
     NCCLCHK(ncclGroupEnd());
     HIPCHK(hipEventRecord(G->ev_t[2], G->cs));
   } else {   // caller transport: synchronous segments (member `other` only)
@@ -1014,7 +1049,7 @@ cbg_status fiber_pipeline(cbg_grid* G, const cbg_dcsc_view& va, const cbg_dcsc_v
     sb[other] = 4 * Po.nnz; rb[other] = 4 * rnnz;
     CBGCHK(t_alltoallv(G, CBG_GROUP_FIBER, Po.ir, sb, rbase, rb));
     if (has_val) {
-      sb[other] = wire * Po.nnz; rb[other] = wire * rnnz;
+      sb[other] = wire * Po.nnz; rb[other] = wire_r * rnnz;
       CBGCHK(t_alltoallv(G, CBG_GROUP_FIBER, sval, sb, rval, rb));
     }
   }
@@ -1033,8 +1068,11 @@ cbg_status fiber_pipeline(cbg_grid* G, const cbg_dcsc_view& va, const cbg_dcsc_v
     HIPCHK(hipEventSynchronize(G->ev_t[2]));
     (void)hipEventElapsedTime(&xfer_ms, G->ev_t[1], G->ev_t[2]);
   }
-  if (all_narrow && has_val && rnnz)
+  if (rlvl == 1 && has_val && rnnz)
     k_f32_to_f64<<<(int)grid_for(rnnz, 256, kMaxGrid), 256, 0, cst>>>(rnnz, r32.as<float>(), (double*)(rbase + ir_bytes));
+  if (rlvl == 2 && has_val && rnnz)
+    k_u16_to_f64<<<(int)grid_for(rnnz, 256, kMaxGrid), 256, 0, cst>>>(rnnz, r32.as<unsigned short>(),
+                                                                     (double*)(rbase + ir_bytes));
   std::shared_ptr<Owner> co(new Owner(ctx->pool));
   HIPCHK(co->cp.reserve(8 * (myc + 1)));
   const int64_t ntiles = (myc + kScanTile - 1) / kScanTile;
