@@ -135,6 +135,92 @@ __global__ void k_u16_to_f64(int64_t n, const unsigned short* __restrict__ in, d
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
     out[i] = (double)in[i];
 }
+// Fiber rows as 16-bit gaps: within a column (rows ascending) entry i travels as d = row[i] - row[i-1] (the first
+// as row - 0) when d <= kGapMax, else as the escape code and its absolute row in a side stream of int32 (offsets:
+// a scan of the per-column escape counts, which ride in the high half of the column counts).  One wave per column.
+constexpr unsigned kGapEsc = 0xFFFFu, kGapMax = 0xFFFEu;
+
+__global__ void k_gap_count(int64_t ncol, const int64_t* __restrict__ cp, const int32_t* __restrict__ ir,
+                            int64_t* __restrict__ cnt) {   // cnt[c] |= escapes << 32 (cnt holds the column counts)
+  const int l = lane_id();
+  for (int64_t c = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / kWave; c < ncol;
+       c += ((int64_t)gridDim.x * blockDim.x) / kWave) {
+    const int64_t s = cp[c], e = cp[c + 1];
+    int64_t ne = 0;
+    for (int64_t i = s + l; i < e; i += kWave) {
+      const int64_t prev = i == s ? 0 : ir[i - 1];
+      ne += (int64_t)ir[i] - prev > (int64_t)kGapMax;
+    }
+    ne = wave_sum64(ne);
+    if (l == 0) cnt[c] |= ne << 32;
+  }
+}
+
+__global__ void k_esc_counts(int64_t n, const int64_t* __restrict__ packed, int64_t* __restrict__ esc,
+                             int64_t* __restrict__ plain) {   // split packed counts (plain may alias packed)
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t v = packed[i];
+    esc[i] = v >> 32;
+    plain[i] = v & 0xffffffffLL;
+  }
+}
+
+__global__ void k_gap_encode(int64_t ncol, const int64_t* __restrict__ cp, const int32_t* __restrict__ ir,
+                             const int64_t* __restrict__ eoff, unsigned short* __restrict__ gap,
+                             int32_t* __restrict__ esc) {
+  const int l = lane_id();
+  for (int64_t c = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / kWave; c < ncol;
+       c += ((int64_t)gridDim.x * blockDim.x) / kWave) {
+    const int64_t s = cp[c], e = cp[c + 1];
+    int64_t eo = eoff[c];
+    for (int64_t i0 = s; i0 < e; i0 += kWave) {
+      const int64_t i = i0 + l;
+      bool x = false;
+      int32_t r = 0;
+      if (i < e) {
+        r = ir[i];
+        const int64_t d = (int64_t)r - (i == s ? 0 : ir[i - 1]);
+        x = d > (int64_t)kGapMax;
+        gap[i] = x ? (unsigned short)kGapEsc : (unsigned short)d;
+      }
+      const uint64_t m = __ballot(x);
+      if (x) esc[eo + __popcll(m & ((1ull << l) - 1))] = r;
+      eo += __popcll(m);
+    }
+  }
+}
+
+__global__ void k_gap_decode(int64_t ncol, const int64_t* __restrict__ cp, const int64_t* __restrict__ eoff,
+                             const unsigned short* __restrict__ gap, const int32_t* __restrict__ esc,
+                             int32_t* __restrict__ ir) {
+  const int l = lane_id();
+  for (int64_t c = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / kWave; c < ncol;
+       c += ((int64_t)gridDim.x * blockDim.x) / kWave) {
+    const int64_t s = cp[c], e = cp[c + 1];
+    int64_t eo = eoff[c];
+    int32_t carry = 0;   // the row before the chunk (0 before the column's first entry)
+    for (int64_t i0 = s; i0 < e; i0 += kWave) {
+      const int64_t i = i0 + l;
+      const unsigned g = i < e ? gap[i] : 0u;
+      const bool x = i < e && g == kGapEsc;
+      const uint64_t m = __ballot(x);
+      const int32_t a = x ? esc[eo + __popcll(m & ((1ull << l) - 1))] : 0;
+      eo += __popcll(m);
+      // inclusive scan of the gaps (escapes add 0), then each lane adds its last escape's row (or the carry)
+      // minus the scan value at that escape
+      int64_t sc = x ? 0 : (int64_t)g;
+      sc = wave_incl_scan64(sc);
+      const uint64_t upto = m & (l == 63 ? ~0ull : ((1ull << (l + 1)) - 1));
+      const int le = upto ? 63 - __clzll(upto) : -1;   // last escape lane <= l
+      const int32_t abs_le = __shfl(a, le < 0 ? 0 : le, kWave);
+      const int64_t sc_le = __shfl(sc, le < 0 ? 0 : le, kWave);
+      const int64_t row = le < 0 ? (int64_t)carry + sc : (int64_t)abs_le + (sc - sc_le);
+      if (i < e) ir[i] = (int32_t)row;
+      carry = (int32_t)__shfl(row, kWave - 1, kWave);
+    }
+  }
+}
+
 __global__ void k_f64_to_f32(int64_t n, const double* __restrict__ in, float* __restrict__ out) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
     out[i] = (float)in[i];
@@ -931,8 +1017,10 @@ cbg_status fiber_pipeline(cbg_grid* G, const cbg_dcsc_view& va, const cbg_dcsc_v
   const int me = G->layer, other = 1 - me;
   const int64_t ncol = vb.ncol;
   const int64_t cb[3] = {0, ncol / 2, ncol};
-  PoolBuf cpo, cpm, scnt, s32, r32, tiles, scal;
-  for (PoolBuf* b : {&cpo, &cpm, &scnt, &s32, &r32, &tiles, &scal}) b->pool = ctx->pool;
+  PoolBuf cpo, cpm, scnt, s32, r32, tiles, scal, secnt, seoff, splain, sgap, sesc, rgap, resc, recnt, reoff;
+  for (PoolBuf* b : {&cpo, &cpm, &scnt, &s32, &r32, &tiles, &scal, &secnt, &seoff, &splain, &sgap, &sesc, &rgap, &resc,
+                     &recnt, &reoff})
+    b->pool = ctx->pool;
   std::shared_ptr<Owner> rx(new Owner(ctx->pool));
   StreamFence fence(cst, G->cs);   // transfers into / out of the buffers above end before they return to the pool
   // column-range views of B: rebased colptr, rows and values from cp[c0]
@@ -975,30 +1063,61 @@ cbg_status fiber_pipeline(cbg_grid* G, const cbg_dcsc_view& va, const cbg_dcsc_v
     const char* env = std::getenv("CBG_FIBER_NARROW");
     narrow = !(env && env[0] == '0');
   }
-  HIPCHK(G->small.reserve(64));
-  int64_t* dsn = G->small.as<int64_t>();   // [0..1] sent flags, [2..3] received, [4..5] inexact counts
+  HIPCHK(G->small.reserve(128));
+  int64_t* dsn = G->small.as<int64_t>();   // [0..3] sent (flags, escapes), [4..7] received, [8..9] inexact counts
+  // rows as 16-bit gaps (k_gap_encode; CBG_FIBER_GAPS=0 sends int32 rows): escape counts packed into the column
+  // counts, their offsets by a scan, the escape total read back with the value verdict below
+  const char* genv = std::getenv("CBG_FIBER_GAPS");
+  const bool gaps = !(genv && genv[0] == '0') && oc > 0 && Po.nnz > 0;
+  if (gaps) {
+    HIPCHK(secnt.reserve(8 * (oc + 1)));
+    HIPCHK(splain.reserve(8 * (oc + 1)));
+    HIPCHK(seoff.reserve(8 * (oc + 1)));
+    const int64_t nt = (oc + kScanTile - 1) / kScanTile;
+    HIPCHK(tiles.reserve(8 * (nt + 1)));
+    HIPCHK(scal.reserve(16));
+    k_gap_count<<<(int)grid_for(oc, 4, kMaxGrid * 2), 256, 0, cst>>>(oc, Po.cp, Po.ir, scnt.as<int64_t>());
+    k_esc_counts<<<(int)grid_for(oc, 256, kMaxGrid), 256, 0, cst>>>(oc, scnt.as<int64_t>(), secnt.as<int64_t>(),
+                                                                   splain.as<int64_t>());
+    k_scan_tiles<<<(int)nt, 256, 0, cst>>>(oc, secnt.as<int64_t>(), tiles.as<int64_t>());
+    k_scan_sums<<<1, 1024, 0, cst>>>(nt, tiles.as<int64_t>(), scal.as<int64_t>());
+    k_scan_apply<<<(int)nt, 256, 0, cst>>>(oc, secnt.as<int64_t>(), tiles.as<int64_t>(), seoff.as<int64_t>());
+    HIPCHK(hipGetLastError());
+  }
   // wire format of this rank's values (each direction its own, announced with the counts): 2 = u16 (integers
   // 0..65535), 1 = f32 (bit-exact round trip), 0 = native
   int lvl = 0;
+  int64_t sE = 0;
   if (narrow) {
-    HIPCHK(hipMemsetAsync(dsn + 4, 0, 16, cst));
+    HIPCHK(hipMemsetAsync(dsn + 8, 0, 16, cst));
     if (Po.nnz) k_narrow_check<<<(int)grid_for(Po.nnz, 256, kMaxGrid), 256, 0, cst>>>(
-        Po.nnz, (const double*)Po.val, (unsigned long long*)(dsn + 4));
-    int64_t nb[2] = {0, 0};
-    HIPCHK(hipMemcpyAsync(nb, dsn + 4, 16, hipMemcpyDeviceToHost, cst));
-    HIPCHK(hipStreamSynchronize(cst));
-    lvl = nb[1] == 0 ? 2 : nb[0] == 0 ? 1 : 0;
+        Po.nnz, (const double*)Po.val, (unsigned long long*)(dsn + 8));
   }
-  const int64_t kNarrowBit = 1LL << 62, kU16Bit = 1LL << 61;
-  int64_t sflag[2] = {0, 0}, rflag[2] = {0, 0};
-  sflag[other] = Po.nnz | (lvl >= 1 ? kNarrowBit : 0) | (lvl == 2 ? kU16Bit : 0);
-  HIPCHK(hipMemcpyAsync(dsn, sflag, 16, hipMemcpyHostToDevice, cst));
-  const int64_t eight[2] = {8, 8};
-  CBGCHK(t_alltoallv(G, CBG_GROUP_FIBER, dsn, eight, dsn + 2, eight));
-  HIPCHK(hipMemcpyAsync(rflag, dsn + 2, 16, hipMemcpyDeviceToHost, cst));
+  int64_t nb[2] = {0, 0};
+  if (narrow) HIPCHK(hipMemcpyAsync(nb, dsn + 8, 16, hipMemcpyDeviceToHost, cst));
+  if (gaps) HIPCHK(hipMemcpyAsync(&sE, seoff.as<int64_t>() + oc, 8, hipMemcpyDeviceToHost, cst));
+  if (narrow || gaps) HIPCHK(hipStreamSynchronize(cst));
+  if (narrow) lvl = nb[1] == 0 ? 2 : nb[0] == 0 ? 1 : 0;
+  if (gaps) {
+    HIPCHK(sgap.reserve(2 * Po.nnz + 16));
+    HIPCHK(sesc.reserve(4 * sE + 16));
+    k_gap_encode<<<(int)grid_for(oc, 4, kMaxGrid * 2), 256, 0, cst>>>(oc, Po.cp, Po.ir, seoff.as<int64_t>(),
+                                                                      sgap.as<unsigned short>(), sesc.as<int32_t>());
+    HIPCHK(hipGetLastError());
+  }
+  const int64_t kNarrowBit = 1LL << 62, kU16Bit = 1LL << 61, kGapBit = 1LL << 60;
+  int64_t sflag[4] = {0, 0, 0, 0}, rflag[4] = {0, 0, 0, 0};
+  sflag[2 * other] = Po.nnz | (lvl >= 1 ? kNarrowBit : 0) | (lvl == 2 ? kU16Bit : 0) | (gaps ? kGapBit : 0);
+  sflag[2 * other + 1] = sE;
+  HIPCHK(hipMemcpyAsync(dsn, sflag, 32, hipMemcpyHostToDevice, cst));
+  const int64_t sixteen[2] = {16, 16};
+  CBGCHK(t_alltoallv(G, CBG_GROUP_FIBER, dsn, sixteen, dsn + 4, sixteen));
+  HIPCHK(hipMemcpyAsync(rflag, dsn + 4, 32, hipMemcpyDeviceToHost, cst));
   HIPCHK(hipStreamSynchronize(cst));
-  const int rlvl = (rflag[other] & kU16Bit) ? 2 : (rflag[other] & kNarrowBit) ? 1 : 0;
-  const int64_t rnnz = rflag[other] & ~(kNarrowBit | kU16Bit);
+  const int64_t rf = rflag[2 * other];
+  const int rlvl = (rf & kU16Bit) ? 2 : (rf & kNarrowBit) ? 1 : 0;
+  const bool rgaps = (rf & kGapBit) != 0;
+  const int64_t rnnz = rf & ~(kNarrowBit | kU16Bit | kGapBit), rE = rflag[2 * other + 1];
   // 3. receive storage (rows, then values; the counts behind them) and the exchange
   const int64_t ir_bytes = (4 * rnnz + 15) & ~15LL;
   HIPCHK(rx->ir.reserve(ir_bytes + vs * rnnz + 16));
@@ -1024,9 +1143,21 @@ cbg_status fiber_pipeline(cbg_grid* G, const cbg_dcsc_view& va, const cbg_dcsc_v
     HIPCHK(r32.reserve(wire_r * rnnz + 16));
     rval = r32.p;
   }
+  // rows: int32, or the 16-bit gaps and the escaped rows (escape buffers always allocated: a transport may be
+  // handed them with zero bytes)
+  HIPCHK(sesc.reserve(16));
+  HIPCHK(resc.reserve(16));
+  const void* srow = gaps ? sgap.p : (const void*)Po.ir;
+  const int64_t srow_b = gaps ? 2 * Po.nnz : 4 * Po.nnz, rrow_b = rgaps ? 2 * rnnz : 4 * rnnz;
+  void* rrow = rbase;
+  if (rgaps) {
+    HIPCHK(rgap.reserve(2 * rnnz + 16));
+    HIPCHK(resc.reserve(4 * rE + 16));
+    rrow = rgap.p;
+  }
   const bool has_val = Po.val != nullptr;
   const double t_setup = now_ms() - t0;
-  if (st) for (int m = 0; m < 2; ++m) if (m == other) st->fiber_bytes += (4 + (has_val ? wire : 0)) * Po.nnz + 8 * oc;
+  if (st) st->fiber_bytes += srow_b + (gaps ? 4 * sE : 0) + (has_val ? wire : 0) * Po.nnz + 8 * oc;
   const bool async = G->rccl;
   if (async) {
     HIPCHK(hipEventRecord(G->ev_t[0], cst));   // counts and narrowed values are ready
@@ -1036,8 +1167,10 @@ cbg_status fiber_pipeline(cbg_grid* G, const cbg_dcsc_view& va, const cbg_dcsc_v
     NCCLCHK(ncclGroupStart());
     if (oc) NCCLCHK(ncclSend(scnt.p, (size_t)(8 * oc), ncclInt8, other, f, G->cs));
     if (myc) NCCLCHK(ncclRecv(rcnt, (size_t)(8 * myc), ncclInt8, other, f, G->cs));
-    if (Po.nnz) NCCLCHK(ncclSend(Po.ir, (size_t)(4 * Po.nnz), ncclInt8, other, f, G->cs));
-    if (rnnz) NCCLCHK(ncclRecv(rbase, (size_t)(4 * rnnz), ncclInt8, other, f, G->cs));
+    if (Po.nnz) NCCLCHK(ncclSend(srow, (size_t)srow_b, ncclInt8, other, f, G->cs));
+    if (rnnz) NCCLCHK(ncclRecv(rrow, (size_t)rrow_b, ncclInt8, other, f, G->cs));
+    if (gaps && sE) NCCLCHK(ncclSend(sesc.p, (size_t)(4 * sE), ncclInt8, other, f, G->cs));
+    if (rgaps && rE) NCCLCHK(ncclRecv(resc.p, (size_t)(4 * rE), ncclInt8, other, f, G->cs));
     if (has_val && Po.nnz) NCCLCHK(ncclSend(sval, (size_t)(wire * Po.nnz), ncclInt8, other, f, G->cs));
     if (has_val && rnnz) NCCLCHK(ncclRecv(rval, (size_t)(wire_r * rnnz), ncclInt8, other, f, G->cs));
     NCCLCHK(ncclGroupEnd());
@@ -1046,8 +1179,10 @@ cbg_status fiber_pipeline(cbg_grid* G, const cbg_dcsc_view& va, const cbg_dcsc_v
     int64_t sb[2] = {0, 0}, rb[2] = {0, 0};
     sb[other] = 8 * oc; rb[other] = 8 * myc;
     CBGCHK(t_alltoallv(G, CBG_GROUP_FIBER, scnt.p, sb, rcnt, rb));
-    sb[other] = 4 * Po.nnz; rb[other] = 4 * rnnz;
-    CBGCHK(t_alltoallv(G, CBG_GROUP_FIBER, Po.ir, sb, rbase, rb));
+    sb[other] = srow_b; rb[other] = rrow_b;
+    CBGCHK(t_alltoallv(G, CBG_GROUP_FIBER, srow, sb, rrow, rb));
+    sb[other] = gaps ? 4 * sE : 0; rb[other] = rgaps ? 4 * rE : 0;
+    if (sb[other] || rb[other]) CBGCHK(t_alltoallv(G, CBG_GROUP_FIBER, sesc.p, sb, resc.p, rb));
     if (has_val) {
       sb[other] = wire * Po.nnz; rb[other] = wire_r * rnnz;
       CBGCHK(t_alltoallv(G, CBG_GROUP_FIBER, sval, sb, rval, rb));
@@ -1078,6 +1213,14 @@ cbg_status fiber_pipeline(cbg_grid* G, const cbg_dcsc_view& va, const cbg_dcsc_v
   const int64_t ntiles = (myc + kScanTile - 1) / kScanTile;
   HIPCHK(tiles.reserve(8 * (ntiles + 1)));
   HIPCHK(scal.reserve(16));
+  if (rgaps && myc > 0) {   // escape counts out of the packed counts, their offsets
+    HIPCHK(recnt.reserve(8 * (myc + 1)));
+    HIPCHK(reoff.reserve(8 * (myc + 1)));
+    k_esc_counts<<<(int)grid_for(myc, 256, kMaxGrid), 256, 0, cst>>>(myc, rcnt, recnt.as<int64_t>(), rcnt);
+    k_scan_tiles<<<(int)ntiles, 256, 0, cst>>>(myc, recnt.as<int64_t>(), tiles.as<int64_t>());
+    k_scan_sums<<<1, 1024, 0, cst>>>(ntiles, tiles.as<int64_t>(), scal.as<int64_t>());
+    k_scan_apply<<<(int)ntiles, 256, 0, cst>>>(myc, recnt.as<int64_t>(), tiles.as<int64_t>(), reoff.as<int64_t>());
+  }
   if (myc > 0) {
     k_scan_tiles<<<(int)ntiles, 256, 0, cst>>>(myc, rcnt, tiles.as<int64_t>());
     k_scan_sums<<<1, 1024, 0, cst>>>(ntiles, tiles.as<int64_t>(), scal.as<int64_t>());
@@ -1085,6 +1228,10 @@ cbg_status fiber_pipeline(cbg_grid* G, const cbg_dcsc_view& va, const cbg_dcsc_v
   } else {
     HIPCHK(hipMemsetAsync(co->cp.p, 0, 8, cst));
   }
+  if (rgaps && myc > 0)
+    k_gap_decode<<<(int)grid_for(myc, 4, kMaxGrid * 2), 256, 0, cst>>>(myc, co->cp.as<int64_t>(), reoff.as<int64_t>(),
+                                                                       rgap.as<unsigned short>(), resc.as<int32_t>(),
+                                                                       (int32_t*)rbase);
   HIPCHK(hipGetLastError());
   Piece Pr;
   Pr.nrow = Pm.nrow; Pr.ncol = myc; Pr.nnz = rnnz;

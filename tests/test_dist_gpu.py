@@ -116,3 +116,13 @@ def test_galerkin_reference_restriction_multirank_gpu(world, port, kind):
     own RCCL node) -- every rank's piece of both products equal to the reference's."""
     from dist_support import run_galerkin_case
     spawn_case(world, kind, ["SUMMA3D", "multiply"], port + (10 if kind != "gpu" else 0), body=run_galerkin_case)
+
+
+@pytest.mark.parametrize("kind,port", [("gpu", 29691), ("gpu-rccl-net", 29692)])
+def test_fiber_row_gaps_tall_sparse(kind, port):
+    """1x1x2 fiber exchange of tall, very sparse products through the 16-bit row gaps (k_gap_encode /
+    k_gap_decode): first rows above 65534 and gaps above it (escapes, also mid-column), columns of one 64-entry
+    chunk and of hundreds; integer values (u16 on the wire), compared exactly with scipy's product."""
+    spawn_case(2, kind, [(2000000, 3000, 96, 5e-6, 0.002, 5),
+                         (1000000, 3000, 120, 2e-5, 0.002, 7),
+                         (300000, 500, 64, 1e-3, 0.2, 9)], port)
