@@ -156,28 +156,40 @@ __global__ void k_member_len(int64_t nnzr, const int32_t* __restrict__ rir, cons
 // entries start at moff[p]) are loaded into LDS as keys (agg(i) << 32 | position) with values
 // R(i,I) A(i,j) R(j,J), bitonic-sorted, and every run of one row is summed in position order
 // (deterministic); count pass -> cnt[J], fill pass -> sorted (row, value) at ccp[J].  Aggregates with
-// more than kRapCap entries are counted in *overflow (the caller falls back to two SpGEMMs).
-constexpr int kRapCap = 512, kRapMem = 64;
+// more than kRapCapBig entries are counted in *overflow (the caller falls back to two SpGEMMs).
+constexpr int kRapCap = 512, kRapCapBig = 2048, kRapMem = 64;
 
-__global__ void __launch_bounds__(64) k_rap_agg(int64_t nagg, const int64_t* __restrict__ rcp,
+// CAP = kRapCap: every aggregate; one with more entries goes to olist (when given) for the CAP = kRapCapBig pass
+// (list = olist, count = its length), and only an aggregate above that is counted in *overflow.
+template <int CAP>
+__global__ void __launch_bounds__(64) k_rap_agg(int64_t nagg, const int32_t* __restrict__ list,
+                                                const unsigned long long* __restrict__ nlist,
+                                                int32_t* __restrict__ olist, unsigned long long* __restrict__ nolist,
+                                                const int64_t* __restrict__ rcp,
                                                 const int32_t* __restrict__ rir, const int64_t* __restrict__ acp,
                                                 const int32_t* __restrict__ air, const double* __restrict__ aval,
                                                 const int32_t* __restrict__ agg, const double* __restrict__ rv,
                                                 const int64_t* __restrict__ moff, int64_t* __restrict__ cnt,
                                                 int32_t* __restrict__ trow, double* __restrict__ tval, int64_t cap,
                                                 unsigned long long* __restrict__ overflow) {
-  __shared__ uint64_t key[kRapCap];
-  __shared__ double val[kRapCap];
+  __shared__ uint64_t key[CAP];
+  __shared__ double val[CAP];
   __shared__ int32_t s_mo[kRapMem + 1];   // members' entry offsets (relative to the aggregate's first entry)
   __shared__ int64_t s_q0[kRapMem];       // members' A column starts
   __shared__ double s_rvj[kRapMem];       // R(j, J)
   const int lane = threadIdx.x;
-  for (int64_t J = blockIdx.x; J < nagg; J += gridDim.x) {
+  const int64_t nj = list ? (int64_t)*nlist : nagg;
+  for (int64_t i = blockIdx.x; i < nj; i += gridDim.x) {
+    const int64_t J = list ? list[i] : i;
     const int64_t p0 = rcp[J], p1 = rcp[J + 1];
     const int64_t base = moff[p0];
-    const int t = (int)min<int64_t>(moff[p1] - base, kRapCap + 1);
-    if (t > kRapCap || base + t > cap) {   // uniform; past `cap` only for an R that is no aggregation
-      if (lane == 0) { atomicAdd(overflow, 1ull); cnt[J] = 0; }
+    const int t = (int)min<int64_t>(moff[p1] - base, CAP + 1);
+    if (t > CAP || base + t > cap) {   // uniform; past `cap` only for an R that is no aggregation
+      if (lane == 0) {
+        cnt[J] = 0;
+        if (olist && base + t <= cap) olist[atomicAdd(nolist, 1ull)] = (int32_t)J;
+        else atomicAdd(overflow, 1ull);
+      }
       continue;
     }
     int N = 64;
@@ -803,8 +815,14 @@ extern "C" cbg_status cbg_galerkin_rap(cbg_ctx* ctx, const cbg_dcsc_view* Av, co
   std::unique_ptr<Owner> own(new Owner(ctx->pool));
   HIPCHK(own->cp.reserve(8 * (nagg + 1)));
   if (nnzr == n) {
-    k_rap_agg<<<ga, 64, 0, st>>>(nagg, R.cp, R.ir, A.cp, A.ir, A.val, agg, rv, moff, len, trow, tval, nraw,
-                                 (unsigned long long*)(sc + 2));
+    // aggregates above kRapCap entries are listed for the kRapCapBig pass (device count, no read-back)
+    HIPCHK(w[8].reserve(4 * (nagg + 1)));
+    unsigned long long* nbig = (unsigned long long*)(sc + 4);
+    k_rap_agg<kRapCap><<<ga, 64, 0, st>>>(nagg, nullptr, nullptr, w[8].as<int32_t>(), nbig, R.cp, R.ir, A.cp, A.ir,
+                                          A.val, agg, rv, moff, len, trow, tval, nraw, (unsigned long long*)(sc + 2));
+    k_rap_agg<kRapCapBig><<<1024, 64, 0, st>>>(nagg, w[8].as<int32_t>(), nbig, nullptr, nullptr, R.cp, R.ir, A.cp,
+                                               A.ir, A.val, agg, rv, moff, len, trow, tval, nraw,
+                                               (unsigned long long*)(sc + 2));
     HIPCHK(hipGetLastError());
     CBGCHK(scan_counts_async(st, nagg, len, own->cp.as<int64_t>(), sc + 3, &w[7]));
   }
@@ -812,7 +830,7 @@ extern "C" cbg_status cbg_galerkin_rap(cbg_ctx* ctx, const cbg_dcsc_view* Av, co
   HIPCHK(hipMemcpyAsync(h, sc, 32, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
   if (nnzr != n || h[0] || h[1] != nraw) return CBG_EUNSUP;   // not an aggregation: two products instead
-  if (h[2]) return CBG_EUNSUP;   // an aggregate gathers more than kRapCap entries: two products instead
+  if (h[2]) return CBG_EUNSUP;   // an aggregate gathers more than kRapCapBig entries: two products instead
   const int64_t nnzc = h[3];
   HIPCHK(own->ir.reserve(4 * (nnzc + 1)));
   HIPCHK(own->val.reserve(8 * (nnzc + 1)));

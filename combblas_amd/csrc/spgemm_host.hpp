@@ -148,7 +148,7 @@ struct cbg_ctx {
   DevBuf hrows, hmode, hpoff, urows;   // symbolic -> numeric row handoff of heavy columns
   DevBuf oitems;                       // heavy items the rows-known kernel does not take
   DevBuf aos;                          // A's rows and values interleaved (k_num_heavy_known gathers)
-  DevBuf gal[8];                       // fused Galerkin product scratch (galerkin.hip)
+  DevBuf gal[9];                       // fused Galerkin product scratch (galerkin.hip)
   void* pin = nullptr;                 // 16 KB of pinned host memory: small read-backs (bin counts, scalars)
   int ncu = 0;                         // compute units (persistent grids)
   int row_handoff = -1;                // -1: read CBG_ROW_HANDOFF once (default on)

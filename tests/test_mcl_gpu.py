@@ -307,6 +307,27 @@ def test_galerkin_rap_large_aggregate_falls_back(gpu_ctx):
         assert_same_product(host(C, 8), OC, "f64", what="fallback RtAR")
 
 
+def test_galerkin_rap_big_aggregates_stay_fused(gpu_ctx):
+    """Aggregates gathering 513..2048 entries of A take the fused kernel's second pass (2048-entry LDS sort)
+    instead of the two-product fallback: C.multiplies = nnz(A), same product as the two products."""
+    G = _random_symmetric(600, 0.02, 6)
+    n = G.nrow
+    A = Csc(n, n, G.cp, G.ir, np.linspace(0.5, 1.5, G.nnz))
+    agg = np.r_[np.zeros(60, np.int64), np.ones(50, np.int64), 2 + np.arange(490) % 40]   # ~1400 and ~1200 entries
+    import scipy.sparse as sp
+    Rs = sp.csc_matrix((np.linspace(0.5, 2.0, n), (np.arange(n), agg)), shape=(n, 42))
+    Rs.sort_indices()
+    R = Csc(n, 42, Rs.indptr, Rs.indices, Rs.data)
+    sizes = np.bincount(agg, weights=np.diff(G.cp))
+    assert sizes.max() > 512 and sizes.max() <= 2048, sizes.max()
+    C = cb.GalerkinRAP(up(gpu_ctx, A), up(gpu_ctx, R))
+    assert C.multiplies == A.nnz   # the fused pass ran
+    Rt = _transpose(R)
+    ORA, _, _ = oracle_spgemm(Rt, A, "plus_times", "f64")
+    OC, _, _ = oracle_spgemm(ORA, R, "plus_times", "f64")
+    assert_same_product(host(C, 42), OC, "f64", what="fused RtAR, big aggregates")
+
+
 # ------------------------------------------------------------------ the reference's RestrictionOp (f3)
 RESTRICTION_CASES = ["poisson6", "poisson12", "poisson80", "g500_s10", "unsym700"]
 
