@@ -297,14 +297,21 @@ hipError_t launch_sym_block(hipStream_t st, const int32_t* l, int64_t n, const i
   return hipGetLastError();
 }
 template <int NT>
-hipError_t launch_sym_part(hipStream_t st, const PartItem* items, const int* count_dev, int64_t cap,
+hipError_t launch_sym_part(hipStream_t st, const PartItem* items, const int* count_dev, int64_t cap, int64_t annz,
                            const int64_t* Acp, const int32_t* Air, const int64_t* Bcp, const int32_t* Bir,
                            const int2* span, const Split& spl, int64_t* nnz, const HeavyOut& ho) {
   const size_t lds = sym_part_lds<NT>();
-  hipError_t e = launch_cfg_lds((const void*)k_sym_part<NT>, lds);
+  // 16-byte row loads (RowLd4) unless CBG_SYM_VEC4=0 or A has fewer than 4 entries
+  static const bool vec_env = [] { const char* e = std::getenv("CBG_SYM_VEC4"); return !(e && e[0] == '0'); }();
+  const bool vec = vec_env && kGroupSym == 4 && annz >= 4;
+  const void* kf = vec ? (const void*)k_sym_part<NT, true> : (const void*)k_sym_part<NT, false>;
+  hipError_t e = launch_cfg_lds(kf, lds);
   if (e != hipSuccess) return e;
-  k_sym_part<NT><<<(int)grid_for(cap, 1, kMaxGrid * 2), NT, lds, st>>>(items, count_dev, Acp, Air, Bcp, Bir, span,
-                                                                       spl, nnz, ho);
+  const int g = (int)grid_for(cap, 1, kMaxGrid * 2);
+  if (vec)
+    k_sym_part<NT, true><<<g, NT, lds, st>>>(items, count_dev, annz, Acp, Air, Bcp, Bir, span, spl, nnz, ho);
+  else
+    k_sym_part<NT, false><<<g, NT, lds, st>>>(items, count_dev, annz, Acp, Air, Bcp, Bir, span, spl, nnz, ho);
   return hipGetLastError();
 }
 template <int LOGT, class SRT, typename V, bool UNIT>
@@ -562,7 +569,7 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
       k_part_items<<<(int)grid_for(nwide, 256, kMaxGrid), 256, 0, st>>>(L(kWideClass), nwide, slog <= kPartLog ? kMaxParts : 0, span, ho,
                                                                          ctx->parts.as<PartItem>(), nparts,
                                                                          ctx->wide_win.as<int32_t>(), nwin);
-      e = launch_sym_part<kPartNT>(st, ctx->parts.as<PartItem>(), nparts, nwide * kMaxParts, A.cp, A.ir, B.cp, B.ir,
+      e = launch_sym_part<kPartNT>(st, ctx->parts.as<PartItem>(), nparts, nwide * kMaxParts, A.nnz, A.cp, A.ir, B.cp, B.ir,
                                span, spl, nnz, ho);
       const int64_t nw_cap = slog <= kPartLog ? n(11) : nwide;
       if (nw_cap && e == hipSuccess) {

@@ -451,6 +451,30 @@ __global__ void __launch_bounds__(256) k_sym_lane(const int32_t* __restrict__ li
 // multiplies whatever the (power-law) segment lengths, consecutive lanes read consecutive A
 // entries of one segment (coalesced), and each lane keeps U independent gathers in flight.
 // ld(q) loads what an insert needs; ins(item, bv, q, b) inserts it.
+// A row loader with a 16-byte path: expand_staged issues ONE global_load_dwordx4 (4-byte alignment suffices on
+// gfx950) for a lane's group of 4 consecutive A entries instead of four dword loads.  Near the end of A.ir the
+// load is moved back to stay in bounds and the entries shifted (the group's entries beyond its segment are
+// never inserted, so what they hold does not matter; only the array end needs care).
+typedef int32_t cbg_v4i __attribute__((ext_vector_type(4)));
+struct RowLd4 {
+  const int32_t* ir;
+  int64_t n;   // entries of A (>= 4 for the vector path)
+  __device__ __forceinline__ int32_t operator()(int64_t q) const { return ir[q]; }
+  __device__ __forceinline__ cbg_v4i vec4(int64_t q) const {
+    const int64_t qv = q + 4 <= n ? q : n - 4;
+    cbg_v4i v;
+    __builtin_memcpy(&v, ir + qv, 16);
+    const int d = (int)(q - qv);
+    if (d == 1) v = cbg_v4i{v.y, v.z, v.w, v.w};
+    else if (d == 2) v = cbg_v4i{v.z, v.w, v.w, v.w};
+    else if (d == 3) v = cbg_v4i{v.w, v.w, v.w, v.w};
+    return v;
+  }
+};
+template <class F> struct HasVec4 { static constexpr bool value = false; };
+template <> struct HasVec4<RowLd4> { static constexpr bool value = true; };
+template <class F> struct HasVec2 { static constexpr bool value = false; };   // (row, value) pairs: NumLd2
+
 template <typename V>
 struct SegBuf {         // LDS, NT entries each (+ scan scratch for block mode)
   int64_t* qb;          // segment start (A index)
@@ -577,8 +601,13 @@ __device__ __forceinline__ void expand_staged(const SegBuf<V>& sb, int tid, int6
       nv[u] = g0 + (int64_t)u * NT + tid < F ? (int)min<int64_t>(G, sb.len[sg] - k0) : 0;
       const int64_t qs = nv[u] > 0 ? qq[u] : 0;
       const int last = nv[u] > 0 ? nv[u] - 1 : 0;
+      if constexpr (G == 4 && HasVec4<LdF>::value) {
+        const cbg_v4i x = ld.vec4(qs);
+        it[u][0] = x.x; it[u][1] = x.y; it[u][2] = x.z; it[u][3] = x.w;
+      } else {
 #pragma unroll
-      for (int i = 0; i < G; ++i) it[u][i] = ld(qs + min(i, last));
+        for (int i = 0; i < G; ++i) it[u][i] = ld(qs + min(i, last));
+      }
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -620,8 +649,12 @@ __device__ __forceinline__ void expand_staged_slots(const SegBuf<V>& sb, int tid
       nv[u] = g0 + (int64_t)u * NT + tid < F ? (int)min<int64_t>(G, sb.len[sg] - k0) : 0;
       const int64_t qs = nv[u] > 0 ? qq[u] : 0;
       const int last = nv[u] > 0 ? nv[u] - 1 : 0;
+      if constexpr (G == 2 && HasVec2<LdF>::value) {
+        ld.vec2(qs, it[u][0], it[u][1]);
+      } else {
 #pragma unroll
-      for (int i = 0; i < G; ++i) it[u][i] = ld(qs + min(i, last));
+        for (int i = 0; i < G; ++i) it[u][i] = ld(qs + min(i, last));
+      }
     }
 #pragma unroll
     for (int u = 0; u < U; ++u)
@@ -1052,9 +1085,9 @@ constexpr size_t sym_part_lds() {
          (size_t)((1 << (kPartLog - kSubLogMin)) + 8) * 4 + 64;
 }
 
-template <int NT>
+template <int NT, bool VEC>
 __global__ void __launch_bounds__(NT) k_sym_part(const PartItem* __restrict__ items, const int* __restrict__ count_dev,
-                                                 const int64_t* __restrict__ Acp, const int32_t* __restrict__ Air,
+                                                 int64_t annz, const int64_t* __restrict__ Acp, const int32_t* __restrict__ Air,
                                                  const int64_t* __restrict__ Bcp, const int32_t* __restrict__ Bir,
                                                  const int2* __restrict__ span, Split spl, int64_t* __restrict__ nnz,
                                                  HeavyOut ho) {
@@ -1102,6 +1135,7 @@ __global__ void __launch_bounds__(NT) k_sym_part(const PartItem* __restrict__ it
       }
     };
     auto ld = [&](int64_t q) { return Air[q]; };
+    const RowLd4 ld4{Air, annz};
     auto ins = [&](int32_t r, uint8_t, int64_t, int64_t) {
       const uint32_t o = (uint32_t)(r - r0);
       if (o < (1u << kPartLog)) {
@@ -1113,7 +1147,8 @@ __global__ void __launch_bounds__(NT) k_sym_part(const PartItem* __restrict__ it
 #endif
       }
     };
-    for_each_multiply<NT, false, kUnrollSym, kGroupSym, uint8_t>(bs, be, sb, seg, ld, ins);
+    if constexpr (VEC) for_each_multiply<NT, false, kUnrollSym, kGroupSym, uint8_t>(bs, be, sb, seg, ld4, ins);
+    else for_each_multiply<NT, false, kUnrollSym, kGroupSym, uint8_t>(bs, be, sb, seg, ld, ins);
     __syncthreads();
     STAMP(27);
     int c = 0;
@@ -1616,6 +1651,31 @@ struct NumItem {
   int32_t r;
   V a;
 };
+
+// (row, value) loader with a paired path: expand_staged_slots loads a lane's group of 2 consecutive A entries as
+// one 8-byte row load and one 2*sizeof(V) value load (CBG_NUM_VEC2, default on) instead of two of each.  At the
+// end of A the pair is moved back to stay in bounds (the entry past the segment is never accumulated).
+#ifndef CBG_NUM_VEC2
+#define CBG_NUM_VEC2 1
+#endif
+template <typename V, bool AV>
+struct NumLd2 {
+  const int32_t* ir;
+  const V* val;
+  int64_t n;   // entries of A (>= 2 for the paired path)
+  __device__ __forceinline__ NumItem<V> operator()(int64_t q) const { return NumItem<V>{ir[q], AV ? val[q] : V(1)}; }
+  __device__ __forceinline__ void vec2(int64_t q, NumItem<V>& x, NumItem<V>& y) const {
+    const int64_t qv = q + 2 <= n ? q : n - 2;
+    int32_t r[2];
+    V v[2] = {V(1), V(1)};
+    __builtin_memcpy(r, ir + qv, 8);
+    if (AV) __builtin_memcpy(v, val + qv, 2 * sizeof(V));
+    if (q != qv) { r[0] = r[1]; v[0] = v[1]; }
+    x = NumItem<V>{r[0], v[0]};
+    y = NumItem<V>{r[1], v[1]};
+  }
+};
+template <typename V, bool AV> struct HasVec2<NumLd2<V, AV>> { static constexpr bool value = true; };
 
 // Compaction of an order-preserving hash table of Tcap slots by NT lanes.
 // out position of an occupied slot s = (#occupied before its run start) + (#keys in its run smaller).
@@ -2425,9 +2485,7 @@ __global__ void __launch_bounds__(NT) k_num_heavy_known(const KnownUnit* __restr
       else if (has1) fetch(hdr[slot ^ 1], 0, pa0, pa1, pbv);
       const int64_t F = stage_segments<NT, false, CBG_GROUP_KNOWN, V>(sb, a0, a1, bv);
       STAMP(3);
-      expand_staged_slots<NT, CBG_UNROLL_KNOWN, CBG_GROUP_KNOWN, V>(
-          sb, tid, F, H.bs + c, (int)min<int64_t>(NT, H.nb - c),
-          [&](int64_t q) {   // AV: no pointer test per load; AOS: one load for the row and the value
+      auto ld_one = [&](int64_t q) {   // AV: no pointer test per load; AOS: one load for the row and the value
             if constexpr (AOS && sizeof(V) == 8) {   // one dwordx4: (row, pad, value)
               typedef int v4i __attribute__((ext_vector_type(4)));
               const v4i w = *(const v4i*)(arv + q);
@@ -2445,17 +2503,29 @@ __global__ void __launch_bounds__(NT) k_num_heavy_known(const KnownUnit* __restr
             } else {
               return NumItem<V>{A.ir[q], AV ? A.val[q] : V(1)};
             }
-          },
-          [&](const NumItem<V>& it) -> int {
+          };
+      auto slotf = [&](const NumItem<V>& it) -> int {
             const uint32_t o = (uint32_t)(it.r - lo);
             const bool ok = o <= (uint32_t)(hi - lo);
             const uint32_t oc = ok ? o : 0u;
             const int sl = (int)pre[oc >> 6] + __popcll(bm2[oc >> 6] & ((1ull << (oc & 63)) - 1ull));
             return ok ? sl : -1;
-          },
-          [&](int sl, const NumItem<V>& it, V bv2, int64_t q, int64_t b) {
+          };
+      auto accf = [&](int sl, const NumItem<V>& it, V bv2, int64_t q, int64_t b) {
             SRT::acc(&vals[sl], SRT::mul(it.a, bv2, q, b));
-          });
+          };
+      const NumLd2<V, AV> ld2{A.ir, A.val, A.nnz};
+      if constexpr (!AOS && CBG_NUM_VEC2 && CBG_GROUP_KNOWN == 2) {
+        if (A.nnz >= 2)   // uniform
+          expand_staged_slots<NT, CBG_UNROLL_KNOWN, CBG_GROUP_KNOWN, V>(sb, tid, F, H.bs + c,
+                                                                      (int)min<int64_t>(NT, H.nb - c), ld2, slotf, accf);
+        else
+          expand_staged_slots<NT, CBG_UNROLL_KNOWN, CBG_GROUP_KNOWN, V>(sb, tid, F, H.bs + c,
+                                                                      (int)min<int64_t>(NT, H.nb - c), ld_one, slotf, accf);
+      } else {
+        expand_staged_slots<NT, CBG_UNROLL_KNOWN, CBG_GROUP_KNOWN, V>(sb, tid, F, H.bs + c,
+                                                                    (int)min<int64_t>(NT, H.nb - c), ld_one, slotf, accf);
+      }
       __syncthreads();
       STAMP(4);
     }
