@@ -2,7 +2,7 @@
 # vector row / (row, value) loads in every hash kernel: parity, s20, config 4
 set -e
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-O=gpurun_out/r03an; mkdir -p $O
+O=gpurun_out/r03ao; mkdir -p $O
 timeout -k 10 400 python -u -m pytest tests/test_spgemm_gpu.py tests/test_mcl_gpu.py -x -q --timeout 120 --timeout-method thread -m gpu > $O/t.log 2>&1 || { tail -30 $O/t.log; exit 1; }
 tail -1 $O/t.log
 timeout -k 10 300 python3 -u bench.py --steps 5 --warmup 2 --no-cpu > $O/s20.log 2>&1
