@@ -53,11 +53,21 @@ def heavy_bytes(flop_col, nnz_c_col, nnz_b_col, heavy):
             + int(nnz_c_col[heavy].sum()) * (S_I + S_V))
 
 
+def round_tag(path):
+    """Sort key of a profiles/ file by its evidence tag: r<round><letters>_..., letters in spreadsheet order
+    (r03y < r03z < r03aa < r03aj), so the newest build's file sorts last."""
+    import re
+    m = re.match(r"r(\d+)([a-z]*)_", os.path.basename(path))
+    if not m:
+        return (-1, 0, "")
+    return (int(m.group(1)), len(m.group(2)), m.group(2))
+
+
 def load_traffic(scale, edgefactor):
     """HBM bytes per product of the heavy kernels from the newest committed rocprofv3 PMC summary for this
     workload (profiles/*_pmc_heavy.json, written by tools/pmc_heavy.py), or (None, None)."""
     best = None
-    for f in sorted(glob.glob(os.path.join(HERE, "profiles", "*_pmc_heavy.json"))):
+    for f in sorted(glob.glob(os.path.join(HERE, "profiles", "*_pmc_heavy.json")), key=round_tag):
         try:
             d = json.load(open(f))
         except (OSError, ValueError):
@@ -106,13 +116,68 @@ def cpu_baseline(cp, ir, val, n, flop_col, target_mults):
 
 def verify_sample(Cdev, cols, R):
     """Bit-exact check of the benchmarked product on the sampled columns against the oracle's product
-    of the same columns (R-MAT values are multiplicities, so PlusTimes<double> sums are exact)."""
+    of the same columns (R-MAT values are multiplicities, so PlusTimes<double> sums are exact).
+    Also returns the sampled columns' entry checksum (compared with the reference's own product)."""
     S = Cdev.select_columns(cols)
     scp, sir, sval = S.to_host()
     S.free()
     ok = bool(np.array_equal(scp, R.cp) and np.array_equal(sir, R.ir) and np.array_equal(sval, R.val))
-    return {"columns": int(len(cols)), "nnz": int(R.cp[-1]), "bit_exact": ok,
-            "against": "oracle/oracle.c product of the cpu_baseline sample columns"}
+    return ({"columns": int(len(cols)), "nnz": int(R.cp[-1]), "bit_exact": ok,
+             "against": "oracle/oracle.c product of the cpu_baseline sample columns"},
+            entry_checksum(scp, sir, sval))
+
+
+REFBENCH = os.path.join(HERE, "oracle", "_ref", "refbench")
+
+
+def _mix64(x):
+    """splitmix64 finaliser on uint64 arrays (wrapping), as oracle/ref/refbench.cpp's mix64."""
+    with np.errstate(over="ignore"):
+        x = x + np.uint64(0x9E3779B97F4A7C15)
+        x = (x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        x = (x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return x ^ (x >> np.uint64(31))
+
+
+def entry_checksum(cp, ir, val, chunk=1 << 24):
+    """Order-independent checksum of a CSC's entries: sum of mix(row << 32 ^ col) ^ mix(value bits) mod 2^64
+    (oracle/ref/refbench.cpp computes the same over the reference's output tuples)."""
+    cols = np.repeat(np.arange(len(cp) - 1, dtype=np.uint64), np.diff(cp))
+    bits = np.ascontiguousarray(val, np.float64).view(np.uint64)
+    s = np.uint64(0)
+    with np.errstate(over="ignore"):
+        for a in range(0, len(ir), chunk):
+            r = ir[a:a + chunk].astype(np.uint64)
+            h = _mix64((r << np.uint64(32)) ^ cols[a:a + chunk]) ^ _mix64(bits[a:a + chunk])
+            s = s + np.sum(h, dtype=np.uint64)
+    return f"{int(s):016x}"
+
+
+def reference_baseline(n, cp, ir, val, stride, threads, synch_factor=3):
+    """The reference's own CPU SpGEMM (oracle/_ref/refbench, compiled from /root/reference's sources by
+    oracle/ref/Makefile) timed on the same sample: LocalSpGEMMHash on every `stride`-th column of B, and the
+    1-rank Mult_AnXBn_Synch (local hash + MultiwayMerge + DCSC build) on every (synch_factor*stride)-th column.
+    Returns the parsed JSON lines, or None when the binary is absent."""
+    import subprocess
+    import tempfile
+    if not os.path.exists(REFBENCH):
+        return None
+    with tempfile.TemporaryDirectory() as td:
+        path = os.path.join(td, "A.bin")
+        with open(path, "wb") as f:   # CBM1 (oracle/ref/refprobe.cpp): f64 values, int64 indices
+            f.write(b"CBM1")
+            np.array([0], np.int32).tofile(f)
+            np.array([n, n, len(ir)], np.int64).tofile(f)
+            np.asarray(cp, np.int64).tofile(f)
+            np.asarray(ir, np.int64).tofile(f)
+            np.asarray(val, np.float64).tofile(f)
+        env = dict(os.environ, OMP_NUM_THREADS=str(threads))
+        r = subprocess.run([REFBENCH, path, str(stride), str(stride * synch_factor)], capture_output=True, text=True,
+                           env=env, timeout=600)
+    if r.returncode != 0:
+        print(f"bench: refbench failed ({r.returncode}): {r.stderr[-2000:]}", file=sys.stderr)
+        return None
+    return {d["call"]: d for d in (json.loads(x) for x in r.stdout.splitlines() if x.startswith("{"))}
 
 
 def input_record(args, cp, ir, val, build_s):
@@ -216,9 +281,33 @@ def bench_local(args):
     }
     out["input"] = input_record(args, cp, ir, val, build_s)
     if not args.no_cpu:
-        out["cpu_baseline"], (cols, R) = cpu_baseline(cp, ir, val, n, flop_col, args.cpu_mults)
-        out["verified"] = verify_sample(keep["C"], cols, R)
-    keep.pop("C").free()
+        port, (cols, R) = cpu_baseline(cp, ir, val, n, flop_col, args.cpu_mults)
+        out["verified"], gpu_sum = verify_sample(keep["C"], cols, R)
+        keep.pop("C").free()
+        stride = int(cols[1] - cols[0]) if len(cols) > 1 else 1
+        ref = reference_baseline(n, cp, ir, val, stride, port["cores"])
+        if ref and "LocalSpGEMMHash" in ref:
+            h = ref["LocalSpGEMMHash"]
+            out["cpu_baseline"] = {
+                "value": h["multiplies"] / h["seconds"], "unit": "multiplies/s", "cores": h["omp_threads"],
+                "mpi_ranks": h["mpi_ranks"], "omp_threads": h["omp_threads"], "kind": "reference",
+                "sample": f"the reference's LocalSpGEMMHash<PlusTimesSRing<double,double>> (mtSpGEMM.h:465-661, "
+                          f"oracle/_ref/refbench built from /root/reference sources, -O3 -fopenmp) at 1 MPI rank x "
+                          f"{h['omp_threads']} OpenMP threads on every {stride}-th column of B ({h['columns']} columns, "
+                          f"{h['multiplies']} multiplies, {h['seconds']:.2f} s)"}
+            out["verified"]["reference_checksum_equal"] = h["checksum"] == gpu_sum and h["nnzC"] == out["verified"]["nnz"]
+            s = ref.get("Mult_AnXBn_Synch")
+            if s:
+                out["cpu_baseline"]["synch"] = {
+                    "value": s["multiplies"] / s["seconds"], "unit": "multiplies/s",
+                    "sample": f"Mult_AnXBn_Synch (ParFriends.h:1004-1108: local hash + MultiwayMerge + DCSC build), "
+                              f"1 rank x {s['omp_threads']} threads, every {s['stride']}-th column "
+                              f"({s['multiplies']} multiplies, {s['seconds']:.2f} s)"}
+            out["cpu_baseline_port"] = port
+        else:
+            out["cpu_baseline"] = port
+    else:
+        keep.pop("C").free()
     print(json.dumps(out), flush=True)
     if not args.no_cpu and not out["verified"]["bit_exact"]:
         sys.exit("bench: the benchmarked product differs from the oracle on the sampled columns")
@@ -418,6 +507,189 @@ def bench_1d(args, world, rank, ctx, be, n, backend):
     dist.destroy_process_group()
 
 
+# ------------------------------------------------------------------------- rank share (one GPU)
+def _hcat(blocks):
+    """Blocks side by side (the panel of a grid row: A pieces in stage order)."""
+    import torch
+    from combblas_amd import dist as cbd
+    cps, off = [blocks[0].cp[:1]], 0
+    for b in blocks:
+        cps.append(b.cp[1:] + off)
+        off += b.nnz
+    return cbd.Block(blocks[0].nrow, sum(b.ncol for b in blocks), torch.cat(cps), torch.cat([b.ir for b in blocks]),
+                     torch.cat([b.val for b in blocks]))
+
+
+def _vstack(blocks):
+    """Blocks stacked by rows (the panel of a grid column: B pieces in stage order), rows ascending per column."""
+    import torch
+    from combblas_amd import dist as cbd
+    ncol, dev = blocks[0].ncol, blocks[0].cp.device
+    keys, irs, vals, roff = [], [], [], 0
+    for b in blocks:
+        col = torch.repeat_interleave(torch.arange(ncol, device=dev), torch.diff(b.cp))
+        keys.append(col)
+        irs.append(b.ir + roff)
+        vals.append(b.val)
+        roff += b.nrow
+    key = torch.cat(keys)
+    order = torch.sort(key, stable=True).indices
+    cnt = torch.bincount(key, minlength=ncol)
+    cp = torch.zeros(ncol + 1, dtype=torch.int64, device=dev)
+    torch.cumsum(cnt, 0, out=cp[1:])
+    return cbd.Block(roff, ncol, cp, torch.cat(irs)[order].contiguous(), torch.cat(vals)[order].contiguous())
+
+
+def _col_slice_block(b, c0, c1):
+    import torch
+    from combblas_amd import dist as cbd
+    lo, hi = int(b.cp[c0].item()), int(b.cp[c1].item())
+    return cbd.Block(b.nrow, c1 - c0, (b.cp[c0:c1 + 1] - lo).contiguous(), b.ir[lo:hi], b.val[lo:hi])
+
+
+def fiber_wire_bytes(P):
+    """Bytes the fiber pipeline (grid.hip fiber_pipeline) puts on the link for partial P: per-column counts (8 B),
+    rows as 16-bit gaps + 4 B per escaped row (gap > 65534), values as u16 / f32 / f64 (narrowest lossless for the
+    whole message).  Also what two candidate encodings would send: a per-column choice of gaps or a row bitmap over
+    the column's row span (+8 B base), and u8 values when every value is an integer in [0, 255]."""
+    import torch
+    n, nc = P.nnz, P.ncol
+    if n == 0:
+        return {"nnz": 0, "bytes": 8 * nc, "bytes_bitmap_u8": 8 * nc}
+    cnt = torch.diff(P.cp)
+    starts = P.cp[:-1][cnt > 0]
+    ir = P.ir.to(torch.int64)
+    prev = torch.roll(ir, 1)
+    prev[starts] = 0
+    esc_mask = (ir - prev) > 0xFFFE
+    esc = int(esc_mask.sum().item())
+    v = P.val
+    is_int = (v == torch.round(v)) & (v >= 0)
+    u16 = bool((is_int & (v <= 65535)).all().item())
+    u8 = bool((is_int & (v <= 255)).all().item())
+    f32 = bool((v.to(torch.float32).to(torch.float64) == v).all().item())
+    vb = 2 if u16 else 4 if f32 else 8
+    rows_gap = 2 * n + 4 * esc
+    # per column: gaps (2 B per entry + 4 B per escape) or a bitmap of the row span (1 bit per row + 8 B base)
+    col = torch.repeat_interleave(torch.arange(nc, device=ir.device), cnt)
+    esc_col = torch.bincount(col[esc_mask], minlength=nc)
+    nz = cnt > 0
+    first = torch.zeros(nc, dtype=torch.int64, device=ir.device)
+    last = torch.zeros(nc, dtype=torch.int64, device=ir.device)
+    first[nz] = ir[P.cp[:-1][nz]]
+    last[nz] = ir[P.cp[1:][nz] - 1]
+    gap_b = 2 * cnt + 4 * esc_col
+    bm_b = torch.where(nz, (last - first + 8) // 8 + 8, torch.zeros_like(cnt))
+    rows_mixed = int(torch.minimum(gap_b, bm_b).sum().item())
+    vb2 = 1 if u8 else vb
+    return {"nnz": n, "escapes": esc, "value_bytes": vb, "bytes": 8 * nc + rows_gap + vb * n,
+            "bitmap_columns": int((bm_b < gap_b).sum().item()),
+            "bytes_bitmap_u8": 8 * nc + rows_mixed + vb2 * n}
+
+
+def bench_rank_share(args):
+    """One rank's share of the N-GPU product, on this one GPU, without a transport: rank (l, i, j) of the
+    mandated layout builds its panels (A's grid row i and B's grid column j over layer l's inner range: what the
+    panel schedule's broadcasts deliver), multiplies the other layer's column half, measures the fiber message that
+    half would make, multiplies its own half, and merges it with the partner's message (the partner rank's product
+    of this rank's half, computed here beforehand).  Records local ms, fiber bytes and the peak HBM in use."""
+    import tempfile
+    import torch
+    import torch.distributed as dist
+    import combblas_amd as cb
+    from combblas_amd import dist as cbd
+    N = args.gpus_virtual
+    L, q, _ = cbd.grid_for(N)
+    ranks = list(range(N)) if args.rank_share == "all" else [int(x) for x in args.rank_share.split(",")]
+    store = tempfile.NamedTemporaryFile(delete=False)
+    dist.init_process_group("gloo", init_method=f"file://{store.name}", rank=0, world_size=1)
+    ctx = cb.Context(0)
+    be = cbd.GpuBackend(ctx)
+    SR = cb.PlusTimesSRing("f64")
+    n = 1 << args.scale
+    dev = be.device
+    total = torch.cuda.mem_get_info()[1]
+    floor = [total]
+
+    def sample():
+        torch.cuda.synchronize()
+        floor[0] = min(floor[0], torch.cuda.mem_get_info()[0])
+
+    def panels(l, i, j, c0=None, c1=None):
+        r0, r1 = cbd.block_range(n, q, i)
+        k_ranges = [cbd.piece_range(n, q, L, k, l) for k in range(q)]
+        b0, b1 = cbd.block_range(n, q, j)
+        AP = _hcat([be.rmat_block(args.scale, args.edgefactor, args.seed, r0, r1, k0, k1) for (k0, k1) in k_ranges])
+        BP = _vstack([be.rmat_block(args.scale, args.edgefactor, args.seed, k0, k1, b0, b1) for (k0, k1) in k_ranges])
+        return AP, BP
+
+    for r in ranks:
+        l, rem = divmod(r, q * q)
+        i, j = divmod(rem, q)
+        t0 = time.perf_counter()
+        AP, BP = panels(l, i, j)
+        nc = BP.ncol
+        halves = [cbd.block_range(nc, L, m) for m in range(L)]
+        me, other = (l, 1 - l) if L == 2 else (0, None)
+        build_s = time.perf_counter() - t0
+        rec = {"rank": r, "layout": f"{L}x{q}x{q}", "l_i_j": [l, i, j], "scale": args.scale,
+               "nnz_A_panel": AP.nnz, "nnz_B_panel": BP.nnz, "panel_build_s": round(build_s, 3)}
+        Pr = None
+        if L == 2:   # the partner's message (its product of this rank's column half), made first
+            PA, PB = panels(other, i, j)
+            Pr = be.multiply(PA, _col_slice_block(PB, *halves[me]), SR)
+            del PA, PB
+            rec["recv_nnz"] = Pr.nnz
+        torch.cuda.empty_cache()
+        sample()
+        for rep in range(2):   # the second repetition is recorded (code objects loaded, pool warm)
+            floor[0] = torch.cuda.mem_get_info()[0]
+            st = {}
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            if L == 2:
+                Po = be.multiply(AP, _col_slice_block(BP, *halves[other]), SR, st)
+                sample()
+                t1 = time.perf_counter()
+                p_other = ctx.last_profile()
+                wire = fiber_wire_bytes(Po)
+                del Po
+                t2 = time.perf_counter()
+                Pm = be.multiply(AP, _col_slice_block(BP, *halves[me]), SR, st)
+                sample()
+                t3 = time.perf_counter()
+                p_mine = ctx.last_profile()
+                M = be.merge([Pm, Pr] if me == 0 else [Pr, Pm], SR)
+                sample()
+                t4 = time.perf_counter()
+                local_ms = 1e3 * ((t1 - t0) + (t3 - t2))
+                merge_ms = 1e3 * (t4 - t3)
+                nnz_out = M.nnz
+                del Pm, M
+                profs = [p_other, p_mine]
+            else:
+                Pm = be.multiply(AP, BP, SR, st)
+                sample()
+                local_ms = 1e3 * (time.perf_counter() - t0)
+                merge_ms, wire = 0.0, None
+                nnz_out = Pm.nnz
+                profs = [ctx.last_profile()]
+                del Pm
+            torch.cuda.synchronize()
+        rec.update({"multiplies": st.get("multiplies", 0), "local_ms": round(local_ms, 3),
+                    "merge_ms": round(merge_ms, 3), "nnz_C_piece": nnz_out,
+                    "heavy_ms": round(sum(p["heavy_ms"] for p in profs), 3),
+                    "symbolic_ms": round(sum(p["symbolic_ms"] for p in profs), 3),
+                    "fiber": wire,
+                    "peak_hbm_GB": round((total - floor[0]) / 1e9, 2), "hbm_total_GB": round(total / 1e9, 1)})
+        print(json.dumps(rec), flush=True)
+        del AP, BP, Pr
+        torch.cuda.empty_cache()
+    dist.destroy_process_group()
+    if os.path.exists(store.name):
+        os.unlink(store.name)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -430,10 +702,18 @@ def main():
     ap.add_argument("--layout", choices=["3d", "1d"], default="3d",
                     help="N > 1: the mandated 1x1x2 / 2x2 / 2x2x2 layouts (default) or SURVEY 8(e)'s 1D comparison")
     ap.add_argument("--cpu-mults", type=float, default=1.5e9, help="multiplies in the CPU baseline sample")
+    ap.add_argument("--rank-share", default=None,
+                    help="with --gpus-virtual N: run these ranks' shares of the N-GPU layout on this one GPU "
+                         "('all' or a comma list); one JSON line per rank (local ms, fiber bytes, peak HBM)")
+    ap.add_argument("--gpus-virtual", type=int, default=8)
     args = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.rank_share is not None:
+        if not args.scale:
+            args.scale = 20 + {1: 0, 2: 1, 4: 1, 8: 2}.get(args.gpus_virtual, 0)
+        return bench_rank_share(args)
     if not args.scale:
         args.scale = 20 + {1: 0, 2: 1, 4: 1, 8: 2}.get(world, 0)
     if world == 1:

@@ -592,6 +592,8 @@ cbg_status fiber_pipeline(cbg_grid* G, const cbg_dcsc_view& va, const cbg_dcsc_v
 // Internal flag: L = 2, plain product -- the layer product runs in two column halves with the fiber exchange
 // of the other layer's half overlapping the own half (fiber_pipeline); parts then holds the reduced piece.
 constexpr uint32_t kFiberPipe = 1u << 29;
+// CUs the own-half product leaves to RCCL while the fiber transfer is in flight (CBG_FIBER_RESERVE_CU overrides)
+constexpr int kFiberReserveCu = 0;
 
 // est != nullptr: count only (EstPerProcessNnzSUMMA) -- every stage runs the symbolic pass alone and est[0] / est[1]
 // accumulate its multiplies and nnz; no product is formed (staged schedule, parts stays empty)
@@ -1188,11 +1190,22 @@ cbg_status fiber_pipeline(cbg_grid* G, const cbg_dcsc_view& va, const cbg_dcsc_v
       CBGCHK(t_alltoallv(G, CBG_GROUP_FIBER, sval, sb, rval, rb));
     }
   }
-  // 4. the own columns, while the exchange runs on the communication stream
+  // 4. the own columns, while the exchange runs on the communication stream.  RCCL's kernel needs 37.6 KB of LDS
+  // per workgroup (ncclDevKernel_Generic on gfx950) and cannot share a CU with the persistent heavy grid (one
+  // 1024-thread workgroup holding 152.7 KB on every CU): CBG_FIBER_RESERVE_CU leaves that many CUs to the transfer
+  // while it is in flight (the heavy kernels take their work from a ticket, so a workgroup held back by RCCL's
+  // finds the work done instead of stretching the kernel)
+  static const int reserve_env = [] {
+    const char* e = std::getenv("CBG_FIBER_RESERVE_CU");
+    return e ? std::max(0, atoi(e)) : kFiberReserveCu;
+  }();
   t0 = now_ms();
   cbg_csc_result Rm;
   int64_t mm = 0;
-  CBGCHK(cbg_spgemm_local(ctx, &va, &vm, sr, dt, CBG_SORTED_COLS, &Rm, &mm));
+  if (async) ctx->reserve_cu = reserve_env;
+  const cbg_status sm = cbg_spgemm_local(ctx, &va, &vm, sr, dt, CBG_SORTED_COLS, &Rm, &mm);
+  ctx->reserve_cu = 0;
+  CBGCHK(sm);
   Piece Pm = piece_of_result(Rm);
   t_local += now_ms() - t0;
   // 5. join, the received piece (colptr from its counts; f32 values widened), the merge in layer order

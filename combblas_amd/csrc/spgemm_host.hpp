@@ -151,6 +151,8 @@ struct cbg_ctx {
   DevBuf gal[9];                       // fused Galerkin product scratch (galerkin.hip)
   void* pin = nullptr;                 // 16 KB of pinned host memory: small read-backs (bin counts, scalars)
   int ncu = 0;                         // compute units (persistent grids)
+  int lds_per_cu = 0;                  // LDS bytes per CU (hipDeviceAttributeMaxSharedMemoryPerMultiprocessor)
+  int reserve_cu = 0;                  // CUs the persistent grids leave free (a concurrent RCCL transfer)
   int row_handoff = -1;                // -1: read CBG_ROW_HANDOFF once (default on)
 };
 
@@ -335,32 +337,33 @@ hipError_t launch_num_block(hipStream_t st, const int32_t* l, const int* n_dev, 
 template <int LOGT, int NT, class SRT, typename V>
 hipError_t launch_num_heavy(hipStream_t st, int grid, const HeavyItem* items, const unsigned long long* nitems,
                             const int32_t* hcols, const Unit* units, int32_t nsub, const DevCsc<V>& A,
-                            const DevCsc<V>& B, const int2* span, const Split& spl, const NumOut<V>& o) {
+                            const DevCsc<V>& B, const int2* span, const Split& spl, const NumOut<V>& o,
+                            unsigned long long* ticket) {
   if (grid <= 0) return hipSuccess;
   const size_t lds = num_heavy_lds<SRT, V, LOGT, NT>();
   hipError_t e = launch_cfg_lds((const void*)k_num_heavy<SRT, V, LOGT, NT>, lds);
   if (e != hipSuccess) return e;
-  k_num_heavy<SRT, V, LOGT, NT><<<grid, NT, lds, st>>>(items, nitems, hcols, units, nsub, A, B, span, spl, o);
+  k_num_heavy<SRT, V, LOGT, NT><<<grid, NT, lds, st>>>(items, nitems, hcols, units, nsub, A, B, span, spl, o, ticket);
   return hipGetLastError();
 }
 template <int LOGT, int NT, class SRT, typename V>
 hipError_t launch_num_heavy_known(hipStream_t st, int grid, const KnownUnit* ku, const unsigned long long* nku,
                                   const DevCsc<V>& A, const DevCsc<V>& B, const Split& spl, const NumOut<V>& o,
-                                  const RowVal<V>* arv = nullptr) {
+                                  unsigned long long* ticket, const RowVal<V>* arv = nullptr) {
   if (grid <= 0) return hipSuccess;
   const size_t lds = num_heavy_known_lds<SRT, V, LOGT, NT>();
   if (A.val && arv) {
     hipError_t e = launch_cfg_lds((const void*)k_num_heavy_known<SRT, V, LOGT, NT, true, true>, lds);
     if (e != hipSuccess) return e;
-    k_num_heavy_known<SRT, V, LOGT, NT, true, true><<<grid, NT, lds, st>>>(ku, nku, A, B, spl, o, arv);
+    k_num_heavy_known<SRT, V, LOGT, NT, true, true><<<grid, NT, lds, st>>>(ku, nku, A, B, spl, o, ticket, arv);
   } else if (A.val) {
     hipError_t e = launch_cfg_lds((const void*)k_num_heavy_known<SRT, V, LOGT, NT, true>, lds);
     if (e != hipSuccess) return e;
-    k_num_heavy_known<SRT, V, LOGT, NT, true><<<grid, NT, lds, st>>>(ku, nku, A, B, spl, o);
+    k_num_heavy_known<SRT, V, LOGT, NT, true><<<grid, NT, lds, st>>>(ku, nku, A, B, spl, o, ticket);
   } else {
     hipError_t e = launch_cfg_lds((const void*)k_num_heavy_known<SRT, V, LOGT, NT, false>, lds);
     if (e != hipSuccess) return e;
-    k_num_heavy_known<SRT, V, LOGT, NT, false><<<grid, NT, lds, st>>>(ku, nku, A, B, spl, o);
+    k_num_heavy_known<SRT, V, LOGT, NT, false><<<grid, NT, lds, st>>>(ku, nku, A, B, spl, o, ticket);
   }
   return hipGetLastError();
 }
@@ -688,13 +691,20 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
       NumOut<V> ou{own->ir.as<int32_t>(), own->val.as<V>(), adderr, uovf_n, ctx->uovf_list.as<int32_t>()};
       HIPCHK(hipEventRecord(ctx->ev[6], st));
       if (ctx->ncu <= 0) {
-        int ncu = 0;
+        int ncu = 0, lds = 0;
         HIPCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device));
+        HIPCHK(hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, ctx->device));
         ctx->ncu = ncu > 0 ? ncu : 256;
+        ctx->lds_per_cu = lds > 0 ? lds : (160 << 10);
       }
-      // persistent: as many workgroups as the LDS lets every CU hold (160 KB per CU)
-      const int per_cu = std::max<int>(1, (int)((160u << 10) / num_heavy_known_lds<SRT, V, CBG_KNOWN_LOGT, CBG_KNOWN_NT>()));
-      const int grid = (int)std::min<int64_t>((int64_t)ctx->ncu * per_cu, nitems * kItemUnits);
+      // persistent: as many workgroups as the LDS lets every CU hold (160 KB per CU on gfx950), less the CUs
+      // reserved for a concurrent transfer (ctx->reserve_cu, set by the fiber pipeline while RCCL runs)
+      const int per_cu =
+          std::max<int>(1, (int)((size_t)ctx->lds_per_cu / num_heavy_known_lds<SRT, V, CBG_KNOWN_LOGT, CBG_KNOWN_NT>()));
+      // CBG_HEAVY_RESERVE_CU: a standing reservation (tuning / tools/coresidency_probe.py)
+      static const int reserve_env = [] { const char* x = std::getenv("CBG_HEAVY_RESERVE_CU"); return x ? atoi(x) : 0; }();
+      const int cus = std::max(1, ctx->ncu - std::max(0, std::max(ctx->reserve_cu, reserve_env)));
+      const int grid = (int)std::min<int64_t>((int64_t)cus * per_cu, nitems * kItemUnits);
       // CBG_AOS=1: A's rows and values interleaved for the rows-known kernel's gathers (one 16-byte load per
       // multiply).  Off by default: measured slower at s20 (heavy 34.3 vs 32.8 ms) and even at s21 (108.1 vs
       // 107.1 ms) -- the extra 4 bytes per gathered entry cost more than the halved load count saves
@@ -710,12 +720,13 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
           arv = ctx->aos.as<RowVal<V>>();
         }
       }
+      // tickets of the persistent kernels: sc[14], sc[15] (zeroed with the scalars)
       e = launch_num_heavy_known<CBG_KNOWN_LOGT, CBG_KNOWN_NT, SRT, V>(st, grid, ctx->items.as<KnownUnit>(), sc + 12,
-                                                                     A, B, spl, ou, arv);
+                                                                     A, B, spl, ou, sc + 14, arv);
       if (e == hipSuccess)
         e = launch_num_heavy<CBG_HEAVY_LOGT, CBG_HEAVY_NT, SRT, V>(st, grid, ctx->oitems.as<HeavyItem>(), sc + 13,
                                                                  ctx->heavy_cols.as<int32_t>(), units, nsub, A, B, span,
-                                                                 spl, ou);
+                                                                 spl, ou, sc + 15);
       HIPCHK(hipEventRecord(ctx->ev[7], st));
       // overflowed hash units -> single-subwindow (dense) units
       if (e == hipSuccess) {

@@ -1041,6 +1041,12 @@ __global__ void __launch_bounds__(NT) k_sym_block(const int32_t* __restrict__ li
 #endif
 constexpr int kPartLog = CBG_PART_LOG;
 constexpr int kPartNT = CBG_PART_NT;
+// persistent heavy kernels take their work from a device ticket (CBG_HEAVY_DYNAMIC=1) instead of a static stride:
+// a workgroup that starts late -- its CU held by another stream's kernel, e.g. RCCL's fiber transfer (37.6 KB of LDS
+// per workgroup) -- finds the work taken instead of holding a fixed share until the other kernel ends
+#ifndef CBG_HEAVY_DYNAMIC
+#define CBG_HEAVY_DYNAMIC 1
+#endif
 #ifndef CBG_KNOWN_OTF
 #define CBG_KNOWN_OTF 0   // 1: k_num_heavy_known computes its unit segments from the split table (r03t: heavy +8 ms)
 #endif
@@ -2034,10 +2040,12 @@ __global__ void __launch_bounds__(NT) k_num_heavy(const HeavyItem* __restrict__ 
                                                   const unsigned long long* __restrict__ nitems,
                                                   const int32_t* __restrict__ hcols, const Unit* __restrict__ units,
                                                   int32_t nsub, DevCsc<V> A, DevCsc<V> B,
-                                                  const int2* __restrict__ span, Split spl, NumOut<V> out) {
+                                                  const int2* __restrict__ span, Split spl, NumOut<V> out,
+                                                  unsigned long long* __restrict__ ticket) {
   using Acc = typename SRT::Acc;
   constexpr int T = 1 << LOGT;
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  __shared__ unsigned long long s_claim;
   // vals and keys are adjacent: rank mode uses the pair as one region (values, then the bitmap)
   int64_t* qb = (int64_t*)smem;                  // NT
   int64_t* off = qb + NT;                        // NT
@@ -2055,8 +2063,16 @@ __global__ void __launch_bounds__(NT) k_num_heavy(const HeavyItem* __restrict__ 
   const SegBuf<V> sb{qb, off, bvs, scr, lens};
   STAMP_DECL
   STAMP(0);
-  const int64_t nit = (int64_t)*nitems;   // persistent: workgroup b takes items b, b+G, ...
-  for (int64_t ii = blockIdx.x; ii < nit; ii += gridDim.x) {
+  const int64_t nit = (int64_t)*nitems;   // persistent: items from the ticket (or b, b+G, ... when static)
+  auto claim = [&](int64_t prev) -> int64_t {
+    if (!CBG_HEAVY_DYNAMIC) return prev < 0 ? (int64_t)blockIdx.x : prev + gridDim.x;
+    if (threadIdx.x == 0) s_claim = atomicAdd(ticket, 1ull);
+    __syncthreads();
+    const int64_t v = (int64_t)s_claim;
+    __syncthreads();
+    return v;
+  };
+  for (int64_t ii = claim(-1); ii < nit; ii = claim(ii)) {
   const HeavyItem item = items[ii];
   const int32_t j = hcols[item.h];
   const int2 sp = span[j];
@@ -2349,6 +2365,7 @@ template <class SRT, typename V, int LOGT, int NT, bool AV, bool AOS = false>
 __global__ void __launch_bounds__(NT) k_num_heavy_known(const KnownUnit* __restrict__ ku,
                                                         const unsigned long long* __restrict__ nku, DevCsc<V> A,
                                                         DevCsc<V> B, Split spl, NumOut<V> out,
+                                                        unsigned long long* __restrict__ ticket,
                                                         const RowVal<V>* __restrict__ arv = nullptr) {
   using Acc = typename SRT::Acc;
   constexpr int T = 1 << LOGT;
@@ -2368,8 +2385,16 @@ __global__ void __launch_bounds__(NT) k_num_heavy_known(const KnownUnit* __restr
   const SegBuf<V> sb{qb, off, bvs, scr, lens};
   const int tid = threadIdx.x;
   const int64_t n = (int64_t)*nku;
+  // units k (current), k1 (next: header and rows in flight), k2 (claimed during unit k, header prefetched)
+#if CBG_HEAVY_DYNAMIC
+  __shared__ unsigned long long s_claim;
+  if (tid == 0) s_claim = atomicAdd(ticket, 2ull);
+  __syncthreads();
+  int64_t k = (int64_t)s_claim, k1 = k + 1;
+#else
   const int64_t G = gridDim.x;
-  int64_t k = blockIdx.x;
+  int64_t k = blockIdx.x, k1 = k + G;
+#endif
   if (k >= n) return;   // uniform
   STAMP_DECL
   STAMP(0);
@@ -2377,7 +2402,7 @@ __global__ void __launch_bounds__(NT) k_num_heavy_known(const KnownUnit* __restr
   uint32_t* hw = (uint32_t*)hdr;
   if (tid < kKnownWords) {
     hw[tid] = kw[k * kKnownWords + tid];
-    if (k + G < n) hw[kKnownWords + tid] = kw[(k + G) * kKnownWords + tid];
+    if (k1 < n) hw[kKnownWords + tid] = kw[k1 * kKnownWords + tid];
   }
   __syncthreads();
   int32_t rr[RPT];
@@ -2435,10 +2460,13 @@ __global__ void __launch_bounds__(NT) k_num_heavy_known(const KnownUnit* __restr
     put_bnd();
     __syncthreads();
   }
-  for (int slot = 0; k < n; k += G, slot ^= 1) {
+  for (int slot = 0; k < n; slot ^= 1) {
     STAMP(1);
     const KnownUnit H = hdr[slot];
-    const bool has1 = k + G < n, has2 = k + 2 * G < n;
+    const bool has1 = k1 < n;
+#if CBG_HEAVY_DYNAMIC
+    if (tid == 0) s_claim = atomicAdd(ticket, 1ull);   // read after the barrier closing step a
+#endif
     const int32_t lo = __builtin_amdgcn_readfirstlane(H.lo), hi = __builtin_amdgcn_readfirstlane(H.hi);
     const int32_t cnt = __builtin_amdgcn_readfirstlane(H.cnt);
     const int cpad = (cnt + 1) & ~1;
@@ -2462,8 +2490,14 @@ __global__ void __launch_bounds__(NT) k_num_heavy_known(const KnownUnit* __restr
       }
     }
     __syncthreads();
-    uint32_t nh = 0;   // header of unit k+2G, written to this unit's ring slot at the end
-    if (tid < kKnownWords && has2) nh = kw[(k + 2 * G) * kKnownWords + tid];
+#if CBG_HEAVY_DYNAMIC
+    const int64_t k2 = (int64_t)s_claim;
+#else
+    const int64_t k2 = k + 2 * G;
+#endif
+    const bool has2 = k2 < n;
+    uint32_t nh = 0;   // header of unit k2, written to this unit's ring slot at the end
+    if (tid < kKnownWords && has2) nh = kw[k2 * kKnownWords + tid];
     // b. bits
 #pragma unroll
     for (int q = 0; q < RPT; ++q) {
@@ -2535,6 +2569,8 @@ __global__ void __launch_bounds__(NT) k_num_heavy_known(const KnownUnit* __restr
     if (has1) put_bnd();
     __syncthreads();
     STAMP(5);
+    k = k1;
+    k1 = k2;
   }
 }
 

@@ -1,0 +1,65 @@
+"""bench.py's host helpers on CPU tensors: the rank-share panels (A pieces side by side, B pieces stacked by rows,
+as grid.hip's panel_cols / panel_rows lay them out), the fiber wire-byte count, the evidence-file order and the
+entry checksum shared with oracle/ref/refbench.cpp."""
+import numpy as np
+import scipy.sparse as sp
+import torch
+
+import bench
+from combblas_amd import dist as cbd
+
+
+def _block(M):
+    M = sp.csc_matrix(M)
+    M.sort_indices()
+    return cbd.Block(M.shape[0], M.shape[1], torch.as_tensor(M.indptr.astype(np.int64)),
+                     torch.as_tensor(M.indices.astype(np.int32)), torch.as_tensor(M.data.astype(np.float64)))
+
+
+def _dense(b):
+    return sp.csc_matrix((b.val.numpy(), b.ir.numpy(), b.cp.numpy()), shape=(b.nrow, b.ncol)).toarray()
+
+
+def test_panels_match_scipy_stacking():
+    rng = np.random.default_rng(7)
+    parts = [sp.random(50, 30 + k, density=0.1, random_state=rng) for k in range(3)]
+    H = bench._hcat([_block(p) for p in parts])
+    assert np.array_equal(_dense(H), sp.hstack(parts).toarray())
+    parts = [sp.random(20 + k, 40, density=0.15, random_state=rng) for k in range(3)]
+    V = bench._vstack([_block(p) for p in parts])
+    assert np.array_equal(_dense(V), sp.vstack(parts).toarray())
+    assert all(np.all(np.diff(V.ir.numpy()[V.cp[c]:V.cp[c + 1]]) > 0) for c in range(V.ncol))
+    S = bench._col_slice_block(V, 5, 17)
+    assert np.array_equal(_dense(S), sp.vstack(parts).toarray()[:, 5:17])
+
+
+def test_fiber_wire_bytes_counts_gaps_escapes_and_values():
+    # column 0: rows 3, 70000 (gap 69997 escapes), 70001; column 1 empty; column 2: dense run 100..163
+    rows = [3, 70000, 70001] + list(range(100, 164))
+    cp = [0, 3, 3, 67]
+    vals = [1.0, 2.0, 300.0] + [1.0] * 64
+    b = cbd.Block(80000, 3, torch.tensor(cp, dtype=torch.int64), torch.tensor(rows, dtype=torch.int32),
+                  torch.tensor(vals, dtype=torch.float64))
+    w = bench.fiber_wire_bytes(b)
+    assert w["escapes"] == 1 and w["value_bytes"] == 2
+    assert w["bytes"] == 8 * 3 + 2 * 67 + 4 * 1 + 2 * 67
+    # column 2 as a bitmap (64 rows: 8 B + 8 B base < 128 B of gaps); 300 > 255: values stay u16
+    assert w["bitmap_columns"] == 1
+    assert w["bytes_bitmap_u8"] == 8 * 3 + (2 * 3 + 4) + (8 + 8) + 2 * 67
+
+
+def test_round_tag_orders_evidence_files():
+    names = ["profiles/r03y_pmc_heavy.json", "profiles/r03aj_pmc_heavy.json", "profiles/r02zf_pmc_heavy.json",
+             "profiles/r04b_pmc_heavy.json", "profiles/r03z_pmc_heavy.json"]
+    assert sorted(names, key=bench.round_tag)[-2:] == ["profiles/r03aj_pmc_heavy.json", "profiles/r04b_pmc_heavy.json"]
+    assert sorted(names, key=bench.round_tag)[0] == "profiles/r02zf_pmc_heavy.json"
+
+
+def test_entry_checksum_is_order_independent():
+    cp = np.array([0, 2, 3], np.int64)
+    ir = np.array([1, 5, 0], np.int32)
+    val = np.array([1.0, 2.0, 3.0])
+    a = bench.entry_checksum(cp, ir, val)
+    # same entries, rows of column 0 swapped: a different CSC order, the same multiset
+    assert a == bench.entry_checksum(cp, np.array([5, 1, 0], np.int32), np.array([2.0, 1.0, 3.0]))
+    assert a != bench.entry_checksum(cp, ir, np.array([1.0, 2.0, 4.0]))

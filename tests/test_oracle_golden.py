@@ -4,6 +4,8 @@ Fixtures come from tests/golden/make_golden.py, i.e. the reference's LocalSpGEMM
 LocalSpGEMM / LocalHybridSpGEMM / Mult_AnXBn_Synch (oracle/_ref/refprobe) and the MATLAB golden
 3DSpGEMM/matlab/C.mtx.  If this file passes, the oracle is a trustworthy checker for the GPU path.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -149,3 +151,26 @@ def test_merged_split_products_equal_the_product_select2nd():
     assert np.array_equal(z["split_select2nd_i64_hash_cp"], f["C_s2_i64_hash_cp"])
     assert np.array_equal(z["split_select2nd_i64_hash_ir"], f["C_s2_i64_hash_ir"])
     assert np.array_equal(z["split_select2nd_i64_hash_val"], f["C_s2_i64_hash_val"])
+
+
+def test_refbench_times_the_reference_on_the_bench_sample():
+    """bench.py's cpu_baseline runs the reference's own LocalSpGEMMHash and 1-rank Mult_AnXBn_Synch
+    (oracle/_ref/refbench) on every s-th column of B and compares their output checksum with the GPU product's
+    sampled columns: here the same checksum of the oracle's product must match on the G500 s12 fixture."""
+    import bench
+    if not os.path.exists(bench.REFBENCH):
+        pytest.skip("oracle/_ref/refbench not built (needs the reference sources)")
+    z = load_fixture("g500_s12")
+    A, _, _, _ = fixture_inputs(z, "pt_f64_hash")
+    stride = 3
+    ref = bench.reference_baseline(A.ncol, A.cp, A.ir, A.val, stride, 4, synch_factor=2)
+    assert ref is not None and set(ref) == {"LocalSpGEMMHash", "Mult_AnXBn_Synch"}
+    for call, s in (("LocalSpGEMMHash", stride), ("Mult_AnXBn_Synch", 2 * stride)):
+        cols = np.arange(0, A.ncol, s)
+        idx = np.concatenate([np.arange(A.cp[c], A.cp[c + 1]) for c in cols])
+        B = Csc(A.nrow, len(cols), np.concatenate([[0], np.cumsum(np.diff(A.cp)[cols])]), A.ir[idx], A.val[idx])
+        C, mults, rc = oracle_spgemm(A, B, "plus_times", "f64")
+        assert rc == 0
+        r = ref[call]
+        assert (r["multiplies"], r["nnzC"], r["mpi_ranks"]) == (mults, C.nnz, 1), call
+        assert r["checksum"] == bench.entry_checksum(C.cp, C.ir, C.val), call

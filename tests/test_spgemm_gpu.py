@@ -3,6 +3,8 @@
 Bars: structure exact; integer/bool semirings bit-exact; PlusTimes<double> within
 1e-12 relative (|c - r| <= 1e-12 * max(|r|, sum|a*b|)); R-MAT multiplicity values are exact.
 """
+import zlib
+
 import numpy as np
 import pytest
 
@@ -100,7 +102,7 @@ CASES = [("plus_times", "f64"), ("plus_times", "f32"), ("plus_times", "i64"), ("
 @pytest.mark.parametrize("shape", [(50, 40, 60, 0.05), (300, 200, 250, 0.02), (2000, 1500, 1800, 0.004)])
 def test_gpu_random_vs_oracle(gpu_ctx, sr, dt, shape):
     m, k, n, d = shape
-    rng = np.random.default_rng(abs(hash((sr, dt, shape))) % 2**32)
+    rng = np.random.default_rng(zlib.crc32(repr((sr, dt, shape)).encode()))   # stable across processes
     A = rand_csc(rng, m, k, d, dt, pattern=(sr == "select_max_bool"))
     B = rand_csc(rng, k, n, d, dt)
     R, rmults, rc = oracle_spgemm(A, B, sr, dt)

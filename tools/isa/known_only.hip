@@ -4,6 +4,6 @@
 namespace cbg {
 void launch_known_only(const KnownUnit* ku, const unsigned long long* n, DevCsc<double> A, DevCsc<double> B, Split spl,
                        NumOut<double> o) {
-  k_num_heavy_known<Semiring<0, double>, double, CBG_KNOWN_LOGT, CBG_KNOWN_NT, true><<<1, CBG_KNOWN_NT>>>(ku, n, A, B, spl, o);
+  k_num_heavy_known<Semiring<0, double>, double, CBG_KNOWN_LOGT, CBG_KNOWN_NT, true><<<1, CBG_KNOWN_NT>>>(ku, n, A, B, spl, o, (unsigned long long*)n);
 }
 }  // namespace cbg
