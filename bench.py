@@ -547,44 +547,41 @@ def _col_slice_block(b, c0, c1):
     return cbd.Block(b.nrow, c1 - c0, (b.cp[c0:c1 + 1] - lo).contiguous(), b.ir[lo:hi], b.val[lo:hi])
 
 
+def _vlen(x):
+    """LEB128 varint bytes of non-negative integers (grid.hip vlen32)."""
+    import torch
+    return 1 + (x >= 1 << 7).long() + (x >= 1 << 14).long() + (x >= 1 << 21).long() + (x >= 1 << 28).long()
+
+
 def fiber_wire_bytes(P):
-    """Bytes the fiber pipeline (grid.hip fiber_pipeline) puts on the link for partial P: per-column counts (8 B),
-    rows as 16-bit gaps + 4 B per escaped row (gap > 65534), values as u16 / f32 / f64 (narrowest lossless for the
-    whole message).  Also what two candidate encodings would send: a per-column choice of gaps or a row bitmap over
-    the column's row span (+8 B base), and u8 values when every value is an integer in [0, 255]."""
+    """Bytes the fiber pipeline (grid.hip fiber_pipeline) puts on the link for partial P, choosing per message as
+    k_code_count's totals do: per-column headers (8 B), rows as varint gaps, 16-bit gaps + 4 B per escaped row (gap >
+    65534) or int32, values as varint integers (+8 B per column), u16, f32 or f64 -- the smallest lossless form."""
     import torch
     n, nc = P.nnz, P.ncol
     if n == 0:
-        return {"nnz": 0, "bytes": 8 * nc, "bytes_bitmap_u8": 8 * nc}
+        return {"nnz": 0, "bytes": 8 * nc}
     cnt = torch.diff(P.cp)
     starts = P.cp[:-1][cnt > 0]
     ir = P.ir.to(torch.int64)
     prev = torch.roll(ir, 1)
     prev[starts] = 0
-    esc_mask = (ir - prev) > 0xFFFE
-    esc = int(esc_mask.sum().item())
+    gap = ir - prev
+    esc = int((gap > 0xFFFE).sum().item())
+    rows = {"int32": 4 * n, "gap16": 2 * n + 4 * esc, "varint": int(_vlen(gap).sum().item())}
     v = P.val
+    vals = {"f64": 8 * n}
+    if bool((v.to(torch.float32).to(torch.float64) == v).all().item()):
+        vals["f32"] = 4 * n
     is_int = (v == torch.round(v)) & (v >= 0)
-    u16 = bool((is_int & (v <= 65535)).all().item())
-    u8 = bool((is_int & (v <= 255)).all().item())
-    f32 = bool((v.to(torch.float32).to(torch.float64) == v).all().item())
-    vb = 2 if u16 else 4 if f32 else 8
-    rows_gap = 2 * n + 4 * esc
-    # per column: gaps (2 B per entry + 4 B per escape) or a bitmap of the row span (1 bit per row + 8 B base)
-    col = torch.repeat_interleave(torch.arange(nc, device=ir.device), cnt)
-    esc_col = torch.bincount(col[esc_mask], minlength=nc)
-    nz = cnt > 0
-    first = torch.zeros(nc, dtype=torch.int64, device=ir.device)
-    last = torch.zeros(nc, dtype=torch.int64, device=ir.device)
-    first[nz] = ir[P.cp[:-1][nz]]
-    last[nz] = ir[P.cp[1:][nz] - 1]
-    gap_b = 2 * cnt + 4 * esc_col
-    bm_b = torch.where(nz, (last - first + 8) // 8 + 8, torch.zeros_like(cnt))
-    rows_mixed = int(torch.minimum(gap_b, bm_b).sum().item())
-    vb2 = 1 if u8 else vb
-    return {"nnz": n, "escapes": esc, "value_bytes": vb, "bytes": 8 * nc + rows_gap + vb * n,
-            "bitmap_columns": int((bm_b < gap_b).sum().item()),
-            "bytes_bitmap_u8": 8 * nc + rows_mixed + vb2 * n}
+    if bool((is_int & (v <= 65535)).all().item()):
+        vals["u16"] = 2 * n
+    if bool((is_int & (v <= 4294967295.0)).all().item()):
+        vals["varint"] = int(_vlen(v.to(torch.int64)).sum().item()) + 8 * nc
+    rf = min(rows, key=rows.get)
+    vf = min(vals, key=vals.get)
+    return {"nnz": n, "escapes": esc, "rows": rf, "values": vf, "row_bytes": rows, "value_bytes": vals,
+            "bytes": 8 * nc + rows[rf] + vals[vf], "bytes_per_entry": round((8 * nc + rows[rf] + vals[vf]) / n, 3)}
 
 
 def bench_rank_share(args):

@@ -52,8 +52,8 @@ class MclStats(ctypes.Structure):
 class GridStats(ctypes.Structure):
     _fields_ = [("multiplies", ctypes.c_int64), ("bcast_bytes", ctypes.c_int64), ("fiber_bytes", ctypes.c_int64),
                 ("bcast_ms", ctypes.c_double), ("local_ms", ctypes.c_double), ("merge_ms", ctypes.c_double),
-                ("fiber_ms", ctypes.c_double), ("total_ms", ctypes.c_double), ("fiber_xfer_ms", ctypes.c_double),
-                ("stages", ctypes.c_int32)]
+                ("fiber_ms", ctypes.c_double), ("total_ms", ctypes.c_double), ("stages", ctypes.c_int32),
+                ("fiber_xfer_ms", ctypes.c_double)]
 
 
 # cbg_transport callbacks (include/cbgpu.h)
@@ -81,6 +81,7 @@ HALVES, RUNNING_MERGE = 4, 8
 SIGNATURES = {
     "cbg_abi_version": (ctypes.c_int32, []),
     "cbg_strerror": (ctypes.c_char_p, [ctypes.c_int]),
+    "cbg_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int32)]),
     "cbg_init": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
     "cbg_destroy": (ctypes.c_int, [ctypes.c_void_p]),
     "cbg_set_stream": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),

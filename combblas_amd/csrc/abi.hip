@@ -23,6 +23,15 @@ const char* cbg_strerror(cbg_status s) {
   return "unknown status";
 }
 
+cbg_status cbg_device_count(int32_t* n) {
+  if (!n) return CBG_EINVAL;
+  *n = 0;
+  int c = 0;
+  if (hipGetDeviceCount(&c) != hipSuccess) return CBG_EDEVICE;
+  *n = c;
+  return CBG_OK;
+}
+
 cbg_status cbg_init(int device, cbg_ctx** out) {
   if (!out) return CBG_EINVAL;
   *out = nullptr;

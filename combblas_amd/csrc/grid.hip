@@ -112,21 +112,6 @@ __global__ void k_f32_inexact(int64_t n, const double* __restrict__ v, unsigned 
   c = (unsigned long long)wave_sum64((int64_t)c);
   if (lane_id() == 0 && c) atomicAdd(bad, c);
 }
-// one pass for both narrowings: bad[0] counts values that do not survive f32, bad[1] values that are not an integer
-// in [0, 65535] (those travel as u16: a quarter of the f64 bytes -- multiplicity-valued products such as R-MAT A*A)
-__global__ void k_narrow_check(int64_t n, const double* __restrict__ v, unsigned long long* __restrict__ bad) {
-  unsigned long long c32 = 0, c16 = 0;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const double x = v[i];
-    c32 += __double_as_longlong((double)(float)x) != __double_as_longlong(x);
-    const bool in16 = x >= 0.0 && x <= 65535.0;   // false for NaN
-    c16 += !(in16 && __double_as_longlong((double)(unsigned short)x) == __double_as_longlong(x));
-  }
-  c32 = (unsigned long long)wave_sum64((int64_t)c32);
-  c16 = (unsigned long long)wave_sum64((int64_t)c16);
-  if (lane_id() == 0 && c32) atomicAdd(bad, c32);
-  if (lane_id() == 0 && c16) atomicAdd(bad + 1, c16);
-}
 __global__ void k_f64_to_u16(int64_t n, const double* __restrict__ in, unsigned short* __restrict__ out) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
     out[i] = (unsigned short)in[i];
@@ -140,28 +125,159 @@ __global__ void k_u16_to_f64(int64_t n, const unsigned short* __restrict__ in, d
 // a scan of the per-column escape counts, which ride in the high half of the column counts).  One wave per column.
 constexpr unsigned kGapEsc = 0xFFFFu, kGapMax = 0xFFFEu;
 
-__global__ void k_gap_count(int64_t ncol, const int64_t* __restrict__ cp, const int32_t* __restrict__ ir,
-                            int64_t* __restrict__ cnt) {   // cnt[c] |= escapes << 32 (cnt holds the column counts)
+// split received column headers (count | aux << 32) in place: aux -> aux[i], the count stays in hdr[i]
+__global__ void k_split_hdr(int64_t n, int64_t* hdr, int64_t* __restrict__ aux) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t v = hdr[i];
+    aux[i] = v >> 32;
+    hdr[i] = v & 0xffffffffLL;
+  }
+}
+// column headers of a message: count | aux << 32 (aux = escapes of the u16 gaps, or the column's varint row bytes)
+__global__ void k_pack_hdr(int64_t n, const int64_t* __restrict__ cp, const int64_t* __restrict__ aux,
+                           int64_t* __restrict__ hdr) {   // aux == nullptr: no aux
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    hdr[i] = (cp[i + 1] - cp[i]) | (aux ? aux[i] << 32 : 0);
+}
+
+// Varint fiber codes (LEB128: 7 bits per byte, high bit = another byte follows).  Rows travel as varint gaps
+// (row - previous row in the column, the first as row - 0), integer values in [0, 2^32) as varint integers: a
+// multiplicity-valued product's entry is ~2-3 bytes instead of 6 (u16 gap + f32).  Per column the sender counts
+// the bytes of every candidate format in one pass (k_code_count) and the message takes the smallest.
+__device__ __forceinline__ int vlen32(uint32_t x) {
+  return 1 + (x >= (1u << 7)) + (x >= (1u << 14)) + (x >= (1u << 21)) + (x >= (1u << 28));
+}
+__device__ __forceinline__ bool as_u32(double x, uint32_t* u) {   // an integer in [0, 2^32), bit-exact round trip
+  const bool in = x >= 0.0 && x <= 4294967295.0;                   // false for NaN
+  *u = in ? (uint32_t)x : 0u;
+  return in && __double_as_longlong((double)*u) == __double_as_longlong(x);
+}
+
+// one wave per column: escapes of the u16 gaps, varint bytes of the row gaps, varint bytes of the values; over
+// the message: bad[0] values that do not survive f32, bad[1] not u16, bad[2] not u32 integers
+__global__ void k_code_count(int64_t ncol, const int64_t* __restrict__ cp, const int32_t* __restrict__ ir,
+                             const double* __restrict__ val, int64_t* __restrict__ esc, int64_t* __restrict__ rbytes,
+                             int64_t* __restrict__ vbytes, unsigned long long* __restrict__ bad) {
+  const int l = lane_id();
+  int64_t b32 = 0, b16 = 0, bvar = 0;
+  for (int64_t c = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / kWave; c < ncol;
+       c += ((int64_t)gridDim.x * blockDim.x) / kWave) {
+    const int64_t s = cp[c], e = cp[c + 1];
+    int64_t ne = 0, nr = 0, nv = 0;
+    for (int64_t i = s + l; i < e; i += kWave) {
+      const int64_t d = (int64_t)ir[i] - (i == s ? 0 : ir[i - 1]);
+      ne += d > (int64_t)kGapMax;
+      nr += vlen32((uint32_t)d);
+      if (val) {
+        const double x = val[i];
+        b32 += __double_as_longlong((double)(float)x) != __double_as_longlong(x);
+        const bool in16 = x >= 0.0 && x <= 65535.0;
+        b16 += !(in16 && __double_as_longlong((double)(unsigned short)x) == __double_as_longlong(x));
+        uint32_t u;
+        const bool ok = as_u32(x, &u);
+        bvar += !ok;
+        nv += ok ? vlen32(u) : 5;
+      }
+    }
+    ne = wave_sum64(ne);
+    nr = wave_sum64(nr);
+    nv = wave_sum64(nv);
+    if (l == 0) {
+      esc[c] = ne;
+      rbytes[c] = nr;
+      if (vbytes) vbytes[c] = nv;
+    }
+  }
+  b32 = wave_sum64(b32);
+  b16 = wave_sum64(b16);
+  bvar = wave_sum64(bvar);
+  if (l == 0 && b32) atomicAdd(bad, (unsigned long long)b32);
+  if (l == 0 && b16) atomicAdd(bad + 1, (unsigned long long)b16);
+  if (l == 0 && bvar) atomicAdd(bad + 2, (unsigned long long)bvar);
+}
+
+// MODE 0: row gaps of ir, MODE 1: values (u32 integers) of val -> varint bytes at off[c] of column c
+template <int MODE>
+__global__ void k_var_encode(int64_t ncol, const int64_t* __restrict__ cp, const int32_t* __restrict__ ir,
+                             const double* __restrict__ val, const int64_t* __restrict__ off,
+                             uint8_t* __restrict__ out) {
   const int l = lane_id();
   for (int64_t c = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / kWave; c < ncol;
        c += ((int64_t)gridDim.x * blockDim.x) / kWave) {
     const int64_t s = cp[c], e = cp[c + 1];
-    int64_t ne = 0;
-    for (int64_t i = s + l; i < e; i += kWave) {
-      const int64_t prev = i == s ? 0 : ir[i - 1];
-      ne += (int64_t)ir[i] - prev > (int64_t)kGapMax;
+    int64_t o = off[c];
+    for (int64_t i0 = s; i0 < e; i0 += kWave) {
+      const int64_t i = i0 + l;
+      uint32_t x = 0;
+      int len = 0;
+      if (i < e) {
+        if (MODE == 0) x = (uint32_t)(ir[i] - (i == s ? 0 : ir[i - 1]));
+        else (void)as_u32(val[i], &x);
+        len = vlen32(x);
+      }
+      const int incl = wave_incl_scan(len);
+      uint8_t* dst = out + o + (incl - len);
+      for (int k = 0; k < len; ++k) dst[k] = (uint8_t)(((x >> (7 * k)) & 0x7Fu) | (k + 1 < len ? 0x80u : 0u));
+      o += __shfl(incl, kWave - 1, kWave);
     }
-    ne = wave_sum64(ne);
-    if (l == 0) cnt[c] |= ne << 32;
   }
 }
 
-__global__ void k_esc_counts(int64_t n, const int64_t* __restrict__ packed, int64_t* __restrict__ esc,
-                             int64_t* __restrict__ plain) {   // split packed counts (plain may alias packed)
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t v = packed[i];
-    esc[i] = v >> 32;
-    plain[i] = v & 0xffffffffLL;
+// one wave per column: bytes [off[c], off[c+1]) -> entries [cp[c], cp[c+1]).  A chunk is 64 bytes, one per lane; a
+// byte without the high bit ends an entry (ballot); the entry's value is gathered from the (at most 5) bytes back to
+// the previous end, an entry begun in the previous chunk continues from its pending bits.  MODE 0: the values are
+// row gaps (inclusive scan + the column's running row -> int32 rows), MODE 1: u32 integers -> f64 values.
+template <int MODE>
+__global__ void k_var_decode(int64_t ncol, const int64_t* __restrict__ cp, const int64_t* __restrict__ off,
+                             const uint8_t* __restrict__ in, int32_t* __restrict__ ir, double* __restrict__ val) {
+  const int l = lane_id();
+  for (int64_t c = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / kWave; c < ncol;
+       c += ((int64_t)gridDim.x * blockDim.x) / kWave) {
+    const int64_t be = off[c + 1];
+    int64_t idx = cp[c];
+    int64_t run = 0;        // MODE 0: the last row decoded in this column
+    uint32_t pend = 0;      // bits of an entry begun in the previous chunk
+    int pbits = 0;
+    for (int64_t p0 = off[c]; p0 < be; p0 += kWave) {
+      const int64_t p = p0 + l;
+      const bool valid = p < be;
+      const uint32_t b = valid ? in[p] : 0u;
+      const bool term = valid && !(b & 0x80u);
+      const uint64_t T = __ballot(term);
+      const uint32_t dig = b & 0x7Fu;
+      const uint64_t below = T & ((1ull << l) - 1ull);
+      const int st = below ? 64 - __clzll(below) : 0;   // first byte lane of this lane's entry in the chunk
+      uint32_t v = st == 0 ? pend : 0u;
+      const int base = st == 0 ? pbits : 0;
+#pragma unroll
+      for (int k = 0; k < 5; ++k) {
+        const int j = l - k;
+        const uint32_t dj = __shfl(dig, j < 0 ? 0 : j, kWave);
+        if (j >= st && j >= 0) v |= dj << (base + 7 * (j - st));
+      }
+      const int64_t at = idx + __popcll(below);
+      if (MODE == 0) {
+        const int64_t inc = wave_incl_scan64(term ? (int64_t)v : 0);
+        if (term) ir[at] = (int32_t)(run + inc);
+        run += __shfl(inc, kWave - 1, kWave);
+      } else if (term) {
+        val[at] = (double)v;
+      }
+      idx += __popcll(T);
+      // an entry left open at the chunk's end (the <= 4 bytes after its last terminator; a 64-byte chunk always
+      // holds a terminator, codes being <= 5 bytes): its bits carry over
+      const int ps = T ? 64 - __clzll(T) : 0;
+      const int nb = p0 + kWave <= be ? kWave - ps : 0;   // no carry past the column's last byte
+      uint32_t np = 0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int j = kWave - 1 - k;
+        const uint32_t dj = __shfl(dig, j, kWave);
+        if (j >= ps && nb > 0) np |= dj << (7 * (j - ps));
+      }
+      pend = np;
+      pbits = 7 * nb;
+    }
   }
 }
 
@@ -593,7 +709,7 @@ cbg_status fiber_pipeline(cbg_grid* G, const cbg_dcsc_view& va, const cbg_dcsc_v
 // of the other layer's half overlapping the own half (fiber_pipeline); parts then holds the reduced piece.
 constexpr uint32_t kFiberPipe = 1u << 29;
 // CUs the own-half product leaves to RCCL while the fiber transfer is in flight (CBG_FIBER_RESERVE_CU overrides)
-constexpr int kFiberReserveCu = 0;
+constexpr int kFiberReserveCu = 16;   // tools/coresidency_probe.py, profiles/r04a_coresidency_probe.jsonl
 
 // est != nullptr: count only (EstPerProcessNnzSUMMA) -- every stage runs the symbolic pass alone and est[0] / est[1]
 // accumulate its multiplies and nnz; no product is formed (staged schedule, parts stays empty)
@@ -1006,11 +1122,16 @@ cbg_status fiber_exchange(cbg_grid* G, const Piece& C, size_t vs, bool f64, std:
 // part (block_range of the local columns, as fiber_exchange cuts them) are multiplied first; their counts, rows
 // and values leave for the other layer as one grouped ncclSend/ncclRecv on the communication stream while the own
 // part multiplies on the compute stream; then the received partial and the own one are merged.  The same two
-// pieces and the same two-way merge as the unpipelined path, so the product is identical.  Each direction's values
-// travel in the narrowest lossless format of its whole message: u16 when every value is an integer in [0, 65535]
-// (multiplicities: R-MAT A*A), else f32 when every value survives the f32 round trip bit for bit, else f64 --
-// announced in the count exchange (bits 61, 62).  With a caller transport the exchange is synchronous (no
-// overlap, same result).
+// pieces and the same two-way merge as the unpipelined path, so the product is identical.  With a caller transport
+// the exchange is synchronous (no overlap, same result).
+//
+// Wire format, per direction, each part in the smallest lossless form of the whole message (counted in one pass,
+// k_code_count), announced in the count exchange (32 bytes per member: entries | formats, escapes, row bytes, value
+// bytes): column headers of 8 bytes (count | aux << 32); rows as varint gaps (aux = the column's row bytes), as
+// 16-bit gaps with escaped absolute rows (aux = the column's escapes) or as int32; values as varint integers (then 8
+// more bytes per column: its value bytes), u16, f32 or the native f64.  A multiplicity-valued product (R-MAT A*A)
+// travels at ~2-3 bytes per entry.  CBG_FIBER_GAPS=0: int32 rows; CBG_FIBER_NARROW=0: native values;
+// CBG_FIBER_VARINT=0: no varint codes.
 cbg_status fiber_pipeline(cbg_grid* G, const cbg_dcsc_view& va, const cbg_dcsc_view& vb, cbg_semiring sr,
                           cbg_dtype dt, Piece* out, cbg_grid_stats* st) {
   cbg_ctx* ctx = G->ctx;
@@ -1019,9 +1140,10 @@ cbg_status fiber_pipeline(cbg_grid* G, const cbg_dcsc_view& va, const cbg_dcsc_v
   const int me = G->layer, other = 1 - me;
   const int64_t ncol = vb.ncol;
   const int64_t cb[3] = {0, ncol / 2, ncol};
-  PoolBuf cpo, cpm, scnt, s32, r32, tiles, scal, secnt, seoff, splain, sgap, sesc, rgap, resc, recnt, reoff;
-  for (PoolBuf* b : {&cpo, &cpm, &scnt, &s32, &r32, &tiles, &scal, &secnt, &seoff, &splain, &sgap, &sesc, &rgap, &resc,
-                     &recnt, &reoff})
+  PoolBuf cpo, cpm, shdr, sval, tiles, scal, saux, svr, svv, sescoff, svroff, svvoff, srow, sesc, svhdr;
+  PoolBuf rrow, resc, rvbuf, raux, rauxoff, rvhdr, rvoff;
+  for (PoolBuf* b : {&cpo, &cpm, &shdr, &sval, &tiles, &scal, &saux, &svr, &svv, &sescoff, &svroff, &svvoff, &srow, &sesc,
+                     &svhdr, &rrow, &resc, &rvbuf, &raux, &rauxoff, &rvhdr, &rvoff})
     b->pool = ctx->pool;
   std::shared_ptr<Owner> rx(new Owner(ctx->pool));
   StreamFence fence(cst, G->cs);   // transfers into / out of the buffers above end before they return to the pool
@@ -1044,6 +1166,24 @@ cbg_status fiber_pipeline(cbg_grid* G, const cbg_dcsc_view& va, const cbg_dcsc_v
     v->val = vb.val ? (const void*)((const char*)vb.val + vs * e0) : nullptr;
     return CBG_OK;
   };
+  // exclusive scan of n int64 counts into out[0..n], the total into *total (device)
+  auto scan = [&](int64_t n, const int64_t* in, int64_t* outp, int64_t* total) -> cbg_status {
+    const int64_t nt = (n + kScanTile - 1) / kScanTile;
+    HIPCHK(tiles.reserve(8 * (nt + 1)));
+    if (n > 0) {
+      k_scan_tiles<<<(int)nt, 256, 0, cst>>>(n, in, tiles.as<int64_t>());
+      k_scan_sums<<<1, 1024, 0, cst>>>(nt, tiles.as<int64_t>(), total);
+      k_scan_apply<<<(int)nt, 256, 0, cst>>>(n, in, tiles.as<int64_t>(), outp);
+    } else {
+      HIPCHK(hipMemsetAsync(outp, 0, 8, cst));
+      HIPCHK(hipMemsetAsync(total, 0, 8, cst));
+    }
+    HIPCHK(hipGetLastError());
+    return CBG_OK;
+  };
+  static const bool gaps_env = [] { const char* x = std::getenv("CBG_FIBER_GAPS"); return !(x && x[0] == '0'); }();
+  static const bool narrow_env = [] { const char* x = std::getenv("CBG_FIBER_NARROW"); return !(x && x[0] == '0'); }();
+  static const bool var_env = [] { const char* x = std::getenv("CBG_FIBER_VARINT"); return !(x && x[0] == '0'); }();
   cbg_dcsc_view vo, vm;
   CBGCHK(col_view(other, cpo, &vo));
   CBGCHK(col_view(me, cpm, &vm));
@@ -1054,140 +1194,139 @@ cbg_status fiber_pipeline(cbg_grid* G, const cbg_dcsc_view& va, const cbg_dcsc_v
   CBGCHK(cbg_spgemm_local(ctx, &va, &vo, sr, dt, CBG_SORTED_COLS, &Ro, &mo));
   Piece Po = piece_of_result(Ro);
   double t_local = now_ms() - t0;
-  // 2. column counts, the f32 verdict and the sizes (host-synchronous, 8 bytes each way)
+  // 2. the message's formats (one counting pass, one host sync), its encoding, the sizes (8 x 8 bytes each way)
   t0 = now_ms();
-  const int64_t myc = cb[me + 1] - cb[me], oc = Po.ncol;
-  HIPCHK(scnt.reserve(8 * (oc + 1)));
-  if (oc) k_col_counts<<<(int)grid_for(oc, 256, kMaxGrid), 256, 0, cst>>>(oc, Po.cp, scnt.as<int64_t>());
+  const int64_t myc = cb[me + 1] - cb[me], oc = Po.ncol, n = Po.nnz;
+  const bool has_val = Po.val != nullptr;
+  const bool coded = gaps_env && oc > 0 && n > 0;
+  const bool vcheck = narrow_env && dt == CBG_F64 && has_val && vs == 8 && n > 0;
+  HIPCHK(G->small.reserve(256));
+  int64_t* dsn = G->small.as<int64_t>();   // [0..7] sent, [8..15] received, [16..18] value verdicts
+  HIPCHK(scal.reserve(64));
+  int64_t* dtot = scal.as<int64_t>();      // [0..2] sender totals (escapes, row bytes, value bytes), [3..5] receiver
+  int64_t tot[3] = {0, 0, 0};
+  unsigned long long bad[3] = {0, 0, 0};
+  if (coded || vcheck) {
+    for (PoolBuf* b : {&saux, &svr, &sescoff, &svroff}) HIPCHK(b->reserve(8 * (oc + 1)));
+    if (vcheck) { HIPCHK(svv.reserve(8 * (oc + 1))); HIPCHK(svvoff.reserve(8 * (oc + 1))); }
+    HIPCHK(hipMemsetAsync(dsn + 16, 0, 24, cst));
+    k_code_count<<<(int)grid_for(oc, 4, kMaxGrid * 2), 256, 0, cst>>>(
+        oc, Po.cp, Po.ir, vcheck ? (const double*)Po.val : nullptr, saux.as<int64_t>(), svr.as<int64_t>(),
+        vcheck ? svv.as<int64_t>() : nullptr, (unsigned long long*)(dsn + 16));
+    HIPCHK(hipGetLastError());
+    CBGCHK(scan(oc, saux.as<int64_t>(), sescoff.as<int64_t>(), dtot + 0));
+    CBGCHK(scan(oc, svr.as<int64_t>(), svroff.as<int64_t>(), dtot + 1));
+    if (vcheck) CBGCHK(scan(oc, svv.as<int64_t>(), svvoff.as<int64_t>(), dtot + 2));
+    HIPCHK(hipMemcpyAsync(tot, dtot, 24, hipMemcpyDeviceToHost, cst));
+    HIPCHK(hipMemcpyAsync(bad, dsn + 16, 24, hipMemcpyDeviceToHost, cst));
+    HIPCHK(hipStreamSynchronize(cst));
+  }
+  // rows: 0 int32, 1 16-bit gaps + escapes, 2 varint gaps
+  int rfmt = 0;
+  int64_t srow_b = 4 * n, sesc_b = 0;
+  if (coded && 2 * n + 4 * tot[0] < srow_b) { rfmt = 1; srow_b = 2 * n; sesc_b = 4 * tot[0]; }
+  if (coded && var_env && tot[1] < srow_b + sesc_b) { rfmt = 2; srow_b = tot[1]; sesc_b = 0; }
+  // values: 0 native, 1 f32, 2 u16, 3 varint (+ 8 bytes per column)
+  int vfmt = 0;
+  int64_t sval_b = has_val ? (int64_t)vs * n : 0;
+  if (vcheck && bad[0] == 0 && 4 * n < sval_b) { vfmt = 1; sval_b = 4 * n; }
+  if (vcheck && bad[1] == 0 && 2 * n < sval_b) { vfmt = 2; sval_b = 2 * n; }
+  if (vcheck && var_env && bad[2] == 0 && tot[2] + 8 * oc < sval_b) { vfmt = 3; sval_b = tot[2]; }
+  const void* srow_p = Po.ir;
+  if (rfmt == 1) {
+    HIPCHK(srow.reserve(srow_b + 16));
+    HIPCHK(sesc.reserve(sesc_b + 16));
+    k_gap_encode<<<(int)grid_for(oc, 4, kMaxGrid * 2), 256, 0, cst>>>(oc, Po.cp, Po.ir, sescoff.as<int64_t>(),
+                                                                      srow.as<unsigned short>(), sesc.as<int32_t>());
+    srow_p = srow.p;
+  } else if (rfmt == 2) {
+    HIPCHK(srow.reserve(srow_b + 16));
+    k_var_encode<0><<<(int)grid_for(oc, 4, kMaxGrid * 2), 256, 0, cst>>>(oc, Po.cp, Po.ir, nullptr, svroff.as<int64_t>(),
+                                                                         srow.as<uint8_t>());
+    srow_p = srow.p;
+  }
+  HIPCHK(shdr.reserve(8 * (oc + 1)));
+  if (oc)
+    k_pack_hdr<<<(int)grid_for(oc, 256, kMaxGrid), 256, 0, cst>>>(
+        oc, Po.cp, rfmt == 1 ? saux.as<int64_t>() : rfmt == 2 ? svr.as<int64_t>() : nullptr, shdr.as<int64_t>());
+  const void* sval_p = Po.val;
+  if (vfmt) {
+    HIPCHK(sval.reserve(sval_b + 16));
+    if (vfmt == 1)
+      k_f64_to_f32<<<(int)grid_for(n, 256, kMaxGrid), 256, 0, cst>>>(n, (const double*)Po.val, sval.as<float>());
+    else if (vfmt == 2)
+      k_f64_to_u16<<<(int)grid_for(n, 256, kMaxGrid), 256, 0, cst>>>(n, (const double*)Po.val, sval.as<unsigned short>());
+    else
+      k_var_encode<1><<<(int)grid_for(oc, 4, kMaxGrid * 2), 256, 0, cst>>>(oc, Po.cp, nullptr, (const double*)Po.val,
+                                                                           svvoff.as<int64_t>(), sval.as<uint8_t>());
+    sval_p = sval.p;
+  }
   HIPCHK(hipGetLastError());
-  bool narrow = dt == CBG_F64 && Po.val != nullptr && vs == 8;
-  if (narrow) {
-    const char* env = std::getenv("CBG_FIBER_NARROW");
-    narrow = !(env && env[0] == '0');
-  }
-  HIPCHK(G->small.reserve(128));
-  int64_t* dsn = G->small.as<int64_t>();   // [0..3] sent (flags, escapes), [4..7] received, [8..9] inexact counts
-  // rows as 16-bit gaps (k_gap_encode; CBG_FIBER_GAPS=0 sends int32 rows): escape counts packed into the column
-  // counts, their offsets by a scan, the escape total read back with the value verdict below
-  const char* genv = std::getenv("CBG_FIBER_GAPS");
-  const bool gaps = !(genv && genv[0] == '0') && oc > 0 && Po.nnz > 0;
-  if (gaps) {
-    HIPCHK(secnt.reserve(8 * (oc + 1)));
-    HIPCHK(splain.reserve(8 * (oc + 1)));
-    HIPCHK(seoff.reserve(8 * (oc + 1)));
-    const int64_t nt = (oc + kScanTile - 1) / kScanTile;
-    HIPCHK(tiles.reserve(8 * (nt + 1)));
-    HIPCHK(scal.reserve(16));
-    k_gap_count<<<(int)grid_for(oc, 4, kMaxGrid * 2), 256, 0, cst>>>(oc, Po.cp, Po.ir, scnt.as<int64_t>());
-    k_esc_counts<<<(int)grid_for(oc, 256, kMaxGrid), 256, 0, cst>>>(oc, scnt.as<int64_t>(), secnt.as<int64_t>(),
-                                                                   splain.as<int64_t>());
-    k_scan_tiles<<<(int)nt, 256, 0, cst>>>(oc, secnt.as<int64_t>(), tiles.as<int64_t>());
-    k_scan_sums<<<1, 1024, 0, cst>>>(nt, tiles.as<int64_t>(), scal.as<int64_t>());
-    k_scan_apply<<<(int)nt, 256, 0, cst>>>(oc, secnt.as<int64_t>(), tiles.as<int64_t>(), seoff.as<int64_t>());
-    HIPCHK(hipGetLastError());
-  }
-  // wire format of this rank's values (each direction its own, announced with the counts): 2 = u16 (integers
-  // 0..65535), 1 = f32 (bit-exact round trip), 0 = native
-  int lvl = 0;
-  int64_t sE = 0;
-  if (narrow) {
-    HIPCHK(hipMemsetAsync(dsn + 8, 0, 16, cst));
-    if (Po.nnz) k_narrow_check<<<(int)grid_for(Po.nnz, 256, kMaxGrid), 256, 0, cst>>>(
-        Po.nnz, (const double*)Po.val, (unsigned long long*)(dsn + 8));
-  }
-  int64_t nb[2] = {0, 0};
-  if (narrow) HIPCHK(hipMemcpyAsync(nb, dsn + 8, 16, hipMemcpyDeviceToHost, cst));
-  if (gaps) HIPCHK(hipMemcpyAsync(&sE, seoff.as<int64_t>() + oc, 8, hipMemcpyDeviceToHost, cst));
-  if (narrow || gaps) HIPCHK(hipStreamSynchronize(cst));
-  if (narrow) lvl = nb[1] == 0 ? 2 : nb[0] == 0 ? 1 : 0;
-  if (gaps) {
-    HIPCHK(sgap.reserve(2 * Po.nnz + 16));
-    HIPCHK(sesc.reserve(4 * sE + 16));
-    k_gap_encode<<<(int)grid_for(oc, 4, kMaxGrid * 2), 256, 0, cst>>>(oc, Po.cp, Po.ir, seoff.as<int64_t>(),
-                                                                      sgap.as<unsigned short>(), sesc.as<int32_t>());
-    HIPCHK(hipGetLastError());
-  }
-  const int64_t kNarrowBit = 1LL << 62, kU16Bit = 1LL << 61, kGapBit = 1LL << 60;
-  int64_t sflag[4] = {0, 0, 0, 0}, rflag[4] = {0, 0, 0, 0};
-  sflag[2 * other] = Po.nnz | (lvl >= 1 ? kNarrowBit : 0) | (lvl == 2 ? kU16Bit : 0) | (gaps ? kGapBit : 0);
-  sflag[2 * other + 1] = sE;
-  HIPCHK(hipMemcpyAsync(dsn, sflag, 32, hipMemcpyHostToDevice, cst));
-  const int64_t sixteen[2] = {16, 16};
-  CBGCHK(t_alltoallv(G, CBG_GROUP_FIBER, dsn, sixteen, dsn + 4, sixteen));
-  HIPCHK(hipMemcpyAsync(rflag, dsn + 4, 32, hipMemcpyDeviceToHost, cst));
+  // the count exchange: [entries | rows format << 56 | values format << 58, escapes, row bytes, value bytes]
+  int64_t sflag[8] = {0, 0, 0, 0, 0, 0, 0, 0}, rflag[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  sflag[4 * other + 0] = n | ((int64_t)rfmt << 56) | ((int64_t)vfmt << 58);
+  sflag[4 * other + 1] = rfmt == 1 ? tot[0] : 0;
+  sflag[4 * other + 2] = srow_b;
+  sflag[4 * other + 3] = sval_b;
+  HIPCHK(hipMemcpyAsync(dsn, sflag, 64, hipMemcpyHostToDevice, cst));
+  const int64_t thirtytwo[2] = {32, 32};
+  CBGCHK(t_alltoallv(G, CBG_GROUP_FIBER, dsn, thirtytwo, dsn + 8, thirtytwo));
+  HIPCHK(hipMemcpyAsync(rflag, dsn + 8, 64, hipMemcpyDeviceToHost, cst));
   HIPCHK(hipStreamSynchronize(cst));
-  const int64_t rf = rflag[2 * other];
-  const int rlvl = (rf & kU16Bit) ? 2 : (rf & kNarrowBit) ? 1 : 0;
-  const bool rgaps = (rf & kGapBit) != 0;
-  const int64_t rnnz = rf & ~(kNarrowBit | kU16Bit | kGapBit), rE = rflag[2 * other + 1];
+  const int64_t rf = rflag[4 * other];
+  const int rrfmt = (int)((rf >> 56) & 3), rvfmt = (int)((rf >> 58) & 3);
+  const int64_t rnnz = rf & ((1LL << 56) - 1), rE = rflag[4 * other + 1], rrow_b = rflag[4 * other + 2],
+                rval_b = rflag[4 * other + 3];
   // 3. receive storage (rows, then values; the counts behind them) and the exchange
   const int64_t ir_bytes = (4 * rnnz + 15) & ~15LL;
   HIPCHK(rx->ir.reserve(ir_bytes + vs * rnnz + 16));
   HIPCHK(rx->val.reserve(8 * (myc + 1)));
   char* rbase = rx->ir.as<char>();
   int64_t* rcnt = rx->val.as<int64_t>();
-  const void* sval = Po.val;
-  void* rval = Po.val ? (void*)(rbase + ir_bytes) : nullptr;
-  auto wire_of = [&](int l) { return l == 2 ? (int64_t)2 : l == 1 ? (int64_t)4 : (int64_t)vs; };
-  const int64_t wire = wire_of(lvl), wire_r = wire_of(rlvl);
-  if (lvl >= 1) {
-    HIPCHK(s32.reserve(wire * Po.nnz + 16));
-    if (Po.nnz && lvl == 2)
-      k_f64_to_u16<<<(int)grid_for(Po.nnz, 256, kMaxGrid), 256, 0, cst>>>(Po.nnz, (const double*)Po.val,
-                                                                          s32.as<unsigned short>());
-    else if (Po.nnz)
-      k_f64_to_f32<<<(int)grid_for(Po.nnz, 256, kMaxGrid), 256, 0, cst>>>(Po.nnz, (const double*)Po.val,
-                                                                          s32.as<float>());
-    HIPCHK(hipGetLastError());
-    sval = s32.p;
-  }
-  if (rlvl >= 1) {
-    HIPCHK(r32.reserve(wire_r * rnnz + 16));
-    rval = r32.p;
-  }
-  // rows: int32, or the 16-bit gaps and the escaped rows (escape buffers always allocated: a transport may be
-  // handed them with zero bytes)
-  HIPCHK(sesc.reserve(16));
-  HIPCHK(resc.reserve(16));
-  const void* srow = gaps ? sgap.p : (const void*)Po.ir;
-  const int64_t srow_b = gaps ? 2 * Po.nnz : 4 * Po.nnz, rrow_b = rgaps ? 2 * rnnz : 4 * rnnz;
-  void* rrow = rbase;
-  if (rgaps) {
-    HIPCHK(rgap.reserve(2 * rnnz + 16));
-    HIPCHK(resc.reserve(4 * rE + 16));
-    rrow = rgap.p;
-  }
-  const bool has_val = Po.val != nullptr;
+  void* rrow_p = rbase;
+  if (rrfmt) { HIPCHK(rrow.reserve(rrow_b + 16)); rrow_p = rrow.p; }
+  HIPCHK(resc.reserve(4 * (rrfmt == 1 ? rE : 0) + 16));
+  HIPCHK(sesc.reserve(16));   // a transport may be handed the escape buffers with zero bytes
+  void* rval_p = has_val ? (void*)(rbase + ir_bytes) : nullptr;
+  if (has_val && rvfmt) { HIPCHK(rvbuf.reserve(rval_b + 16)); rval_p = rvbuf.p; }
+  if (vfmt == 3) HIPCHK(svhdr.reserve(8 * (oc + 1)));
+  if (vfmt == 3 && oc) HIPCHK(hipMemcpyAsync(svhdr.p, svv.p, 8 * oc, hipMemcpyDeviceToDevice, cst));
+  if (rvfmt == 3) HIPCHK(rvhdr.reserve(8 * (myc + 1)));
+  const int64_t svh_b = vfmt == 3 ? 8 * oc : 0, rvh_b = rvfmt == 3 ? 8 * myc : 0;
   const double t_setup = now_ms() - t0;
-  if (st) st->fiber_bytes += srow_b + (gaps ? 4 * sE : 0) + (has_val ? wire : 0) * Po.nnz + 8 * oc;
+  if (st) st->fiber_bytes += 8 * oc + srow_b + sesc_b + (has_val ? sval_b + svh_b : 0);
   const bool async = G->rccl;
   if (async) {
-    HIPCHK(hipEventRecord(G->ev_t[0], cst));   // counts and narrowed values are ready
+    HIPCHK(hipEventRecord(G->ev_t[0], cst));   // headers and encoded streams are ready
     HIPCHK(hipStreamWaitEvent(G->cs, G->ev_t[0], 0));
     HIPCHK(hipEventRecord(G->ev_t[1], G->cs));
     ncclComm_t f = G->comm[CBG_GROUP_FIBER];
     NCCLCHK(ncclGroupStart());
-    if (oc) NCCLCHK(ncclSend(scnt.p, (size_t)(8 * oc), ncclInt8, other, f, G->cs));
+    if (oc) NCCLCHK(ncclSend(shdr.p, (size_t)(8 * oc), ncclInt8, other, f, G->cs));
     if (myc) NCCLCHK(ncclRecv(rcnt, (size_t)(8 * myc), ncclInt8, other, f, G->cs));
-    if (Po.nnz) NCCLCHK(ncclSend(srow, (size_t)srow_b, ncclInt8, other, f, G->cs));
-    if (rnnz) NCCLCHK(ncclRecv(rrow, (size_t)rrow_b, ncclInt8, other, f, G->cs));
-    if (gaps && sE) NCCLCHK(ncclSend(sesc.p, (size_t)(4 * sE), ncclInt8, other, f, G->cs));
-    if (rgaps && rE) NCCLCHK(ncclRecv(resc.p, (size_t)(4 * rE), ncclInt8, other, f, G->cs));
-    if (has_val && Po.nnz) NCCLCHK(ncclSend(sval, (size_t)(wire * Po.nnz), ncclInt8, other, f, G->cs));
-    if (has_val && rnnz) NCCLCHK(ncclRecv(rval, (size_t)(wire_r * rnnz), ncclInt8, other, f, G->cs));
+    if (srow_b) NCCLCHK(ncclSend(srow_p, (size_t)srow_b, ncclInt8, other, f, G->cs));
+    if (rrow_b) NCCLCHK(ncclRecv(rrow_p, (size_t)rrow_b, ncclInt8, other, f, G->cs));
+    if (sesc_b) NCCLCHK(ncclSend(sesc.p, (size_t)sesc_b, ncclInt8, other, f, G->cs));
+    if (rrfmt == 1 && rE) NCCLCHK(ncclRecv(resc.p, (size_t)(4 * rE), ncclInt8, other, f, G->cs));
+    if (has_val && sval_b) NCCLCHK(ncclSend(sval_p, (size_t)sval_b, ncclInt8, other, f, G->cs));
+    if (has_val && rval_b) NCCLCHK(ncclRecv(rval_p, (size_t)rval_b, ncclInt8, other, f, G->cs));
+    if (has_val && svh_b) NCCLCHK(ncclSend(svhdr.p, (size_t)svh_b, ncclInt8, other, f, G->cs));
+    if (has_val && rvh_b) NCCLCHK(ncclRecv(rvhdr.p, (size_t)rvh_b, ncclInt8, other, f, G->cs));
     NCCLCHK(ncclGroupEnd());
     HIPCHK(hipEventRecord(G->ev_t[2], G->cs));
   } else {   // caller transport: synchronous segments (member `other` only)
     int64_t sb[2] = {0, 0}, rb[2] = {0, 0};
-    sb[other] = 8 * oc; rb[other] = 8 * myc;
-    CBGCHK(t_alltoallv(G, CBG_GROUP_FIBER, scnt.p, sb, rcnt, rb));
-    sb[other] = srow_b; rb[other] = rrow_b;
-    CBGCHK(t_alltoallv(G, CBG_GROUP_FIBER, srow, sb, rrow, rb));
-    sb[other] = gaps ? 4 * sE : 0; rb[other] = rgaps ? 4 * rE : 0;
-    if (sb[other] || rb[other]) CBGCHK(t_alltoallv(G, CBG_GROUP_FIBER, sesc.p, sb, resc.p, rb));
+    auto seg = [&](const void* sp, int64_t sn, void* rp, int64_t rn) -> cbg_status {
+      sb[other] = sn; rb[other] = rn;
+      if (sn || rn) CBGCHK(t_alltoallv(G, CBG_GROUP_FIBER, sp, sb, rp, rb));
+      return CBG_OK;
+    };
+    CBGCHK(seg(shdr.p, 8 * oc, rcnt, 8 * myc));
+    CBGCHK(seg(srow_p, srow_b, rrow_p, rrow_b));
+    CBGCHK(seg(sesc.p, sesc_b, resc.p, rrfmt == 1 ? 4 * rE : 0));
     if (has_val) {
-      sb[other] = wire * Po.nnz; rb[other] = wire_r * rnnz;
-      CBGCHK(t_alltoallv(G, CBG_GROUP_FIBER, sval, sb, rval, rb));
+      CBGCHK(seg(sval_p, sval_b, rval_p, rval_b));
+      CBGCHK(seg(svhdr.p ? svhdr.p : sesc.p, svh_b, rvhdr.p ? rvhdr.p : resc.p, rvh_b));
     }
   }
   // 4. the own columns, while the exchange runs on the communication stream.  RCCL's kernel needs 37.6 KB of LDS
@@ -1196,8 +1335,8 @@ cbg_status fiber_pipeline(cbg_grid* G, const cbg_dcsc_view& va, const cbg_dcsc_v
   // while it is in flight (the heavy kernels take their work from a ticket, so a workgroup held back by RCCL's
   // finds the work done instead of stretching the kernel)
   static const int reserve_env = [] {
-    const char* e = std::getenv("CBG_FIBER_RESERVE_CU");
-    return e ? std::max(0, atoi(e)) : kFiberReserveCu;
+    const char* x = std::getenv("CBG_FIBER_RESERVE_CU");
+    return x ? std::max(0, atoi(x)) : kFiberReserveCu;
   }();
   t0 = now_ms();
   cbg_csc_result Rm;
@@ -1208,7 +1347,7 @@ cbg_status fiber_pipeline(cbg_grid* G, const cbg_dcsc_view& va, const cbg_dcsc_v
   CBGCHK(sm);
   Piece Pm = piece_of_result(Rm);
   t_local += now_ms() - t0;
-  // 5. join, the received piece (colptr from its counts; f32 values widened), the merge in layer order
+  // 5. join, decode the received piece (colptr from its counts), the merge in layer order
   t0 = now_ms();
   float xfer_ms = 0.f;
   if (async) {
@@ -1216,41 +1355,43 @@ cbg_status fiber_pipeline(cbg_grid* G, const cbg_dcsc_view& va, const cbg_dcsc_v
     HIPCHK(hipEventSynchronize(G->ev_t[2]));
     (void)hipEventElapsedTime(&xfer_ms, G->ev_t[1], G->ev_t[2]);
   }
-  if (rlvl == 1 && has_val && rnnz)
-    k_f32_to_f64<<<(int)grid_for(rnnz, 256, kMaxGrid), 256, 0, cst>>>(rnnz, r32.as<float>(), (double*)(rbase + ir_bytes));
-  if (rlvl == 2 && has_val && rnnz)
-    k_u16_to_f64<<<(int)grid_for(rnnz, 256, kMaxGrid), 256, 0, cst>>>(rnnz, r32.as<unsigned short>(),
-                                                                     (double*)(rbase + ir_bytes));
   std::shared_ptr<Owner> co(new Owner(ctx->pool));
   HIPCHK(co->cp.reserve(8 * (myc + 1)));
-  const int64_t ntiles = (myc + kScanTile - 1) / kScanTile;
-  HIPCHK(tiles.reserve(8 * (ntiles + 1)));
-  HIPCHK(scal.reserve(16));
-  if (rgaps && myc > 0) {   // escape counts out of the packed counts, their offsets
-    HIPCHK(recnt.reserve(8 * (myc + 1)));
-    HIPCHK(reoff.reserve(8 * (myc + 1)));
-    k_esc_counts<<<(int)grid_for(myc, 256, kMaxGrid), 256, 0, cst>>>(myc, rcnt, recnt.as<int64_t>(), rcnt);
-    k_scan_tiles<<<(int)ntiles, 256, 0, cst>>>(myc, recnt.as<int64_t>(), tiles.as<int64_t>());
-    k_scan_sums<<<1, 1024, 0, cst>>>(ntiles, tiles.as<int64_t>(), scal.as<int64_t>());
-    k_scan_apply<<<(int)ntiles, 256, 0, cst>>>(myc, recnt.as<int64_t>(), tiles.as<int64_t>(), reoff.as<int64_t>());
+  if (rrfmt && myc > 0) {   // row aux (escapes or row bytes) out of the headers, its offsets
+    HIPCHK(raux.reserve(8 * (myc + 1)));
+    HIPCHK(rauxoff.reserve(8 * (myc + 1)));
+    k_split_hdr<<<(int)grid_for(myc, 256, kMaxGrid), 256, 0, cst>>>(myc, rcnt, raux.as<int64_t>());
+    CBGCHK(scan(myc, raux.as<int64_t>(), rauxoff.as<int64_t>(), dtot + 3));
   }
-  if (myc > 0) {
-    k_scan_tiles<<<(int)ntiles, 256, 0, cst>>>(myc, rcnt, tiles.as<int64_t>());
-    k_scan_sums<<<1, 1024, 0, cst>>>(ntiles, tiles.as<int64_t>(), scal.as<int64_t>());
-    k_scan_apply<<<(int)ntiles, 256, 0, cst>>>(myc, rcnt, tiles.as<int64_t>(), co->cp.as<int64_t>());
-  } else {
-    HIPCHK(hipMemsetAsync(co->cp.p, 0, 8, cst));
+  CBGCHK(scan(myc, rcnt, co->cp.as<int64_t>(), dtot + 4));
+  int32_t* rir = (int32_t*)rbase;
+  if (rrfmt == 1 && myc > 0)
+    k_gap_decode<<<(int)grid_for(myc, 4, kMaxGrid * 2), 256, 0, cst>>>(myc, co->cp.as<int64_t>(), rauxoff.as<int64_t>(),
+                                                                       rrow.as<unsigned short>(), resc.as<int32_t>(), rir);
+  else if (rrfmt == 2 && myc > 0)
+    k_var_decode<0><<<(int)grid_for(myc, 4, kMaxGrid * 2), 256, 0, cst>>>(myc, co->cp.as<int64_t>(),
+                                                                          rauxoff.as<int64_t>(), rrow.as<uint8_t>(), rir,
+                                                                          nullptr);
+  double* rv = (double*)(rbase + ir_bytes);
+  if (has_val && rnnz) {
+    if (rvfmt == 1)
+      k_f32_to_f64<<<(int)grid_for(rnnz, 256, kMaxGrid), 256, 0, cst>>>(rnnz, rvbuf.as<float>(), rv);
+    else if (rvfmt == 2)
+      k_u16_to_f64<<<(int)grid_for(rnnz, 256, kMaxGrid), 256, 0, cst>>>(rnnz, rvbuf.as<unsigned short>(), rv);
+    else if (rvfmt == 3) {
+      HIPCHK(rvoff.reserve(8 * (myc + 1)));
+      CBGCHK(scan(myc, rvhdr.as<int64_t>(), rvoff.as<int64_t>(), dtot + 5));
+      k_var_decode<1><<<(int)grid_for(myc, 4, kMaxGrid * 2), 256, 0, cst>>>(myc, co->cp.as<int64_t>(),
+                                                                            rvoff.as<int64_t>(), rvbuf.as<uint8_t>(),
+                                                                            nullptr, rv);
+    }
   }
-  if (rgaps && myc > 0)
-    k_gap_decode<<<(int)grid_for(myc, 4, kMaxGrid * 2), 256, 0, cst>>>(myc, co->cp.as<int64_t>(), reoff.as<int64_t>(),
-                                                                       rgap.as<unsigned short>(), resc.as<int32_t>(),
-                                                                       (int32_t*)rbase);
   HIPCHK(hipGetLastError());
   Piece Pr;
   Pr.nrow = Pm.nrow; Pr.ncol = myc; Pr.nnz = rnnz;
   Pr.cp = co->cp.as<int64_t>();
-  Pr.ir = (const int32_t*)rbase;
-  Pr.val = has_val ? (const void*)(rbase + ir_bytes) : nullptr;
+  Pr.ir = rir;
+  Pr.val = has_val ? (const void*)rv : nullptr;
   Pr.own = co;
   Pr.keep = rx;
   Po = Piece();   // the sent partial is no longer needed (the exchange has completed)

@@ -837,6 +837,9 @@ __device__ __forceinline__ V merge_pair(V a, V b) {
 #ifndef CBG_MERGE_PL
 #define CBG_MERGE_PL 4   // merged positions per lane per window (window = 64 * CBG_MERGE_PL)
 #endif
+#ifndef CBG_MERGE_LDS
+#define CBG_MERGE_LDS 1   // fill pass: values staged in LDS, merged output staged in LDS, coalesced loads/stores
+#endif
 constexpr int kMergePL = CBG_MERGE_PL;
 constexpr int kMergeW = kWave * kMergePL;
 
@@ -850,9 +853,13 @@ __global__ void __launch_bounds__(256) k_merge2(int64_t ncol, const int64_t* __r
                                                 unsigned long long* __restrict__ disorder) {
   constexpr int W = kMergeW, PL = kMergePL;
   __shared__ int32_t swin[4][2][W];
+  constexpr bool SV = FILL && CBG_MERGE_LDS;
+  __shared__ V svw[SV ? 4 : 1][2][SV ? W : 1];   // fill: the window's values (then the merged output's)
   const int w = threadIdx.x / kWave, l = lane_id();
   int32_t* sa = swin[w][0];
   int32_t* sb = swin[w][1];
+  V* sva = svw[SV ? w : 0][0];
+  V* svb = svw[SV ? w : 0][1];
   for (int64_t j = (int64_t)blockIdx.x * 4 + w; j < ncol; j += (int64_t)gridDim.x * 4) {
     int64_t ia = acp[j], ib = bcp[j];
     const int64_t ea = acp[j + 1], eb = bcp[j + 1];
@@ -865,6 +872,10 @@ __global__ void __launch_bounds__(256) k_merge2(int64_t ncol, const int64_t* __r
         const int x = l + r * kWave;
         sa[x] = ia + x < ea ? air[ia + x] : INT32_MAX;
         sb[x] = ib + x < eb ? bir[ib + x] : INT32_MAX;
+        if (SV) {   // coalesced value loads: the merge reads them from LDS
+          sva[x] = ia + x < ea ? (aval ? aval[ia + x] : V(1)) : V(0);
+          svb[x] = ib + x < eb ? (bval ? bval[ib + x] : V(1)) : V(0);
+        }
       }
       wave_sync();
       if (!FILL) {   // the merge needs strictly ascending rows per column: verify in the count pass
@@ -915,21 +926,49 @@ __global__ void __launch_bounds__(256) k_merge2(int64_t ncol, const int64_t* __r
 #pragma unroll
       for (int e = 0; e < PL; ++e) nin += d0 + e < K && row[e] != INT32_MAX;
       const int ta = (int)wave_sum64(na), tin = (int)wave_sum64(nin);
-      if (FILL) {
+      if (FILL && !SV) {
         int64_t pos = o + incl - c;
 #pragma unroll
         for (int e = 0; e < PL; ++e)
           if (head[e]) {
             const int s = src[e];
             V v = s >= 0 ? (aval ? aval[ia + s] : V(1)) : (bval ? bval[ib + (-1 - s)] : V(1));
-            if (pair[e]) {   // the part-1 half is the next part-1 element: index (positions so far) - (part-0 taken)
-              const int jn = d0 + e - s;   // part-1 elements before this position
-              v = merge_pair<SRI, V>(v, bval ? bval[ib + jn] : V(1));
-            }
+            if (pair[e]) v = merge_pair<SRI, V>(v, bval ? bval[ib + d0 + e - s] : V(1));
             crow[pos] = row[e];
             cval[pos] = v;
             ++pos;
           }
+      }
+      if (SV) {
+        V ov[PL];
+#pragma unroll
+        for (int e = 0; e < PL; ++e) {
+          const int s = src[e];
+          V v = V(0);
+          if (head[e]) {
+            v = s >= 0 ? sva[s] : svb[-1 - s];
+            if (pair[e]) v = merge_pair<SRI, V>(v, svb[d0 + e - s]);   // part-1 half: (positions so far) - (part-0 taken)
+          }
+          ov[e] = v;
+        }
+        wave_sync();   // every lane's reads of the staged window are done: the output is staged over it
+        int p = incl - c;
+#pragma unroll
+        for (int e = 0; e < PL; ++e)
+          if (head[e]) {
+            sa[p] = row[e];
+            sva[p] = ov[e];
+            ++p;
+          }
+        wave_sync();
+#pragma unroll
+        for (int r = 0; r < PL; ++r) {   // coalesced stores of the window's merged entries
+          const int x = l + r * kWave;
+          if (x < tot) {
+            crow[o + x] = sa[x];
+            cval[o + x] = sva[x];
+          }
+        }
       }
       o += tot;
       ia += ta;

@@ -51,7 +51,7 @@
 extern "C" {
 #endif
 
-#define CBG_ABI_VERSION 1
+#define CBG_ABI_VERSION 2   /* 2: cbg_grid_stats.fiber_xfer_ms after stages; cbg_device_count */
 
 typedef enum {
   CBG_OK = 0,
@@ -122,6 +122,8 @@ typedef struct {
 int32_t     cbg_abi_version(void);
 const char* cbg_strerror(cbg_status s);
 
+/* Number of visible HIP devices (the C++ drop-in binds MPI rank r to device node-local-rank % count). */
+cbg_status cbg_device_count(int32_t* n);
 cbg_status cbg_init(int device, cbg_ctx** ctx);
 cbg_status cbg_destroy(cbg_ctx* ctx);
 /* Use an external HIP stream (hipStream_t) for all subsequent work on ctx; NULL = own stream. */
@@ -301,8 +303,9 @@ typedef struct {
   int64_t multiplies;          /* this rank's local multiplies */
   int64_t bcast_bytes, fiber_bytes;
   double bcast_ms, local_ms, merge_ms, fiber_ms, total_ms;
-  double fiber_xfer_ms;        /* two layers: the fiber transfer on the communication stream (overlaps local_ms) */
   int32_t stages;
+  /* ABI 2: fields after `stages` (callers built against ABI 1 never read past it) */
+  double fiber_xfer_ms;        /* two layers: the fiber transfer on the communication stream (overlaps local_ms) */
 } cbg_grid_stats;
 
 /* RCCL unique id (128 bytes) made on one rank and handed to all (any out-of-band channel). */

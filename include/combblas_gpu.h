@@ -40,6 +40,7 @@
 #define COMBBLAS_GPU_H
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstdint>
 #include <memory>
 #include <stdexcept>
@@ -83,13 +84,29 @@ inline void check(cbg_status s, const char* where) {
   if (s != CBG_OK) throw std::runtime_error(std::string(where) + ": " + cbg_strerror(s));
 }
 
-// one context per process/host thread, on the device the caller selected (default 0)
+// One context per process/host thread.  context(d) selects device d; without a choice, an MPI process takes its
+// node-local rank's device (rank within MPI_COMM_TYPE_SHARED, modulo the visible devices: one GPU per rank on an
+// 8-GPU node), any other process device 0.
+inline int node_local_device() {
+  int init = 0, fin = 0;
+  MPI_Initialized(&init);
+  MPI_Finalized(&fin);
+  int32_t n = 0;
+  if (!init || fin || cbg_device_count(&n) != CBG_OK || n <= 0) return 0;
+  MPI_Comm node;
+  MPI_Comm_split_type(MPI_COMM_WORLD, MPI_COMM_TYPE_SHARED, 0, MPI_INFO_NULL, &node);
+  int lr = 0;
+  MPI_Comm_rank(node, &lr);
+  MPI_Comm_free(&node);
+  return lr % n;
+}
+
 inline cbg_ctx* context(int device = -1) {
   static thread_local cbg_ctx* ctx = nullptr;
   static thread_local int dev = 0;
   if (device >= 0 && ctx && device != dev) { cbg_destroy(ctx); ctx = nullptr; }
   if (!ctx) {
-    dev = device >= 0 ? device : 0;
+    dev = device >= 0 ? device : node_local_device();
     check(cbg_init(dev, &ctx), "cbg_init");
   }
   return ctx;
@@ -237,51 +254,180 @@ SpTuples<IT, NT>* MultiwayMergeHash(std::vector<SpTuples<IT, NT>*>& lists, IT md
   }
 }
 
-// MCLPruneRecoverySelect (ParFriends.h:185-353) on an SpParMat whose local blocks hold complete
-// columns (one processor row: every column's nonzeros are on one rank) -> cbg_mcl_prune on the
-// device, in place.  Otherwise (columns split over processor rows, or a non-float NT) the
-// reference's own distributed version runs.
+// MCLPruneRecoverySelect (ParFriends.h:185-353) on the device: the statistics, the k-th-value selection and the
+// prune of every column (cbg_mcl_prune) need complete columns.  On a q x q grid each processor column's q row blocks
+// are gathered column group by column group (group m of the local columns goes to the column's rank m, one
+// MPI_Alltoallv; the role of the processor-column Reduce / Kselect1 exchanges, SpParMat.cpp:1413-1700), pruned on
+// the device, and scattered back by row block.  A non-float NT runs the reference's own version.
+template <class LIT, class NT, class DER>
+void block_to_csc(DER& L, std::vector<int64_t>& cp, std::vector<int32_t>& row, std::vector<NT>& val) {
+  SpTuples<LIT, NT> T(L);
+  T.SortColBased();
+  const int64_t ncol = L.getncol(), nnz = T.getnnz();
+  cp.assign(ncol + 1, 0);
+  row.resize(nnz);
+  val.resize(nnz);
+  for (int64_t k = 0; k < nnz; ++k) {
+    ++cp[T.colindex(k) + 1];
+    row[k] = (int32_t)T.rowindex(k);
+    val[k] = T.numvalue(k);
+  }
+  for (int64_t j = 0; j < ncol; ++j) cp[j + 1] += cp[j];
+}
+
+template <class NT>
+void mcl_prune_host_csc(int64_t nrow, int64_t ncol, std::vector<int64_t>& cp, std::vector<int32_t>& row,
+                        std::vector<NT>& val, NT thr, int64_t sel, int64_t rec, NT pct) {
+  cbg_ctx* ctx = context();
+  cbg_dcsc_view v{};
+  v.nrow = nrow; v.ncol = ncol; v.nnz = cp[ncol]; v.nzc = ncol;
+  v.cp = cp.data(); v.ir = row.empty() ? nullptr : row.data(); v.idx_bytes = 4; v.ptr_bytes = 8;
+  v.val = val.empty() ? nullptr : val.data(); v.val_type = DeviceType<NT>::code; v.on_device = 0;
+  cbg_csc_result D{}, P{};
+  check(cbg_upload(ctx, &v, &D), "cbg_upload");
+  cbg_status s = cbg_mcl_prune(ctx, &D, (double)thr, sel, rec, (double)pct, &P, nullptr);
+  cbg_result_free(ctx, &D);
+  check(s, "cbg_mcl_prune");
+  cp.assign(ncol + 1, 0);
+  row.resize(P.nnz);
+  val.resize(P.nnz);
+  s = cbg_result_to_host(ctx, &P, cp.data(), P.nnz ? row.data() : nullptr, P.nnz ? val.data() : nullptr);
+  cbg_result_free(ctx, &P);
+  check(s, "cbg_result_to_host");
+}
+
+inline void mpi_counts(const std::vector<int64_t>& n, std::vector<int>& c, std::vector<int>& d, size_t elem) {
+  c.resize(n.size());
+  d.resize(n.size());
+  int64_t o = 0;
+  for (size_t m = 0; m < n.size(); ++m) {
+    if (n[m] * (int64_t)elem > INT32_MAX || o * (int64_t)elem > INT32_MAX)
+      throw std::runtime_error("MCLPruneRecoverySelect: a column exchange above 2^31 bytes per rank");
+    c[m] = (int)(n[m] * (int64_t)elem);
+    d[m] = (int)(o * (int64_t)elem);
+    o += n[m];
+  }
+}
+
 template <class IT, class NT, class DER>
 void MCLPruneRecoverySelect(SpParMat<IT, NT, DER>& A, NT hardThreshold, IT selectNum, IT recoverNum,
                             NT recoverPct, int kselectVersion) {
   constexpr bool dev = std::is_same<NT, double>::value || std::is_same<NT, float>::value;
+  (void)kselectVersion;   // Kselect1 / Kselect2 pick the same k-th value
   if constexpr (!dev) {
     combblas::MCLPruneRecoverySelect(A, hardThreshold, selectNum, recoverNum, recoverPct, kselectVersion);
   } else {
-    if (A.getcommgrid()->GetGridRows() != 1) {
-      combblas::MCLPruneRecoverySelect(A, hardThreshold, selectNum, recoverNum, recoverPct, kselectVersion);
-      return;
-    }
     typedef typename DER::LocalIT LIT;
     DER& L = A.seq();
-    cbg_ctx* ctx = context();
-    // local block -> host CSC (int64 colptr, int32 rows) -> device
-    SpTuples<LIT, NT> T(L);
-    T.SortColBased();
-    const int64_t ncol = L.getncol(), nnz = T.getnnz();
-    std::vector<int64_t> cp(ncol + 1, 0);
-    std::vector<int32_t> row(nnz > 0 ? nnz : 1);
-    std::vector<NT> val(nnz > 0 ? nnz : 1);
-    for (int64_t k = 0; k < nnz; ++k) {
-      ++cp[T.colindex(k) + 1];
-      row[k] = (int32_t)T.rowindex(k);
-      val[k] = T.numvalue(k);
+    std::vector<int64_t> cp;
+    std::vector<int32_t> row;
+    std::vector<NT> val;
+    block_to_csc<LIT, NT>(L, cp, row, val);
+    const int64_t nrl = L.getnrow(), ncl = L.getncol();
+    MPI_Comm colw = A.getcommgrid()->GetColWorld();
+    int q = 1, me = 0;
+    MPI_Comm_size(colw, &q);
+    MPI_Comm_rank(colw, &me);
+    if (q == 1) {
+      mcl_prune_host_csc<NT>(nrl, ncl, cp, row, val, hardThreshold, (int64_t)selectNum, (int64_t)recoverNum, recoverPct);
+    } else {
+      // row offsets of the processor column's q row blocks; column groups of the local columns
+      std::vector<int64_t> nrows(q), roff(q + 1, 0);
+      MPI_Allgather(&nrl, 1, MPI_INT64_T, nrows.data(), 1, MPI_INT64_T, colw);
+      for (int i = 0; i < q; ++i) roff[i + 1] = roff[i] + nrows[i];
+      auto grp = [&](int m, int64_t n, int64_t* g0, int64_t* g1) {
+        *g0 = (n / q) * m;
+        *g1 = m == q - 1 ? n : *g0 + n / q;
+      };
+      // 1. gather: group m of my columns (counts, rows, values) -> rank m of the processor column
+      std::vector<int64_t> scol(q), snz(q), rcol(q), rnz(q);
+      for (int m = 0; m < q; ++m) {
+        int64_t g0, g1;
+        grp(m, ncl, &g0, &g1);
+        scol[m] = g1 - g0;
+        snz[m] = cp[g1] - cp[g0];
+      }
+      MPI_Alltoall(snz.data(), 1, MPI_INT64_T, rnz.data(), 1, MPI_INT64_T, colw);
+      MPI_Alltoall(scol.data(), 1, MPI_INT64_T, rcol.data(), 1, MPI_INT64_T, colw);
+      const int64_t ng = rcol[0];   // every source holds the same local columns (one processor column)
+      std::vector<int64_t> scnt(ncl), rcnt((size_t)q * ng);
+      for (int64_t j = 0; j < ncl; ++j) scnt[j] = cp[j + 1] - cp[j];
+      int64_t rtot = 0;
+      for (int i = 0; i < q; ++i) rtot += rnz[i];
+      std::vector<int32_t> rrow(rtot);
+      std::vector<NT> rval(rtot);
+      std::vector<int> sc, sd, rc, rd;
+      mpi_counts(scol, sc, sd, 8); mpi_counts(rcol, rc, rd, 8);
+      MPI_Alltoallv(scnt.data(), sc.data(), sd.data(), MPI_BYTE, rcnt.data(), rc.data(), rd.data(), MPI_BYTE, colw);
+      mpi_counts(snz, sc, sd, 4); mpi_counts(rnz, rc, rd, 4);
+      MPI_Alltoallv(row.data(), sc.data(), sd.data(), MPI_BYTE, rrow.data(), rc.data(), rd.data(), MPI_BYTE, colw);
+      mpi_counts(snz, sc, sd, sizeof(NT)); mpi_counts(rnz, rc, rd, sizeof(NT));
+      MPI_Alltoallv(val.data(), sc.data(), sd.data(), MPI_BYTE, rval.data(), rc.data(), rd.data(), MPI_BYTE, colw);
+      // complete columns: for every column, source 0's rows (+ roff[0]), then source 1's, ...
+      std::vector<int64_t> fcp(ng + 1, 0);
+      for (int i = 0; i < q; ++i)
+        for (int64_t c = 0; c < ng; ++c) fcp[c + 1] += rcnt[(size_t)i * ng + c];
+      for (int64_t c = 0; c < ng; ++c) fcp[c + 1] += fcp[c];
+      std::vector<int32_t> frow(rtot);
+      std::vector<NT> fval(rtot);
+      {
+        std::vector<int64_t> cur(fcp.begin(), fcp.end() - 1);
+        int64_t src = 0;
+        for (int i = 0; i < q; ++i)
+          for (int64_t c = 0; c < ng; ++c)
+            for (int64_t k = 0; k < rcnt[(size_t)i * ng + c]; ++k, ++src) {
+              frow[cur[c]] = (int32_t)(rrow[src] + roff[i]);
+              fval[cur[c]++] = rval[src];
+            }
+      }
+      // 2. prune the complete columns on the device
+      mcl_prune_host_csc<NT>(roff[q], ng, fcp, frow, fval, hardThreshold, (int64_t)selectNum, (int64_t)recoverNum,
+                             recoverPct);
+      // 3. scatter: row block i of the pruned group -> rank i (counts per column, rows rebased, values)
+      std::vector<int64_t> bcnt((size_t)q * ng, 0), bnz(q, 0), bcol(q, ng);
+      for (int64_t c = 0; c < ng; ++c)
+        for (int64_t k = fcp[c]; k < fcp[c + 1]; ++k) {
+          const int i = (int)(std::upper_bound(roff.begin(), roff.end(), (int64_t)frow[k]) - roff.begin()) - 1;
+          ++bcnt[(size_t)i * ng + c];
+          ++bnz[i];
+        }
+      std::vector<int32_t> brow(fcp[ng]);
+      std::vector<NT> bval(fcp[ng]);
+      {
+        std::vector<int64_t> boff(q + 1, 0);
+        for (int i = 0; i < q; ++i) boff[i + 1] = boff[i] + bnz[i];
+        for (int64_t c = 0; c < ng; ++c)   // rows ascend within a column, so each block's entries stay in order
+          for (int64_t k = fcp[c]; k < fcp[c + 1]; ++k) {
+            const int i = (int)(std::upper_bound(roff.begin(), roff.end(), (int64_t)frow[k]) - roff.begin()) - 1;
+            brow[boff[i]] = (int32_t)(frow[k] - roff[i]);
+            bval[boff[i]++] = fval[k];
+          }
+      }
+      std::vector<int64_t> gnz(q), gcol(q);
+      MPI_Alltoall(bnz.data(), 1, MPI_INT64_T, gnz.data(), 1, MPI_INT64_T, colw);
+      MPI_Alltoall(bcol.data(), 1, MPI_INT64_T, gcol.data(), 1, MPI_INT64_T, colw);
+      std::vector<int64_t> gcnt(ncl);
+      int64_t gtot = 0;
+      for (int m = 0; m < q; ++m) gtot += gnz[m];
+      row.resize(gtot);
+      val.resize(gtot);
+      mpi_counts(bcol, sc, sd, 8); mpi_counts(gcol, rc, rd, 8);
+      MPI_Alltoallv(bcnt.data(), sc.data(), sd.data(), MPI_BYTE, gcnt.data(), rc.data(), rd.data(), MPI_BYTE, colw);
+      mpi_counts(bnz, sc, sd, 4); mpi_counts(gnz, rc, rd, 4);
+      MPI_Alltoallv(brow.data(), sc.data(), sd.data(), MPI_BYTE, row.data(), rc.data(), rd.data(), MPI_BYTE, colw);
+      mpi_counts(bnz, sc, sd, sizeof(NT)); mpi_counts(gnz, rc, rd, sizeof(NT));
+      MPI_Alltoallv(bval.data(), sc.data(), sd.data(), MPI_BYTE, val.data(), rc.data(), rd.data(), MPI_BYTE, colw);
+      // the q groups arrive in column order: the local block's columns, concatenated
+      cp.assign(ncl + 1, 0);
+      for (int64_t j = 0; j < ncl; ++j) cp[j + 1] = cp[j] + gcnt[j];
     }
-    for (int64_t j = 0; j < ncol; ++j) cp[j + 1] += cp[j];
-    cbg_dcsc_view v{};
-    v.nrow = L.getnrow(); v.ncol = ncol; v.nnz = nnz; v.nzc = ncol;
-    v.cp = cp.data(); v.ir = row.data(); v.idx_bytes = 4; v.ptr_bytes = 8;
-    v.val = val.data(); v.val_type = DeviceType<NT>::code; v.on_device = 0;
-    cbg_csc_result D{}, P{};
-    check(cbg_upload(ctx, &v, &D), "cbg_upload");
-    cbg_status s = cbg_mcl_prune(ctx, &D, (double)hardThreshold, (int64_t)selectNum, (int64_t)recoverNum,
-                                 (double)recoverPct, &P, nullptr);
-    cbg_result_free(ctx, &D);
-    check(s, "cbg_mcl_prune");
-    SpTuples<LIT, NT>* pt = to_tuples<LIT, NT>(ctx, P);
-    L = DER(*pt, false);
-    delete pt;
-    (void)kselectVersion;   // Kselect1 / Kselect2 pick the same k-th value
+    // host CSC -> the local block (column-sorted tuples, rows ascending)
+    const int64_t nnz = cp[ncl];
+    std::tuple<LIT, LIT, NT>* t = new std::tuple<LIT, LIT, NT>[nnz > 0 ? nnz : 1];
+    for (int64_t j = 0; j < ncl; ++j)
+      for (int64_t k = cp[j]; k < cp[j + 1]; ++k) t[k] = std::make_tuple((LIT)row[k], (LIT)j, val[k]);
+    SpTuples<LIT, NT> T(nnz, (LIT)nrl, (LIT)ncl, t, true, false);
+    L = DER(T, false);
   }
 }
 
@@ -323,22 +469,58 @@ struct GridHandle {
   ~GridHandle() { if (grid) cbg_grid_destroy(grid); }
 };
 
+// The grid under the distributed drivers: the library's own RCCL communicators (ncclCommInitRank on the world +
+// ncclCommSplit into row / column / fiber; device buffers, broadcasts and the fiber exchange on a communication
+// stream, over xGMI between the node's GPUs), the unique id handed out by an MPI_Bcast from world rank 0.
+// CBG_GRID_TRANSPORT=mpi takes the host-staged MPI transport instead (MpiTransport: D2H, MPI, H2D).
 // grid_rank: the rank's position l*rows*cols + i*cols + j in the library's grid numbering (default: its
 // rank in `world`, which is that numbering for CommGrid / CommGrid3D; CCGrid numbers layers fastest)
+// what the last distributed driver's grid ran over (cbg_grid_query: rccl = 1 and the members RCCL counts per
+// communicator, or the caller transport's group sizes)
+inline cbg_grid_info& last_grid_info() {
+  static thread_local cbg_grid_info gi{};
+  return gi;
+}
+
+inline bool grid_over_mpi() {
+  const char* t = std::getenv("CBG_GRID_TRANSPORT");
+  return t && std::string(t) == "mpi";
+}
+
 inline cbg_grid* make_grid(GridHandle& h, MPI_Comm world, MPI_Comm row, MPI_Comm col, MPI_Comm fiber, int layers,
                            int rows, int cols, int grid_rank = -1) {
+  int wsize = 0, wrank = 0;
+  MPI_Comm_size(world, &wsize);
+  MPI_Comm_rank(world, &wrank);
+  const int grank = grid_rank >= 0 ? grid_rank : wrank;
+  if (!grid_over_mpi()) {
+    // every rank learns whether rank 0 got an id, then every rank whether all communicators came up: a
+    // failure throws on all ranks together instead of leaving some blocked in a collective
+    char id[128] = {0};
+    int ok = wrank == 0 ? (cbg_rccl_unique_id(id) == CBG_OK) : 1;
+    MPI_Bcast(&ok, 1, MPI_INT, 0, world);
+    if (!ok) throw std::runtime_error("cbg_rccl_unique_id failed on rank 0");
+    MPI_Bcast(id, 128, MPI_BYTE, 0, world);
+    const cbg_status s = cbg_grid_create_rccl(context(), id, wsize, grank, layers, rows, cols, &h.grid);
+    int mine = s == CBG_OK, all = 0;
+    MPI_Allreduce(&mine, &all, 1, MPI_INT, MPI_MIN, world);
+    if (!all) {
+      if (h.grid) { cbg_grid_destroy(h.grid); h.grid = nullptr; }
+      throw std::runtime_error(std::string("cbg_grid_create_rccl: ") + cbg_strerror(s == CBG_OK ? CBG_ECOMM : s));
+    }
+    check(cbg_grid_query(h.grid, &last_grid_info()), "cbg_grid_query");
+    return h.grid;
+  }
   h.mt.comm[CBG_GROUP_ROW] = row; h.mt.comm[CBG_GROUP_COL] = col;
   h.mt.comm[CBG_GROUP_FIBER] = fiber; h.mt.comm[CBG_GROUP_WORLD] = world;
   cbg_transport t{};
   t.user = &h.mt; t.bcast = &MpiTransport::bcast; t.alltoallv = &MpiTransport::alltoallv;
   t.allgather = &MpiTransport::allgather; t.host_buffers = 1;
-  int wsize = 0, wrank = 0;
-  MPI_Comm_size(world, &wsize);
-  MPI_Comm_rank(world, &wrank);
-  check(cbg_grid_create(context(), &t, wsize, grid_rank >= 0 ? grid_rank : wrank, layers, rows, cols, &h.grid),
-        "cbg_grid_create");
+  check(cbg_grid_create(context(), &t, wsize, grank, layers, rows, cols, &h.grid), "cbg_grid_create");
+  check(cbg_grid_query(h.grid, &last_grid_info()), "cbg_grid_query");
   return h.grid;
 }
+
 
 // the rank's product piece (device CSC) -> UDERO via column-sorted SpTuples
 template <class IU, class NUO, class UDERO>
@@ -542,7 +724,8 @@ void RestrictionOp(CCGrid& CMG, SpDCCols<IT, NT>* localmat, SpDCCols<IT, NT>*& R
   MPI_Gatherv(mine.data(), cnt, MPI_INT64_T, all.data(), cnts.data(), displs.data(), MPI_INT64_T, 0, lw);
   int64_t nagg = 0;
   std::vector<int64_t> agg;   // aggregate (column of R) of every vertex, on rank 0
-  if (lr == 0) {
+  std::string err;            // rank 0's failure, broadcast as a status so every rank throws together
+  if (lr == 0) try {
     const int64_t nnz = (int64_t)all.size() / 2;
     std::vector<int64_t> cp((size_t)N + 1, 0);
     for (int64_t k = 0; k < nnz; ++k) cp[(size_t)all[2 * k + 1] + 1]++;
@@ -565,7 +748,12 @@ void RestrictionOp(CCGrid& CMG, SpDCCols<IT, NT>* localmat, SpDCCols<IT, NT>*& R
     cbg_result_free(context(), &Rd);
     cbg_result_free(context(), &RTd);
     agg.assign(trow.begin(), trow.begin() + M);
+  } catch (std::exception& e) {
+    err = e.what();
   }
+  int failed = !err.empty();
+  MPI_Bcast(&failed, 1, MPI_INT, 0, lw);
+  if (failed) throw std::runtime_error(lr == 0 ? err : std::string("RestrictionOp failed on the layer's rank 0"));
   MPI_Bcast(&nagg, 1, MPI_INT64_T, 0, lw);
   agg.resize((size_t)M);
   MPI_Bcast(agg.data(), (int)M, MPI_INT64_T, 0, lw);

@@ -573,3 +573,61 @@ def run_galerkin_case(rank, world, port, backend_kind, cases, errq):
         import traceback
         errq.put(f"rank {rank}: {e!r}\n{traceback.format_exc()}")
         raise
+
+
+def _values_csc(n, m, density, seed, kind):
+    """Random CSC whose product exercises one fiber value format: 'small' (integers 1..4: varint, 1 byte),
+    'wide' (integers up to 3000: products above 65535, varint of 2-4 bytes), 'huge' (integers ~2^20: products above
+    2^32, neither varint nor f32 -> f64), 'real' (uniform reals: f64)."""
+    rng = np.random.default_rng(seed)
+    gen = {"small": lambda k: rng.integers(1, 5, k).astype(np.float64),
+           "wide": lambda k: rng.integers(1, 3000, k).astype(np.float64),
+           "huge": lambda k: rng.integers(1 << 20, 1 << 21, k).astype(np.float64),
+           "real": lambda k: rng.random(k)}[kind]
+    M = sp.random(n, m, density=density, format="csc", random_state=rng, data_rvs=gen)
+    M.sort_indices()
+    return M
+
+
+def run_fiber_case(rank, world, port, backend_kind, cases, errq):
+    """1x1x2 products whose fiber messages take every wire format (k_code_count picks per message): varint / 16-bit
+    gap / int32 rows (dense runs, tall sparse columns with gaps above 2^14 and 2^16, columns of one chunk and of many),
+    varint / u16 / f32 / f64 values; every rank's piece against scipy (exact for integer values, 1e-12 for reals),
+    and the bytes on the wire reported by the grid stats within the bound of the format expected."""
+    try:
+        init_group(rank, world, port, backend_kind)
+        L, q, _ = cbd.grid_for(world)
+        grid = cbd.CommGrid3D(L, q, q)
+        import combblas_amd as cb
+        be = cbd.GpuBackend(cb.Context(0))
+        for (n, k, m, dA, dB, seed, kind, max_bpe) in cases:
+            A = _values_csc(n, k, dA, seed, kind)
+            B = _values_csc(k, m, dB, seed + 1, kind)
+            Ad = cbd.SpParMat3D.from_global_csc(grid, n, k, A.indptr, A.indices, A.data, True, be)
+            Bd = cbd.SpParMat3D.from_global_csc(grid, k, m, B.indptr, B.indices, B.data, False, be)
+            stats = {}
+            C = cbd.Mult_AnXBn_SUMMA3D(cb_sr(backend_kind), Ad, Bd, stats)
+            R = (A @ B).tocsc()
+            R.sort_indices()
+            (r0, r1), (c0, c1) = C.local_range()
+            Rl = R[r0:r1, c0:c1].tocsc()
+            Rl.sort_indices()
+            blk = C.block
+            assert np.array_equal(blk.cp.cpu().numpy(), Rl.indptr), f"rank {rank} {kind}: colptr differs"
+            assert np.array_equal(blk.ir.cpu().numpy(), Rl.indices), f"rank {rank} {kind}: rows differ"
+            v = blk.val.cpu().numpy()
+            if kind == "real":
+                assert np.allclose(v, Rl.data, rtol=1e-12, atol=0), f"rank {rank} {kind}: values differ"
+            else:
+                assert np.array_equal(v, Rl.data), f"rank {rank} {kind}: values differ"
+            # what this rank sent: about half its layer partial (entries of the other layer's column half)
+            t = torch.tensor([stats.get("fiber_bytes", 0), R.nnz], dtype=torch.float64)
+            dist.all_reduce(t)
+            if max_bpe is not None and R.nnz > 0:
+                assert float(t[0]) <= max_bpe * R.nnz * 1.2 + 16 * m, (kind, float(t[0]), R.nnz)
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:
+        import traceback
+        errq.put(f"rank {rank}: {e!r}\n{traceback.format_exc()}")
+        raise

@@ -171,6 +171,11 @@ int run3d(int q, int L, const std::string& fa, const std::string& fc, const std:
     SpDCCols<IT3, double>* S = multiply(absA, absB, CMG, false, true);   // sum|a*b| per entry (reference)
     SpDCCols<IT3, double>* R = multiply(splitA, splitB, CMG, false, true);
     SpDCCols<IT3, double>* D = gpu::multiply(splitA, splitB, CMG, false, true);
+    {
+      const cbg_grid_info& gi = gpu::last_grid_info();
+      printf("GRID rccl=%d world=%d row=%d col=%d fiber=%d\n", gi.rccl, gi.ranks[CBG_GROUP_WORLD],
+             gi.ranks[CBG_GROUP_ROW], gi.ranks[CBG_GROUP_COL], gi.ranks[CBG_GROUP_FIBER]);
+    }
     SpTuples<IT3, double> st(*S);
     {
       SpTuples<IT3, double> dt(*D), rt(*R), ct(controlC), s2(st);
@@ -423,6 +428,9 @@ int main(int argc, char** argv) {
         delete dt; delete rc2;
       }
       delete rt;
+      const cbg_grid_info& gi = gpu::last_grid_info();   // the grid the drivers ran over
+      printf("GRID rccl=%d world=%d row=%d col=%d fiber=%d\n", gi.rccl, gi.ranks[CBG_GROUP_WORLD],
+             gi.ranks[CBG_GROUP_ROW], gi.ranks[CBG_GROUP_COL], gi.ranks[CBG_GROUP_FIBER]);
       int bad = rc, any = 0;
       MPI_Allreduce(&bad, &any, 1, MPI_INT, MPI_MAX, MPI_COMM_WORLD);
       rc = any;

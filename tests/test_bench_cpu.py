@@ -41,11 +41,11 @@ def test_fiber_wire_bytes_counts_gaps_escapes_and_values():
     b = cbd.Block(80000, 3, torch.tensor(cp, dtype=torch.int64), torch.tensor(rows, dtype=torch.int32),
                   torch.tensor(vals, dtype=torch.float64))
     w = bench.fiber_wire_bytes(b)
-    assert w["escapes"] == 1 and w["value_bytes"] == 2
-    assert w["bytes"] == 8 * 3 + 2 * 67 + 4 * 1 + 2 * 67
-    # column 2 as a bitmap (64 rows: 8 B + 8 B base < 128 B of gaps); 300 > 255: values stay u16
-    assert w["bitmap_columns"] == 1
-    assert w["bytes_bitmap_u8"] == 8 * 3 + (2 * 3 + 4) + (8 + 8) + 2 * 67
+    assert w["escapes"] == 1
+    assert w["row_bytes"] == {"int32": 4 * 67, "gap16": 2 * 67 + 4, "varint": 1 + 3 + 1 + 1 + 63}
+    assert w["value_bytes"]["u16"] == 2 * 67 and w["value_bytes"]["varint"] == 66 + 2 + 8 * 3
+    assert (w["rows"], w["values"]) == ("varint", "varint")
+    assert w["bytes"] == 8 * 3 + 69 + 92
 
 
 def test_round_tag_orders_evidence_files():

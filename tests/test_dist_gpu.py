@@ -126,3 +126,26 @@ def test_fiber_row_gaps_tall_sparse(kind, port):
     spawn_case(2, kind, [(2000000, 3000, 96, 5e-6, 0.002, 5),
                          (1000000, 3000, 120, 2e-5, 0.002, 7),
                          (300000, 500, 64, 1e-3, 0.2, 9)], port)
+
+
+# (n, k, m, density A, density B, seed, value kind, bound on wire bytes per output entry or None)
+FIBER_CASES = [(4000, 600, 300, 0.05, 0.05, 41, "small", 3.0),        # dense runs: 1-byte gaps and values
+               (300000, 500, 64, 1e-3, 0.2, 43, "small", None),       # gaps around 2^8..2^14
+               (2000000, 3000, 96, 5e-6, 0.002, 45, "wide", None),    # gaps above 2^16 (u16 escapes / 3-byte varint)
+               (3000, 400, 200, 0.05, 0.05, 47, "huge", None),        # products above 2^32: f64 values
+               (3000, 400, 200, 0.05, 0.05, 49, "real", None),        # reals: f64
+               (50, 40, 30, 0.0, 0.0, 51, "small", None)]             # empty product
+
+
+@pytest.mark.parametrize("env", ["default", "CBG_FIBER_VARINT=0", "CBG_FIBER_GAPS=0"])
+@pytest.mark.parametrize("kind,port", [("gpu", 29701), ("gpu-rccl-net", 29711)])
+def test_fiber_wire_formats(kind, port, env, monkeypatch):
+    """The fiber pipeline's per-message wire formats (varint / 16-bit-gap / int32 rows; varint / u16 / f32 / f64
+    values) at world 2 over gloo and over RCCL, exact against scipy, with the varint codes on and off."""
+    from dist_support import run_fiber_case
+    off = {"default": 0, "CBG_FIBER_VARINT=0": 1, "CBG_FIBER_GAPS=0": 2}[env]
+    if env != "default":
+        k, v = env.split("=")
+        monkeypatch.setenv(k, v)
+    cases = FIBER_CASES if env == "default" else [c[:-1] + (None,) for c in FIBER_CASES]
+    spawn_case(2, kind, cases, port + off, body=run_fiber_case)

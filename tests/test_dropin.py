@@ -40,16 +40,45 @@ def test_dropin_matches_reference_on_gpu():
     assert r.returncode == 0 and "DROPIN OK" in r.stdout, r.stdout + r.stderr
 
 
+MPIRUN = "/opt/conda/bin/mpirun"
+
+
+def mpi_cmd(world, args, transport):
+    """mpirun line for `world` ranks of dropin_test sharing cuda:0.  transport "rccl" (the drop-in's default: the
+    library's RCCL communicators) gives every rank its own NCCL_HOSTID through MPICH's MPMD syntax, so each rank is its
+    own RCCL "node" and RCCL's socket transport carries the bytes (RCCL refuses two ranks of one host on one device);
+    "mpi" selects the host-staged MPI transport (CBG_GRID_TRANSPORT=mpi)."""
+    cmd = [MPIRUN]
+    if transport == "mpi":
+        return cmd + ["-genv", "CBG_GRID_TRANSPORT", "mpi", "-np", str(world), BIN] + list(args)
+    cmd += ["-genv", "NCCL_SOCKET_IFNAME", "lo", "-genv", "NCCL_IB_DISABLE", "1"]
+    for r in range(world):
+        if r:
+            cmd.append(":")
+        cmd += ["-np", "1", "-env", "NCCL_HOSTID", f"cbg-dropin-{r}", BIN] + list(args)
+    return cmd
+
+
+def assert_grid(out, world, q, L, transport):
+    """Every rank reports the grid its distributed drivers ran over (cbg_grid_query): RCCL's own member counts of
+    the world / row / column / fiber communicators, or the MPI transport's group sizes."""
+    want = f"GRID rccl={1 if transport == 'rccl' else 0} world={world} row={q} col={q} fiber={L}"
+    assert out.count(want) == world, (want, out)
+
+
 @pytest.mark.gpu
-def test_dropin_distributed_drivers_4_ranks_on_gpu():
+@pytest.mark.parametrize("transport", ["rccl", "mpi"])
+def test_dropin_distributed_drivers_4_ranks_on_gpu(transport):
     """gpu::Mult_AnXBn_Synch / DoubleBuff / Overlap / PSpGEMM at 4 MPI ranks (2x2 CommGrid, ranks sharing
-    cuda:0, libcbgpu's grid over the SpParMat's MPI communicators) against the reference's own
-    Mult_AnXBn_Synch on the same operands, block by block (the reference's duplicates summed)."""
-    mpirun = "/opt/conda/bin/mpirun"
-    if not os.path.exists(BIN) or not os.path.exists(mpirun):
+    cuda:0; libcbgpu's grid over its own RCCL communicators, or over the SpParMat's MPI communicators) against the
+    reference's own Mult_AnXBn_Synch on the same operands, block by block (the reference's duplicates summed); and
+    gpu::MCLPruneRecoverySelect on the 2x2 grid (columns gathered along the processor column, pruned on the device)
+    against the reference's MCLPruneRecoverySelect (ParFriends.h:185-353) on the same SpParMat."""
+    if not os.path.exists(BIN) or not os.path.exists(MPIRUN):
         pytest.skip("dropin_test or MPICH's mpirun not available")
-    r = subprocess.run([mpirun, "-np", "4", BIN], capture_output=True, text=True, timeout=300)
+    r = subprocess.run(mpi_cmd(4, [], transport), capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and r.stdout.count("DROPIN OK") == 4, r.stdout + r.stderr
+    assert_grid(r.stdout, 4, 2, 1, transport)
 
 
 def _write_mtx(path, nrow, ncol, cp, ir, val):
@@ -79,8 +108,9 @@ def _fixture_mtx(tmp_path):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("transport", ["rccl", "mpi"])
 @pytest.mark.parametrize("q,L", [(1, 2), (2, 1), (1, 4), (2, 2)])
-def test_dropin_3dspgemm_and_summa3d_on_gpu(q, L, tmp_path):
+def test_dropin_3dspgemm_and_summa3d_on_gpu(q, L, transport, tmp_path):
     """gpu::multiply / gpu::SUMMALayer (3DSpGEMM/Multiplier.h:10-61, SUMMALayer.h:24-97) on a CCGrid of
     q x q x L MPI ranks sharing cuda:0, set up as test_mpipspgemm.cpp:101-153 does (ReadMat + SplitMat of
     bcsstk01), against the reference's multiply / SUMMALayer on the same split pieces and against MATLAB's
@@ -88,14 +118,14 @@ def test_dropin_3dspgemm_and_summa3d_on_gpu(q, L, tmp_path):
     with L layers (bcsstk01 within 1e-12 of sum|a*b|, Graph500 s10 bit-exact), every rank's piece, where the
     world is a square (the reference's SpParMat3D is built from a 2D SpParMat on a square CommGrid: 2x2x1 and
     1x1x4 here; 1x1x2 and 2x2x2 exercise the split-3D driver)."""
-    mpirun = "/opt/conda/bin/mpirun"
-    if not os.path.exists(BIN) or not os.path.exists(mpirun):
+    if not os.path.exists(BIN) or not os.path.exists(MPIRUN):
         pytest.skip("dropin_test or MPICH's mpirun not available")
     fa, fc, fg = _fixture_mtx(tmp_path)
     world = q * q * L
-    r = subprocess.run([mpirun, "-np", str(world), BIN, "--3d", str(q), str(L), fa, fc, fg], capture_output=True,
+    r = subprocess.run(mpi_cmd(world, ["--3d", str(q), str(L), fa, fc, fg], transport), capture_output=True,
                        text=True, timeout=300)
     assert r.returncode == 0 and r.stdout.count("DROPIN3D OK") == world, r.stdout + r.stderr
+    assert_grid(r.stdout, world, q, L, transport)
 
 
 @pytest.mark.gpu
@@ -105,8 +135,7 @@ def test_dropin_restriction_op_on_gpu(q, name, tmp_path):
     """gpu::RestrictionOp (3DSpGEMM/RestrictionOp.h:196-291) on a CCGrid layer of q x q MPI ranks: the layer's pieces
     go to the device on the layer's rank 0, and every rank's R and R^T blocks (SpParMat distribution of the layer
     grid) must hold the reference's one-rank R -- oracle/_ref/refrestrict's output in golden/restriction.npz."""
-    mpirun = "/opt/conda/bin/mpirun"
-    if not os.path.exists(BIN) or not os.path.exists(mpirun):
+    if not os.path.exists(BIN) or not os.path.exists(MPIRUN):
         pytest.skip("dropin_test or MPICH's mpirun not available")
     import numpy as np
     z = np.load(os.path.join(HERE, "golden", "restriction.npz"))
@@ -122,6 +151,6 @@ def test_dropin_restriction_op_on_gpu(q, name, tmp_path):
     fa, fg = str(tmp_path / "A.mtx"), str(tmp_path / "agg.txt")
     _write_mtx(fa, n, n, cp, ir, val)
     np.savetxt(fg, z[f"{name}_agg"].astype(np.int64), fmt="%d")
-    r = subprocess.run([mpirun, "-np", str(q * q), BIN, "--restrict", str(q), fa, fg], capture_output=True, text=True,
+    r = subprocess.run(mpi_cmd(q * q, ["--restrict", str(q), fa, fg], "rccl"), capture_output=True, text=True,
                        timeout=300)
     assert r.returncode == 0 and r.stdout.count("DROPINR OK") == q * q, r.stdout + r.stderr

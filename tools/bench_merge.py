@@ -15,14 +15,18 @@ import time
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.dirname(HERE))
-import combblas_amd as cb  # noqa: E402
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--scale", type=int, default=19)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--lib", default=None, help="another libcbgpu.so (a tools/var build)")
     a = ap.parse_args()
+    from combblas_amd import _abi
+    if a.lib:
+        _abi.LIB_PATH = os.path.abspath(a.lib)
+    import combblas_amd as cb
     ctx = cb.Context(0)
     PT = cb.PlusTimesSRing("f64")
     n = 1 << a.scale
@@ -46,7 +50,7 @@ def main():
     t = min(ts[1:])
     nparts = [p.getnnz() for p in parts]
     byts = sum(nparts) * 12 * 2 + nnzc * 12
-    print(json.dumps({"what": "cbg_merge of the two 1x1x2 layer partials", "scale": a.scale,
+    print(json.dumps({"what": "cbg_merge of the two 1x1x2 layer partials", "scale": a.scale, "lib": a.lib,
                       "nnz_partials": nparts, "nnz_C": nnzc, "merge_ms": t * 1e3,
                       "merge_bytes": byts, "merge_GBps": byts / t / 1e9, "reps_ms": [x * 1e3 for x in ts]}),
           flush=True)
