@@ -365,6 +365,9 @@ struct cbg_grid {
   int world = 1, rank = 0, L = 1, q = 1, layer = 0, row = 0, col = 0;
   bool rccl = false;
   ncclComm_t comm[4] = {nullptr, nullptr, nullptr, nullptr};
+  // a second fiber communicator for the fiber pipeline's per-chunk count exchanges: operations on one communicator
+  // run in issue order, so on the data communicator chunk c+1's counts would wait behind chunk c's transfer
+  ncclComm_t fiber_ctl = nullptr;
   cbg_transport cb{};
   hipStream_t cs = nullptr;          // communication stream
   hipEvent_t ev_comm[2] = {}, ev_used[2] = {}, ev_t[4] = {};
@@ -418,7 +421,8 @@ cbg_status t_bcast(cbg_grid* G, int g, int n, void* const* bufs, const int64_t* 
 
 // all-to-all-v of device buffers over group g: segment m of `send` (sbytes[m]) goes to member m;
 // segments land in member order in `recv`.  Synchronous on return.
-cbg_status t_alltoallv(cbg_grid* G, int g, const void* send, const int64_t* sbytes, void* recv, const int64_t* rbytes) {
+cbg_status t_alltoallv(cbg_grid* G, int g, const void* send, const int64_t* sbytes, void* recv, const int64_t* rbytes,
+                       ncclComm_t comm = nullptr) {
   const int P = G->gsize(g), me = G->grank(g);
   std::vector<int64_t> so(P + 1, 0), ro(P + 1, 0);
   for (int m = 0; m < P; ++m) { so[m + 1] = so[m] + sbytes[m]; ro[m + 1] = ro[m] + rbytes[m]; }
@@ -434,8 +438,8 @@ cbg_status t_alltoallv(cbg_grid* G, int g, const void* send, const int64_t* sbyt
     NCCLCHK(ncclGroupStart());
     for (int m = 0; m < P; ++m) {
       if (m == me) continue;
-      if (sbytes[m]) NCCLCHK(ncclSend((const char*)send + so[m], (size_t)sbytes[m], ncclInt8, m, G->comm[g], st));
-      if (rbytes[m]) NCCLCHK(ncclRecv((char*)recv + ro[m], (size_t)rbytes[m], ncclInt8, m, G->comm[g], st));
+      if (sbytes[m]) NCCLCHK(ncclSend((const char*)send + so[m], (size_t)sbytes[m], ncclInt8, m, comm ? comm : G->comm[g], st));
+      if (rbytes[m]) NCCLCHK(ncclRecv((char*)recv + ro[m], (size_t)rbytes[m], ncclInt8, m, comm ? comm : G->comm[g], st));
     }
     NCCLCHK(ncclGroupEnd());
     HIPCHK(hipStreamSynchronize(st));
@@ -1118,14 +1122,37 @@ cbg_status fiber_exchange(cbg_grid* G, const Piece& C, size_t vs, bool f64, std:
   return CBG_OK;
 }
 
+// One chunk of the fiber message, both directions: the partial this rank sends (a chunk of the other layer's
+// columns), its encoding, and the streams it receives for the same chunk of its own columns.
+struct FiberMsg {
+  Piece P;                                         // the sent partial
+  int64_t oc = 0, n = 0;                           // its columns and entries
+  int rfmt = 0, vfmt = 0;                          // rows: 0 int32, 1 16-bit gaps, 2 varint; values: 0 native,
+                                                   // 1 f32, 2 u16, 3 varint
+  int64_t E = 0, srow_b = 0, sesc_b = 0, sval_b = 0, svh_b = 0;
+  const void* srow_p = nullptr;
+  const void* sval_p = nullptr;
+  PoolBuf cpv, shdr, sval, saux, svr, svv, sescoff, svroff, svvoff, srow, sesc;
+  int64_t c0 = 0, mc = 0;                          // received: my columns [c0, c0 + mc)
+  int rrfmt = 0, rvfmt = 0;
+  int64_t rnnz = 0, rE = 0, rrow_b = 0, rval_b = 0, rvh_b = 0;
+  PoolBuf rrow, resc, rvbuf, rvhdr, rauxoff, rvoff;
+  explicit FiberMsg(const std::shared_ptr<Pool>& pl) {
+    for (PoolBuf* b : {&cpv, &shdr, &sval, &saux, &svr, &svv, &sescoff, &svroff, &svvoff, &srow, &sesc, &rrow, &resc,
+                       &rvbuf, &rvhdr, &rauxoff, &rvoff})
+      b->pool = pl;
+  }
+};
+
 // L = 2, plain product (reduce_all_impl's exchange-after-product, overlapped): the columns of the other layer's
-// part (block_range of the local columns, as fiber_exchange cuts them) are multiplied first; their counts, rows
-// and values leave for the other layer as one grouped ncclSend/ncclRecv on the communication stream while the own
-// part multiplies on the compute stream; then the received partial and the own one are merged.  The same two
-// pieces and the same two-way merge as the unpipelined path, so the product is identical.  With a caller transport
-// the exchange is synchronous (no overlap, same result).
+// part (block_range of the local columns, as fiber_exchange cuts them) are multiplied first, in C chunks of columns
+// (CBG_FIBER_CHUNKS, default 2): each chunk's counts, rows and values leave for the other layer as one grouped
+// ncclSend/ncclRecv on the communication stream as soon as it is made, so the link works while the next chunk and
+// then the own part multiply on the compute stream; the received chunks and the own part are then merged.  The
+// same two pieces and the same two-way merge as the unpipelined path, so the product is identical.  With a caller
+// transport the exchange is synchronous (no overlap, same result).
 //
-// Wire format, per direction, each part in the smallest lossless form of the whole message (counted in one pass,
+// Wire format, per chunk and direction, each part in the smallest lossless form of the chunk (counted in one pass,
 // k_code_count), announced in the count exchange (32 bytes per member: entries | formats, escapes, row bytes, value
 // bytes): column headers of 8 bytes (count | aux << 32); rows as varint gaps (aux = the column's row bytes), as
 // 16-bit gaps with escaped absolute rows (aux = the column's escapes) or as int32; values as varint integers (then 8
@@ -1140,30 +1167,37 @@ cbg_status fiber_pipeline(cbg_grid* G, const cbg_dcsc_view& va, const cbg_dcsc_v
   const int me = G->layer, other = 1 - me;
   const int64_t ncol = vb.ncol;
   const int64_t cb[3] = {0, ncol / 2, ncol};
-  PoolBuf cpo, cpm, shdr, sval, tiles, scal, saux, svr, svv, sescoff, svroff, svvoff, srow, sesc, svhdr;
-  PoolBuf rrow, resc, rvbuf, raux, rauxoff, rvhdr, rvoff;
-  for (PoolBuf* b : {&cpo, &cpm, &shdr, &sval, &tiles, &scal, &saux, &svr, &svv, &sescoff, &svroff, &svvoff, &srow, &sesc,
-                     &svhdr, &rrow, &resc, &rvbuf, &raux, &rauxoff, &rvhdr, &rvoff})
-    b->pool = ctx->pool;
-  std::shared_ptr<Owner> rx(new Owner(ctx->pool));
+  const int64_t myc = cb[me + 1] - cb[me], ocw = cb[other + 1] - cb[other];
+  static const int chunks_env = [] {
+    const char* x = std::getenv("CBG_FIBER_CHUNKS");
+    return x ? std::max(1, std::min(8, atoi(x))) : 2;
+  }();
+  // both members cut the columns they send (their other half = the receiver's own half) the same way
+  const int C = (int)std::max<int64_t>(1, std::min<int64_t>(chunks_env, std::min(myc, ocw)));
+  auto chunk = [&](int64_t w, int c, int64_t* a, int64_t* b) {
+    *a = (w / C) * c;
+    *b = c == C - 1 ? w : *a + w / C;
+  };
+  PoolBuf cpm, tiles, scal, raux;
+  for (PoolBuf* b : {&cpm, &tiles, &scal, &raux}) b->pool = ctx->pool;
+  std::vector<std::unique_ptr<FiberMsg>> msgs;
+  std::shared_ptr<Owner> rx(new Owner(ctx->pool));   // received headers (val), rows + values (ir)
   StreamFence fence(cst, G->cs);   // transfers into / out of the buffers above end before they return to the pool
-  // column-range views of B: rebased colptr, rows and values from cp[c0]
-  int64_t e[4] = {0, 0, 0, 0};
-  for (int m = 0; m < 2; ++m) {
-    HIPCHK(hipMemcpyAsync(&e[2 * m], (const int64_t*)vb.cp + cb[m], 8, hipMemcpyDeviceToHost, cst));
-    HIPCHK(hipMemcpyAsync(&e[2 * m + 1], (const int64_t*)vb.cp + cb[m + 1], 8, hipMemcpyDeviceToHost, cst));
-  }
-  HIPCHK(hipStreamSynchronize(cst));
-  auto col_view = [&](int m, PoolBuf& cpbuf, cbg_dcsc_view* v) -> cbg_status {
-    const int64_t c0 = cb[m], n = cb[m + 1] - cb[m], e0 = e[2 * m], e1 = e[2 * m + 1];
+  // columns [c0, c1) of B as a view: rebased colptr, rows and values from cp[c0]
+  auto col_view = [&](int64_t c0, int64_t c1, PoolBuf& cpbuf, cbg_dcsc_view* v) -> cbg_status {
+    int64_t e[2] = {0, 0};
+    HIPCHK(hipMemcpyAsync(&e[0], (const int64_t*)vb.cp + c0, 8, hipMemcpyDeviceToHost, cst));
+    HIPCHK(hipMemcpyAsync(&e[1], (const int64_t*)vb.cp + c1, 8, hipMemcpyDeviceToHost, cst));
+    HIPCHK(hipStreamSynchronize(cst));
+    const int64_t n = c1 - c0;
     HIPCHK(cpbuf.reserve(8 * (n + 1)));
     k_cp_rebase<<<(int)grid_for(n + 1, 256, kMaxGrid), 256, 0, cst>>>(n, (const int64_t*)vb.cp, c0, cpbuf.as<int64_t>());
     HIPCHK(hipGetLastError());
     *v = vb;
-    v->ncol = n; v->nzc = n; v->nnz = e1 - e0;
+    v->ncol = n; v->nzc = n; v->nnz = e[1] - e[0];
     v->cp = cpbuf.p;
-    v->ir = (const int32_t*)vb.ir + e0;
-    v->val = vb.val ? (const void*)((const char*)vb.val + vs * e0) : nullptr;
+    v->ir = (const int32_t*)vb.ir + e[0];
+    v->val = vb.val ? (const void*)((const char*)vb.val + vs * e[0]) : nullptr;
     return CBG_OK;
   };
   // exclusive scan of n int64 counts into out[0..n], the total into *total (device)
@@ -1184,209 +1218,241 @@ cbg_status fiber_pipeline(cbg_grid* G, const cbg_dcsc_view& va, const cbg_dcsc_v
   static const bool gaps_env = [] { const char* x = std::getenv("CBG_FIBER_GAPS"); return !(x && x[0] == '0'); }();
   static const bool narrow_env = [] { const char* x = std::getenv("CBG_FIBER_NARROW"); return !(x && x[0] == '0'); }();
   static const bool var_env = [] { const char* x = std::getenv("CBG_FIBER_VARINT"); return !(x && x[0] == '0'); }();
-  cbg_dcsc_view vo, vm;
-  CBGCHK(col_view(other, cpo, &vo));
-  CBGCHK(col_view(me, cpm, &vm));
-  // 1. the other layer's columns
-  double t0 = now_ms();
-  cbg_csc_result Ro;
-  int64_t mo = 0;
-  CBGCHK(cbg_spgemm_local(ctx, &va, &vo, sr, dt, CBG_SORTED_COLS, &Ro, &mo));
-  Piece Po = piece_of_result(Ro);
-  double t_local = now_ms() - t0;
-  // 2. the message's formats (one counting pass, one host sync), its encoding, the sizes (8 x 8 bytes each way)
-  t0 = now_ms();
-  const int64_t myc = cb[me + 1] - cb[me], oc = Po.ncol, n = Po.nnz;
-  const bool has_val = Po.val != nullptr;
-  const bool coded = gaps_env && oc > 0 && n > 0;
-  const bool vcheck = narrow_env && dt == CBG_F64 && has_val && vs == 8 && n > 0;
-  HIPCHK(G->small.reserve(256));
-  int64_t* dsn = G->small.as<int64_t>();   // [0..7] sent, [8..15] received, [16..18] value verdicts
-  HIPCHK(scal.reserve(64));
-  int64_t* dtot = scal.as<int64_t>();      // [0..2] sender totals (escapes, row bytes, value bytes), [3..5] receiver
-  int64_t tot[3] = {0, 0, 0};
-  unsigned long long bad[3] = {0, 0, 0};
-  if (coded || vcheck) {
-    for (PoolBuf* b : {&saux, &svr, &sescoff, &svroff}) HIPCHK(b->reserve(8 * (oc + 1)));
-    if (vcheck) { HIPCHK(svv.reserve(8 * (oc + 1))); HIPCHK(svvoff.reserve(8 * (oc + 1))); }
-    HIPCHK(hipMemsetAsync(dsn + 16, 0, 24, cst));
-    k_code_count<<<(int)grid_for(oc, 4, kMaxGrid * 2), 256, 0, cst>>>(
-        oc, Po.cp, Po.ir, vcheck ? (const double*)Po.val : nullptr, saux.as<int64_t>(), svr.as<int64_t>(),
-        vcheck ? svv.as<int64_t>() : nullptr, (unsigned long long*)(dsn + 16));
-    HIPCHK(hipGetLastError());
-    CBGCHK(scan(oc, saux.as<int64_t>(), sescoff.as<int64_t>(), dtot + 0));
-    CBGCHK(scan(oc, svr.as<int64_t>(), svroff.as<int64_t>(), dtot + 1));
-    if (vcheck) CBGCHK(scan(oc, svv.as<int64_t>(), svvoff.as<int64_t>(), dtot + 2));
-    HIPCHK(hipMemcpyAsync(tot, dtot, 24, hipMemcpyDeviceToHost, cst));
-    HIPCHK(hipMemcpyAsync(bad, dsn + 16, 24, hipMemcpyDeviceToHost, cst));
-    HIPCHK(hipStreamSynchronize(cst));
-  }
-  // rows: 0 int32, 1 16-bit gaps + escapes, 2 varint gaps
-  int rfmt = 0;
-  int64_t srow_b = 4 * n, sesc_b = 0;
-  if (coded && 2 * n + 4 * tot[0] < srow_b) { rfmt = 1; srow_b = 2 * n; sesc_b = 4 * tot[0]; }
-  if (coded && var_env && tot[1] < srow_b + sesc_b) { rfmt = 2; srow_b = tot[1]; sesc_b = 0; }
-  // values: 0 native, 1 f32, 2 u16, 3 varint (+ 8 bytes per column)
-  int vfmt = 0;
-  int64_t sval_b = has_val ? (int64_t)vs * n : 0;
-  if (vcheck && bad[0] == 0 && 4 * n < sval_b) { vfmt = 1; sval_b = 4 * n; }
-  if (vcheck && bad[1] == 0 && 2 * n < sval_b) { vfmt = 2; sval_b = 2 * n; }
-  if (vcheck && var_env && bad[2] == 0 && tot[2] + 8 * oc < sval_b) { vfmt = 3; sval_b = tot[2]; }
-  const void* srow_p = Po.ir;
-  if (rfmt == 1) {
-    HIPCHK(srow.reserve(srow_b + 16));
-    HIPCHK(sesc.reserve(sesc_b + 16));
-    k_gap_encode<<<(int)grid_for(oc, 4, kMaxGrid * 2), 256, 0, cst>>>(oc, Po.cp, Po.ir, sescoff.as<int64_t>(),
-                                                                      srow.as<unsigned short>(), sesc.as<int32_t>());
-    srow_p = srow.p;
-  } else if (rfmt == 2) {
-    HIPCHK(srow.reserve(srow_b + 16));
-    k_var_encode<0><<<(int)grid_for(oc, 4, kMaxGrid * 2), 256, 0, cst>>>(oc, Po.cp, Po.ir, nullptr, svroff.as<int64_t>(),
-                                                                         srow.as<uint8_t>());
-    srow_p = srow.p;
-  }
-  HIPCHK(shdr.reserve(8 * (oc + 1)));
-  if (oc)
-    k_pack_hdr<<<(int)grid_for(oc, 256, kMaxGrid), 256, 0, cst>>>(
-        oc, Po.cp, rfmt == 1 ? saux.as<int64_t>() : rfmt == 2 ? svr.as<int64_t>() : nullptr, shdr.as<int64_t>());
-  const void* sval_p = Po.val;
-  if (vfmt) {
-    HIPCHK(sval.reserve(sval_b + 16));
-    if (vfmt == 1)
-      k_f64_to_f32<<<(int)grid_for(n, 256, kMaxGrid), 256, 0, cst>>>(n, (const double*)Po.val, sval.as<float>());
-    else if (vfmt == 2)
-      k_f64_to_u16<<<(int)grid_for(n, 256, kMaxGrid), 256, 0, cst>>>(n, (const double*)Po.val, sval.as<unsigned short>());
-    else
-      k_var_encode<1><<<(int)grid_for(oc, 4, kMaxGrid * 2), 256, 0, cst>>>(oc, Po.cp, nullptr, (const double*)Po.val,
-                                                                           svvoff.as<int64_t>(), sval.as<uint8_t>());
-    sval_p = sval.p;
-  }
-  HIPCHK(hipGetLastError());
-  // the count exchange: [entries | rows format << 56 | values format << 58, escapes, row bytes, value bytes]
-  int64_t sflag[8] = {0, 0, 0, 0, 0, 0, 0, 0}, rflag[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  sflag[4 * other + 0] = n | ((int64_t)rfmt << 56) | ((int64_t)vfmt << 58);
-  sflag[4 * other + 1] = rfmt == 1 ? tot[0] : 0;
-  sflag[4 * other + 2] = srow_b;
-  sflag[4 * other + 3] = sval_b;
-  HIPCHK(hipMemcpyAsync(dsn, sflag, 64, hipMemcpyHostToDevice, cst));
-  const int64_t thirtytwo[2] = {32, 32};
-  CBGCHK(t_alltoallv(G, CBG_GROUP_FIBER, dsn, thirtytwo, dsn + 8, thirtytwo));
-  HIPCHK(hipMemcpyAsync(rflag, dsn + 8, 64, hipMemcpyDeviceToHost, cst));
-  HIPCHK(hipStreamSynchronize(cst));
-  const int64_t rf = rflag[4 * other];
-  const int rrfmt = (int)((rf >> 56) & 3), rvfmt = (int)((rf >> 58) & 3);
-  const int64_t rnnz = rf & ((1LL << 56) - 1), rE = rflag[4 * other + 1], rrow_b = rflag[4 * other + 2],
-                rval_b = rflag[4 * other + 3];
-  // 3. receive storage (rows, then values; the counts behind them) and the exchange
-  const int64_t ir_bytes = (4 * rnnz + 15) & ~15LL;
-  HIPCHK(rx->ir.reserve(ir_bytes + vs * rnnz + 16));
-  HIPCHK(rx->val.reserve(8 * (myc + 1)));
-  char* rbase = rx->ir.as<char>();
-  int64_t* rcnt = rx->val.as<int64_t>();
-  void* rrow_p = rbase;
-  if (rrfmt) { HIPCHK(rrow.reserve(rrow_b + 16)); rrow_p = rrow.p; }
-  HIPCHK(resc.reserve(4 * (rrfmt == 1 ? rE : 0) + 16));
-  HIPCHK(sesc.reserve(16));   // a transport may be handed the escape buffers with zero bytes
-  void* rval_p = has_val ? (void*)(rbase + ir_bytes) : nullptr;
-  if (has_val && rvfmt) { HIPCHK(rvbuf.reserve(rval_b + 16)); rval_p = rvbuf.p; }
-  if (vfmt == 3) HIPCHK(svhdr.reserve(8 * (oc + 1)));
-  if (vfmt == 3 && oc) HIPCHK(hipMemcpyAsync(svhdr.p, svv.p, 8 * oc, hipMemcpyDeviceToDevice, cst));
-  if (rvfmt == 3) HIPCHK(rvhdr.reserve(8 * (myc + 1)));
-  const int64_t svh_b = vfmt == 3 ? 8 * oc : 0, rvh_b = rvfmt == 3 ? 8 * myc : 0;
-  const double t_setup = now_ms() - t0;
-  if (st) st->fiber_bytes += 8 * oc + srow_b + sesc_b + (has_val ? sval_b + svh_b : 0);
-  const bool async = G->rccl;
-  if (async) {
-    HIPCHK(hipEventRecord(G->ev_t[0], cst));   // headers and encoded streams are ready
-    HIPCHK(hipStreamWaitEvent(G->cs, G->ev_t[0], 0));
-    HIPCHK(hipEventRecord(G->ev_t[1], G->cs));
-    ncclComm_t f = G->comm[CBG_GROUP_FIBER];
-    NCCLCHK(ncclGroupStart());
-    if (oc) NCCLCHK(ncclSend(shdr.p, (size_t)(8 * oc), ncclInt8, other, f, G->cs));
-    if (myc) NCCLCHK(ncclRecv(rcnt, (size_t)(8 * myc), ncclInt8, other, f, G->cs));
-    if (srow_b) NCCLCHK(ncclSend(srow_p, (size_t)srow_b, ncclInt8, other, f, G->cs));
-    if (rrow_b) NCCLCHK(ncclRecv(rrow_p, (size_t)rrow_b, ncclInt8, other, f, G->cs));
-    if (sesc_b) NCCLCHK(ncclSend(sesc.p, (size_t)sesc_b, ncclInt8, other, f, G->cs));
-    if (rrfmt == 1 && rE) NCCLCHK(ncclRecv(resc.p, (size_t)(4 * rE), ncclInt8, other, f, G->cs));
-    if (has_val && sval_b) NCCLCHK(ncclSend(sval_p, (size_t)sval_b, ncclInt8, other, f, G->cs));
-    if (has_val && rval_b) NCCLCHK(ncclRecv(rval_p, (size_t)rval_b, ncclInt8, other, f, G->cs));
-    if (has_val && svh_b) NCCLCHK(ncclSend(svhdr.p, (size_t)svh_b, ncclInt8, other, f, G->cs));
-    if (has_val && rvh_b) NCCLCHK(ncclRecv(rvhdr.p, (size_t)rvh_b, ncclInt8, other, f, G->cs));
-    NCCLCHK(ncclGroupEnd());
-    HIPCHK(hipEventRecord(G->ev_t[2], G->cs));
-  } else {   // caller transport: synchronous segments (member `other` only)
-    int64_t sb[2] = {0, 0}, rb[2] = {0, 0};
-    auto seg = [&](const void* sp, int64_t sn, void* rp, int64_t rn) -> cbg_status {
-      sb[other] = sn; rb[other] = rn;
-      if (sn || rn) CBGCHK(t_alltoallv(G, CBG_GROUP_FIBER, sp, sb, rp, rb));
-      return CBG_OK;
-    };
-    CBGCHK(seg(shdr.p, 8 * oc, rcnt, 8 * myc));
-    CBGCHK(seg(srow_p, srow_b, rrow_p, rrow_b));
-    CBGCHK(seg(sesc.p, sesc_b, resc.p, rrfmt == 1 ? 4 * rE : 0));
-    if (has_val) {
-      CBGCHK(seg(sval_p, sval_b, rval_p, rval_b));
-      CBGCHK(seg(svhdr.p ? svhdr.p : sesc.p, svh_b, rvhdr.p ? rvhdr.p : resc.p, rvh_b));
-    }
-  }
-  // 4. the own columns, while the exchange runs on the communication stream.  RCCL's kernel needs 37.6 KB of LDS
-  // per workgroup (ncclDevKernel_Generic on gfx950) and cannot share a CU with the persistent heavy grid (one
-  // 1024-thread workgroup holding 152.7 KB on every CU): CBG_FIBER_RESERVE_CU leaves that many CUs to the transfer
-  // while it is in flight (the heavy kernels take their work from a ticket, so a workgroup held back by RCCL's
-  // finds the work done instead of stretching the kernel)
+  // RCCL's kernel needs 37.6 KB of LDS per workgroup (ncclDevKernel_Generic on gfx950) and cannot share a CU with the
+  // persistent heavy grid (one 1024-thread workgroup holding 152.7 KB on every CU): while a transfer is in flight the
+  // products leave CBG_FIBER_RESERVE_CU CUs to it (the heavy kernels take their work from a ticket, so a workgroup held
+  // back by RCCL's finds the work done instead of stretching the kernel)
   static const int reserve_env = [] {
     const char* x = std::getenv("CBG_FIBER_RESERVE_CU");
     return x ? std::max(0, atoi(x)) : kFiberReserveCu;
   }();
-  t0 = now_ms();
+  const bool async = G->rccl;
+  bool in_flight = false;
+  HIPCHK(G->small.reserve(256));
+  int64_t* dsn = G->small.as<int64_t>();   // [0..7] sent, [8..15] received, [16..18] value verdicts
+  HIPCHK(scal.reserve(64));
+  int64_t* dtot = scal.as<int64_t>();      // [0..2] sender totals (escapes, row bytes, value bytes), [3..5] receiver
+  HIPCHK(rx->val.reserve(8 * (myc + 1)));
+  int64_t* rcnt = rx->val.as<int64_t>();   // every chunk's column headers, my columns in order
+  double t_local = 0, t_setup = 0;
+  int64_t mults = 0;
+  auto local = [&](const cbg_dcsc_view& vbx, cbg_csc_result* R, int64_t* m) -> cbg_status {
+    const double t0 = now_ms();
+    if (async && in_flight) ctx->reserve_cu = reserve_env;
+    const cbg_status s = cbg_spgemm_local(ctx, &va, &vbx, sr, dt, CBG_SORTED_COLS, R, m);
+    ctx->reserve_cu = 0;
+    t_local += now_ms() - t0;
+    return s;
+  };
+  // 1. the other layer's columns, chunk by chunk: product, encoding, count exchange, transfer posted
+  for (int c = 0; c < C; ++c) {
+    msgs.emplace_back(new FiberMsg(ctx->pool));
+    FiberMsg& m = *msgs.back();
+    int64_t a, b;
+    chunk(ocw, c, &a, &b);
+    cbg_dcsc_view vo;
+    CBGCHK(col_view(cb[other] + a, cb[other] + b, m.cpv, &vo));
+    cbg_csc_result Ro;
+    int64_t mo = 0;
+    CBGCHK(local(vo, &Ro, &mo));
+    mults += mo;
+    m.P = piece_of_result(Ro);
+    const double t0 = now_ms();
+    const Piece& Po = m.P;
+    m.oc = Po.ncol;
+    m.n = Po.nnz;
+    const int64_t oc = m.oc, n = m.n;
+    const bool has_val = Po.val != nullptr;
+    const bool coded = gaps_env && oc > 0 && n > 0;
+    const bool vcheck = narrow_env && dt == CBG_F64 && has_val && vs == 8 && n > 0;
+    int64_t tot[3] = {0, 0, 0};
+    unsigned long long bad[3] = {0, 0, 0};
+    if (coded || vcheck) {
+      for (PoolBuf* pb : {&m.saux, &m.svr, &m.sescoff, &m.svroff}) HIPCHK(pb->reserve(8 * (oc + 1)));
+      if (vcheck) { HIPCHK(m.svv.reserve(8 * (oc + 1))); HIPCHK(m.svvoff.reserve(8 * (oc + 1))); }
+      HIPCHK(hipMemsetAsync(dsn + 16, 0, 24, cst));
+      k_code_count<<<(int)grid_for(oc, 4, kMaxGrid * 2), 256, 0, cst>>>(
+          oc, Po.cp, Po.ir, vcheck ? (const double*)Po.val : nullptr, m.saux.as<int64_t>(), m.svr.as<int64_t>(),
+          vcheck ? m.svv.as<int64_t>() : nullptr, (unsigned long long*)(dsn + 16));
+      HIPCHK(hipGetLastError());
+      CBGCHK(scan(oc, m.saux.as<int64_t>(), m.sescoff.as<int64_t>(), dtot + 0));
+      CBGCHK(scan(oc, m.svr.as<int64_t>(), m.svroff.as<int64_t>(), dtot + 1));
+      if (vcheck) CBGCHK(scan(oc, m.svv.as<int64_t>(), m.svvoff.as<int64_t>(), dtot + 2));
+      HIPCHK(hipMemcpyAsync(tot, dtot, 24, hipMemcpyDeviceToHost, cst));
+      HIPCHK(hipMemcpyAsync(bad, dsn + 16, 24, hipMemcpyDeviceToHost, cst));
+      HIPCHK(hipStreamSynchronize(cst));
+    }
+    m.srow_b = 4 * n;
+    if (coded && 2 * n + 4 * tot[0] < m.srow_b) { m.rfmt = 1; m.srow_b = 2 * n; m.sesc_b = 4 * tot[0]; m.E = tot[0]; }
+    if (coded && var_env && tot[1] < m.srow_b + m.sesc_b) { m.rfmt = 2; m.srow_b = tot[1]; m.sesc_b = 0; m.E = 0; }
+    m.sval_b = has_val ? (int64_t)vs * n : 0;
+    if (vcheck && bad[0] == 0 && 4 * n < m.sval_b) { m.vfmt = 1; m.sval_b = 4 * n; }
+    if (vcheck && bad[1] == 0 && 2 * n < m.sval_b) { m.vfmt = 2; m.sval_b = 2 * n; }
+    if (vcheck && var_env && bad[2] == 0 && tot[2] + 8 * oc < m.sval_b) { m.vfmt = 3; m.sval_b = tot[2]; m.svh_b = 8 * oc; }
+    m.srow_p = Po.ir;
+    if (m.rfmt == 1) {
+      HIPCHK(m.srow.reserve(m.srow_b + 16));
+      HIPCHK(m.sesc.reserve(m.sesc_b + 16));
+      k_gap_encode<<<(int)grid_for(oc, 4, kMaxGrid * 2), 256, 0, cst>>>(oc, Po.cp, Po.ir, m.sescoff.as<int64_t>(),
+                                                                        m.srow.as<unsigned short>(), m.sesc.as<int32_t>());
+      m.srow_p = m.srow.p;
+    } else if (m.rfmt == 2) {
+      HIPCHK(m.srow.reserve(m.srow_b + 16));
+      k_var_encode<0><<<(int)grid_for(oc, 4, kMaxGrid * 2), 256, 0, cst>>>(oc, Po.cp, Po.ir, nullptr,
+                                                                           m.svroff.as<int64_t>(), m.srow.as<uint8_t>());
+      m.srow_p = m.srow.p;
+    }
+    HIPCHK(m.sesc.reserve(16));   // a transport may be handed the escape buffers with zero bytes
+    HIPCHK(m.shdr.reserve(8 * (oc + 1)));
+    if (oc)
+      k_pack_hdr<<<(int)grid_for(oc, 256, kMaxGrid), 256, 0, cst>>>(
+          oc, Po.cp, m.rfmt == 1 ? m.saux.as<int64_t>() : m.rfmt == 2 ? m.svr.as<int64_t>() : nullptr,
+          m.shdr.as<int64_t>());
+    m.sval_p = Po.val;
+    if (m.vfmt) {
+      HIPCHK(m.sval.reserve(m.sval_b + 16));
+      if (m.vfmt == 1)
+        k_f64_to_f32<<<(int)grid_for(n, 256, kMaxGrid), 256, 0, cst>>>(n, (const double*)Po.val, m.sval.as<float>());
+      else if (m.vfmt == 2)
+        k_f64_to_u16<<<(int)grid_for(n, 256, kMaxGrid), 256, 0, cst>>>(n, (const double*)Po.val,
+                                                                      m.sval.as<unsigned short>());
+      else
+        k_var_encode<1><<<(int)grid_for(oc, 4, kMaxGrid * 2), 256, 0, cst>>>(oc, Po.cp, nullptr, (const double*)Po.val,
+                                                                             m.svvoff.as<int64_t>(), m.sval.as<uint8_t>());
+      m.sval_p = m.sval.p;
+    }
+    HIPCHK(hipGetLastError());
+    // the count exchange: [entries | rows format << 56 | values format << 58, escapes, row bytes, value bytes]
+    int64_t sflag[8] = {0, 0, 0, 0, 0, 0, 0, 0}, rflag[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    sflag[4 * other + 0] = n | ((int64_t)m.rfmt << 56) | ((int64_t)m.vfmt << 58);
+    sflag[4 * other + 1] = m.E;
+    sflag[4 * other + 2] = m.srow_b;
+    sflag[4 * other + 3] = m.sval_b;
+    HIPCHK(hipMemcpyAsync(dsn, sflag, 64, hipMemcpyHostToDevice, cst));
+    const int64_t thirtytwo[2] = {32, 32};
+    CBGCHK(t_alltoallv(G, CBG_GROUP_FIBER, dsn, thirtytwo, dsn + 8, thirtytwo, G->fiber_ctl));
+    HIPCHK(hipMemcpyAsync(rflag, dsn + 8, 64, hipMemcpyDeviceToHost, cst));
+    HIPCHK(hipStreamSynchronize(cst));
+    const int64_t rf = rflag[4 * other];
+    m.rrfmt = (int)((rf >> 56) & 3);
+    m.rvfmt = (int)((rf >> 58) & 3);
+    m.rnnz = rf & ((1LL << 56) - 1);
+    m.rE = rflag[4 * other + 1];
+    m.rrow_b = rflag[4 * other + 2];
+    m.rval_b = has_val ? rflag[4 * other + 3] : 0;
+    chunk(myc, c, &m.c0, &a);
+    m.mc = a - m.c0;
+    m.rvh_b = m.rvfmt == 3 ? 8 * m.mc : 0;
+    // receive staging of this chunk (decoded into the piece once every chunk has arrived)
+    HIPCHK(m.rrow.reserve(m.rrow_b + 16));
+    HIPCHK(m.resc.reserve(4 * (m.rrfmt == 1 ? m.rE : 0) + 16));
+    HIPCHK(m.rvbuf.reserve(m.rval_b + 16));
+    HIPCHK(m.rvhdr.reserve(m.rvh_b + 16));
+    if (st) st->fiber_bytes += 8 * oc + m.srow_b + m.sesc_b + (has_val ? m.sval_b + m.svh_b : 0);
+    const void* svh_p = m.vfmt == 3 ? (const void*)m.svv.p : (const void*)m.sesc.p;
+    t_setup += now_ms() - t0;
+    if (async) {
+      HIPCHK(hipEventRecord(G->ev_t[0], cst));   // this chunk's headers and encoded streams are ready
+      HIPCHK(hipStreamWaitEvent(G->cs, G->ev_t[0], 0));
+      if (c == 0) HIPCHK(hipEventRecord(G->ev_t[1], G->cs));
+      ncclComm_t f = G->comm[CBG_GROUP_FIBER];
+      NCCLCHK(ncclGroupStart());
+      if (oc) NCCLCHK(ncclSend(m.shdr.p, (size_t)(8 * oc), ncclInt8, other, f, G->cs));
+      if (m.mc) NCCLCHK(ncclRecv(rcnt + m.c0, (size_t)(8 * m.mc), ncclInt8, other, f, G->cs));
+      if (m.srow_b) NCCLCHK(ncclSend(m.srow_p, (size_t)m.srow_b, ncclInt8, other, f, G->cs));
+      if (m.rrow_b) NCCLCHK(ncclRecv(m.rrow.p, (size_t)m.rrow_b, ncclInt8, other, f, G->cs));
+      if (m.sesc_b) NCCLCHK(ncclSend(m.sesc.p, (size_t)m.sesc_b, ncclInt8, other, f, G->cs));
+      if (m.rrfmt == 1 && m.rE) NCCLCHK(ncclRecv(m.resc.p, (size_t)(4 * m.rE), ncclInt8, other, f, G->cs));
+      if (has_val && m.sval_b) NCCLCHK(ncclSend(m.sval_p, (size_t)m.sval_b, ncclInt8, other, f, G->cs));
+      if (m.rval_b) NCCLCHK(ncclRecv(m.rvbuf.p, (size_t)m.rval_b, ncclInt8, other, f, G->cs));
+      if (has_val && m.svh_b) NCCLCHK(ncclSend(svh_p, (size_t)m.svh_b, ncclInt8, other, f, G->cs));
+      if (m.rvh_b) NCCLCHK(ncclRecv(m.rvhdr.p, (size_t)m.rvh_b, ncclInt8, other, f, G->cs));
+      NCCLCHK(ncclGroupEnd());
+      in_flight = true;
+    } else {   // caller transport: synchronous segments (member `other` only)
+      int64_t sb[2] = {0, 0}, rb[2] = {0, 0};
+      auto seg = [&](const void* sp, int64_t sn, void* rp, int64_t rn) -> cbg_status {
+        sb[other] = sn; rb[other] = rn;
+        if (sn || rn) CBGCHK(t_alltoallv(G, CBG_GROUP_FIBER, sp, sb, rp, rb));
+        return CBG_OK;
+      };
+      CBGCHK(seg(m.shdr.p, 8 * oc, rcnt + m.c0, 8 * m.mc));
+      CBGCHK(seg(m.srow_p, m.srow_b, m.rrow.p, m.rrow_b));
+      CBGCHK(seg(m.sesc.p, m.sesc_b, m.resc.p, m.rrfmt == 1 ? 4 * m.rE : 0));
+      if (has_val) {
+        CBGCHK(seg(m.sval_p, m.sval_b, m.rvbuf.p, m.rval_b));
+        CBGCHK(seg(svh_p, m.svh_b, m.rvhdr.p, m.rvh_b));
+      }
+    }
+  }
+  if (async) HIPCHK(hipEventRecord(G->ev_t[2], G->cs));
+  // 2. the own columns, while the chunks travel on the communication stream
+  cbg_dcsc_view vm;
+  CBGCHK(col_view(cb[me], cb[me + 1], cpm, &vm));
   cbg_csc_result Rm;
   int64_t mm = 0;
-  if (async) ctx->reserve_cu = reserve_env;
-  const cbg_status sm = cbg_spgemm_local(ctx, &va, &vm, sr, dt, CBG_SORTED_COLS, &Rm, &mm);
-  ctx->reserve_cu = 0;
-  CBGCHK(sm);
+  CBGCHK(local(vm, &Rm, &mm));
+  mults += mm;
   Piece Pm = piece_of_result(Rm);
-  t_local += now_ms() - t0;
-  // 5. join, decode the received piece (colptr from its counts), the merge in layer order
-  t0 = now_ms();
+  // 3. join; decode every chunk into the received piece (colptr from all chunks' counts); the merge in layer order
+  double t0 = now_ms();
   float xfer_ms = 0.f;
   if (async) {
     HIPCHK(hipStreamWaitEvent(cst, G->ev_t[2], 0));
     HIPCHK(hipEventSynchronize(G->ev_t[2]));
     (void)hipEventElapsedTime(&xfer_ms, G->ev_t[1], G->ev_t[2]);
   }
+  const bool has_val = msgs.empty() || msgs[0]->P.val != nullptr;
+  int64_t rnnz = 0;
+  for (auto& mp : msgs) rnnz += mp->rnnz;
+  const int64_t ir_bytes = (4 * rnnz + 15) & ~15LL;
+  HIPCHK(rx->ir.reserve(ir_bytes + vs * rnnz + 16));
+  char* rbase = rx->ir.as<char>();
+  int32_t* rir = (int32_t*)rbase;
+  char* rv = rbase + ir_bytes;
+  HIPCHK(raux.reserve(8 * (myc + 1)));
+  if (myc > 0) k_split_hdr<<<(int)grid_for(myc, 256, kMaxGrid), 256, 0, cst>>>(myc, rcnt, raux.as<int64_t>());
   std::shared_ptr<Owner> co(new Owner(ctx->pool));
   HIPCHK(co->cp.reserve(8 * (myc + 1)));
-  if (rrfmt && myc > 0) {   // row aux (escapes or row bytes) out of the headers, its offsets
-    HIPCHK(raux.reserve(8 * (myc + 1)));
-    HIPCHK(rauxoff.reserve(8 * (myc + 1)));
-    k_split_hdr<<<(int)grid_for(myc, 256, kMaxGrid), 256, 0, cst>>>(myc, rcnt, raux.as<int64_t>());
-    CBGCHK(scan(myc, raux.as<int64_t>(), rauxoff.as<int64_t>(), dtot + 3));
-  }
   CBGCHK(scan(myc, rcnt, co->cp.as<int64_t>(), dtot + 4));
-  int32_t* rir = (int32_t*)rbase;
-  if (rrfmt == 1 && myc > 0)
-    k_gap_decode<<<(int)grid_for(myc, 4, kMaxGrid * 2), 256, 0, cst>>>(myc, co->cp.as<int64_t>(), rauxoff.as<int64_t>(),
-                                                                       rrow.as<unsigned short>(), resc.as<int32_t>(), rir);
-  else if (rrfmt == 2 && myc > 0)
-    k_var_decode<0><<<(int)grid_for(myc, 4, kMaxGrid * 2), 256, 0, cst>>>(myc, co->cp.as<int64_t>(),
-                                                                          rauxoff.as<int64_t>(), rrow.as<uint8_t>(), rir,
-                                                                          nullptr);
-  double* rv = (double*)(rbase + ir_bytes);
-  if (has_val && rnnz) {
-    if (rvfmt == 1)
-      k_f32_to_f64<<<(int)grid_for(rnnz, 256, kMaxGrid), 256, 0, cst>>>(rnnz, rvbuf.as<float>(), rv);
-    else if (rvfmt == 2)
-      k_u16_to_f64<<<(int)grid_for(rnnz, 256, kMaxGrid), 256, 0, cst>>>(rnnz, rvbuf.as<unsigned short>(), rv);
-    else if (rvfmt == 3) {
-      HIPCHK(rvoff.reserve(8 * (myc + 1)));
-      CBGCHK(scan(myc, rvhdr.as<int64_t>(), rvoff.as<int64_t>(), dtot + 5));
-      k_var_decode<1><<<(int)grid_for(myc, 4, kMaxGrid * 2), 256, 0, cst>>>(myc, co->cp.as<int64_t>(),
-                                                                            rvoff.as<int64_t>(), rvbuf.as<uint8_t>(),
-                                                                            nullptr, rv);
+  int64_t eoff = 0;
+  for (auto& mp : msgs) {
+    FiberMsg& m = *mp;
+    const int64_t* ccp = co->cp.as<int64_t>() + m.c0;   // absolute entry offsets of the chunk's columns
+    if (m.rrfmt) {
+      HIPCHK(m.rauxoff.reserve(8 * (m.mc + 1)));
+      CBGCHK(scan(m.mc, raux.as<int64_t>() + m.c0, m.rauxoff.as<int64_t>(), dtot + 3));
     }
+    if (m.rnnz) {
+      if (m.rrfmt == 0)
+        HIPCHK(hipMemcpyAsync(rir + eoff, m.rrow.p, 4 * m.rnnz, hipMemcpyDeviceToDevice, cst));
+      else if (m.rrfmt == 1)
+        k_gap_decode<<<(int)grid_for(m.mc, 4, kMaxGrid * 2), 256, 0, cst>>>(m.mc, ccp, m.rauxoff.as<int64_t>(),
+                                                                             m.rrow.as<unsigned short>(),
+                                                                             m.resc.as<int32_t>(), rir);
+      else
+        k_var_decode<0><<<(int)grid_for(m.mc, 4, kMaxGrid * 2), 256, 0, cst>>>(m.mc, ccp, m.rauxoff.as<int64_t>(),
+                                                                                m.rrow.as<uint8_t>(), rir, nullptr);
+      if (has_val) {
+        double* dv = (double*)rv;
+        if (m.rvfmt == 0)
+          HIPCHK(hipMemcpyAsync(rv + vs * eoff, m.rvbuf.p, vs * m.rnnz, hipMemcpyDeviceToDevice, cst));
+        else if (m.rvfmt == 1)
+          k_f32_to_f64<<<(int)grid_for(m.rnnz, 256, kMaxGrid), 256, 0, cst>>>(m.rnnz, m.rvbuf.as<float>(), dv + eoff);
+        else if (m.rvfmt == 2)
+          k_u16_to_f64<<<(int)grid_for(m.rnnz, 256, kMaxGrid), 256, 0, cst>>>(m.rnnz, m.rvbuf.as<unsigned short>(),
+                                                                               dv + eoff);
+        else {
+          HIPCHK(m.rvoff.reserve(8 * (m.mc + 1)));
+          CBGCHK(scan(m.mc, m.rvhdr.as<int64_t>(), m.rvoff.as<int64_t>(), dtot + 5));
+          k_var_decode<1><<<(int)grid_for(m.mc, 4, kMaxGrid * 2), 256, 0, cst>>>(m.mc, ccp, m.rvoff.as<int64_t>(),
+                                                                                  m.rvbuf.as<uint8_t>(), nullptr, dv);
+        }
+      }
+    }
+    HIPCHK(hipGetLastError());
+    eoff += m.rnnz;
   }
-  HIPCHK(hipGetLastError());
   Piece Pr;
   Pr.nrow = Pm.nrow; Pr.ncol = myc; Pr.nnz = rnnz;
   Pr.cp = co->cp.as<int64_t>();
@@ -1394,7 +1460,8 @@ cbg_status fiber_pipeline(cbg_grid* G, const cbg_dcsc_view& va, const cbg_dcsc_v
   Pr.val = has_val ? (const void*)rv : nullptr;
   Pr.own = co;
   Pr.keep = rx;
-  Po = Piece();   // the sent partial is no longer needed (the exchange has completed)
+  HIPCHK(hipStreamSynchronize(cst));
+  msgs.clear();   // the sent partials and the staging go back to the pool (the exchange has completed)
   const double t_wait = now_ms() - t0;
   t0 = now_ms();
   std::vector<cbg_csc_result> two;
@@ -1405,9 +1472,9 @@ cbg_status fiber_pipeline(cbg_grid* G, const cbg_dcsc_view& va, const cbg_dcsc_v
   *out = piece_of_result(M);
   out->reduced = true;
   if (st) {
-    st->multiplies += mo + mm;
+    st->multiplies += mults;
     st->local_ms += t_local;
-    st->fiber_ms += t_setup + t_wait;   // exposed exchange time (the transfer itself overlaps the own product)
+    st->fiber_ms += t_setup + t_wait;   // exposed exchange time (the transfers themselves overlap the products)
     st->merge_ms += now_ms() - t0;
     st->fiber_xfer_ms += xfer_ms;
   }
@@ -1546,6 +1613,8 @@ cbg_status cbg_grid_create_rccl(cbg_ctx* ctx, const char id[128], int32_t world,
   if (r == ncclSuccess) r = ncclCommSplit(G->comm[CBG_GROUP_WORLD], G->layer * rows + G->row, G->col, &G->comm[CBG_GROUP_ROW], nullptr);
   if (r == ncclSuccess) r = ncclCommSplit(G->comm[CBG_GROUP_WORLD], G->layer * cols + G->col, G->row, &G->comm[CBG_GROUP_COL], nullptr);
   if (r == ncclSuccess) r = ncclCommSplit(G->comm[CBG_GROUP_WORLD], G->row * cols + G->col, G->layer, &G->comm[CBG_GROUP_FIBER], nullptr);
+  if (r == ncclSuccess && layers > 1)
+    r = ncclCommSplit(G->comm[CBG_GROUP_WORLD], G->row * cols + G->col, G->layer, &G->fiber_ctl, nullptr);
   if (r != ncclSuccess) {
     fprintf(stderr, "cbgpu: RCCL grid setup failed: %s\n", ncclGetErrorString(r));
     cbg_grid_destroy(G);
@@ -1571,6 +1640,7 @@ cbg_status cbg_grid_destroy(cbg_grid* G) {
   if (G->cs) (void)hipStreamSynchronize(G->cs);
   for (int g = 0; g < 4; ++g)
     if (G->comm[g]) (void)ncclCommDestroy(G->comm[g]);
+  if (G->fiber_ctl) (void)ncclCommDestroy(G->fiber_ctl);
   for (int i = 0; i < 2; ++i) {
     if (G->ev_comm[i]) (void)hipEventDestroy(G->ev_comm[i]);
     if (G->ev_used[i]) (void)hipEventDestroy(G->ev_used[i]);

@@ -303,6 +303,7 @@ hipError_t launch_sym_part(hipStream_t st, const PartItem* items, const int* cou
                            const int64_t* Acp, const int32_t* Air, const int64_t* Bcp, const int32_t* Bir,
                            const int2* span, const Split& spl, int64_t* nnz, const HeavyOut& ho) {
   const size_t lds = sym_part_lds<NT>();
+  if (sizeof(SymIx) == 4 && annz >= INT32_MAX) return hipErrorInvalidValue;   // 32-bit staging build
   // 16-byte row loads (RowLd4) unless CBG_SYM_VEC4=0 or A has fewer than 4 entries
   static const bool vec_env = [] { const char* e = std::getenv("CBG_SYM_VEC4"); return !(e && e[0] == '0'); }();
   const bool vec = vec_env && kGroupSym == 4 && annz >= 4;

@@ -475,10 +475,10 @@ template <class F> struct HasVec4 { static constexpr bool value = false; };
 template <> struct HasVec4<RowLd4> { static constexpr bool value = true; };
 template <class F> struct HasVec2 { static constexpr bool value = false; };   // (row, value) pairs: NumLd2
 
-template <typename V>
+template <typename V, typename IX = int64_t>
 struct SegBuf {         // LDS, NT entries each (+ scan scratch for block mode)
-  int64_t* qb;          // segment start (A index)
-  int64_t* off;         // exclusive prefix of segment group counts
+  IX* qb;               // segment start (A index)
+  IX* off;              // exclusive prefix of segment group counts (< A.nnz: a chunk's segments are distinct A columns)
   V* bv;                // B value of the segment's nonzero
   int64_t* scratch;     // block mode: NT/64 + 1 entries
   int32_t* len;         // segment length (multiplies)
@@ -518,8 +518,8 @@ __device__ __forceinline__ void wait_vmem_all() { __builtin_amdgcn_s_waitcnt(0x0
 
 // last s in [0, P) with off[s] <= m (off non-decreasing, off[0] = 0 <= m): the non-empty segment
 // holding flat multiply m.  P is a power of two covering the staged segments (P <= NT).
-template <int NT>
-__device__ __forceinline__ int seg_search(const int64_t* off, int64_t m, int P) {
+template <int NT, typename IX>
+__device__ __forceinline__ int seg_search(const IX* off, int64_t m, int P) {
   int s = 0;
   for (int step = P >> 1; step > 0; step >>= 1)
     if (off[s + step] <= m) s += step;
@@ -528,8 +528,8 @@ __device__ __forceinline__ int seg_search(const int64_t* off, int64_t m, int P) 
 
 // U searches in lockstep: each step issues the U independent LDS reads together (one latency per
 // step instead of U); steps >= P are skipped by a uniform branch.
-template <int NT, int U>
-__device__ __forceinline__ void seg_search_n(const int64_t* off, const int64_t (&m)[U], int P, int (&s)[U]) {
+template <int NT, int U, typename IX>
+__device__ __forceinline__ void seg_search_n(const IX* off, const int64_t (&m)[U], int P, int (&s)[U]) {
 #pragma unroll
   for (int u = 0; u < U; ++u) s[u] = 0;
 #pragma unroll
@@ -548,8 +548,8 @@ __device__ __forceinline__ void seg_search_n(const int64_t* off, const int64_t (
 // GROUPS: a segment of len multiplies is cut into ceil(len/G) groups of G consecutive A
 // entries, and the groups (not the multiplies) are what lanes are dealt.  The LDS arrays are valid
 // on return (synchronised).
-template <int NT, bool WAVE, int G, typename V>
-__device__ __forceinline__ int64_t stage_segments(const SegBuf<V>& sb, int64_t a0, int64_t a1, V bv) {
+template <int NT, bool WAVE, int G, typename V, typename IX>
+__device__ __forceinline__ int64_t stage_segments(const SegBuf<V, IX>& sb, int64_t a0, int64_t a1, V bv) {
   const int tid = WAVE ? lane_id() : (int)threadIdx.x;
   const int64_t len = a1 - a0;
   const int64_t ng = (len + G - 1) / G;
@@ -561,8 +561,8 @@ __device__ __forceinline__ int64_t stage_segments(const SegBuf<V>& sb, int64_t a
   } else {
     ex = block_excl_scan64<NT>(ng, sb.scratch, &F);
   }
-  sb.qb[tid] = a0;
-  sb.off[tid] = ex;
+  sb.qb[tid] = (IX)a0;
+  sb.off[tid] = (IX)ex;
   sb.len[tid] = (int32_t)len;
   sb.bv[tid] = bv;
   if constexpr (WAVE) wave_sync(); else __syncthreads();
@@ -573,8 +573,8 @@ __device__ __forceinline__ int64_t stage_segments(const SegBuf<V>& sb, int64_t a
 // group's segment by a binary search over the LDS prefix offsets (one search per G multiplies),
 // then issues the group's G gathers back to back (U*G independent gathers per lane).
 // `base` is the B position of staged segment 0.  The caller synchronises before re-staging.
-template <int NT, int U, int G, typename V, class LdF, class InsF>
-__device__ __forceinline__ void expand_staged(const SegBuf<V>& sb, int tid, int64_t F, int64_t base, int nseg,
+template <int NT, int U, int G, typename V, class LdF, class InsF, typename IX>
+__device__ __forceinline__ void expand_staged(const SegBuf<V, IX>& sb, int tid, int64_t F, int64_t base, int nseg,
                                               LdF ld, InsF ins) {
   using Item = decltype(ld(int64_t(0)));
   int P = 1;
@@ -624,8 +624,8 @@ __device__ __forceinline__ void expand_staged(const SegBuf<V>& sb, int tid, int6
 // expand_staged for an accumulator whose slot lookup only READS LDS (the rank directory): all U*G
 // slots are looked up first (slotf, branch-free on the clamped items; < 0 = drop), so their LDS reads
 // issue together, then the U*G accumulations run.
-template <int NT, int U, int G, typename V, class LdF, class SlotF, class AccF>
-__device__ __forceinline__ void expand_staged_slots(const SegBuf<V>& sb, int tid, int64_t F, int64_t base, int nseg,
+template <int NT, int U, int G, typename V, class LdF, class SlotF, class AccF, typename IX>
+__device__ __forceinline__ void expand_staged_slots(const SegBuf<V, IX>& sb, int tid, int64_t F, int64_t base, int nseg,
                                                     LdF ld, SlotF slotf, AccF acc) {
   using Item = decltype(ld(int64_t(0)));
   int P = 1;
@@ -683,8 +683,9 @@ __device__ __forceinline__ void expand_staged_slots(const SegBuf<V>& sb, int tid
 // see all marks; false aborts); sweep 2 gathers the values (ldv) and acc(row, value, bv, q, b)s --
 // the rank mode's two sweeps with each A entry's row and value gathered once.  Only the rows and a
 // packed (segment, count) word per group stay live across mid(); q is recomputed from LDS.
-template <int NT, int U, int G, int RI, typename V, class LdR, class LdV, class MarkF, class MidF, class AccF>
-__device__ __forceinline__ bool expand_staged_twice(const SegBuf<V>& sb, int tid, int64_t F, int64_t base, int nseg,
+template <int NT, int U, int G, int RI, typename V, class LdR, class LdV, class MarkF, class MidF, class AccF,
+          typename IX>
+__device__ __forceinline__ bool expand_staged_twice(const SegBuf<V, IX>& sb, int tid, int64_t F, int64_t base, int nseg,
                                                     LdR ldr, LdV ldv, MarkF mark, MidF mid, AccF acc) {
   int P = 1;
   while (P < nseg) P <<= 1;
@@ -737,8 +738,8 @@ __device__ __forceinline__ bool expand_staged_twice(const SegBuf<V>& sb, int tid
   return true;
 }
 
-template <int NT, bool WAVE, int U, int G, typename V, class SegF, class LdF, class InsF>
-__device__ __forceinline__ void for_each_multiply(int64_t bs, int64_t be, SegBuf<V> sb, SegF seg, LdF ld, InsF ins) {
+template <int NT, bool WAVE, int U, int G, typename V, class SegF, class LdF, class InsF, typename IX>
+__device__ __forceinline__ void for_each_multiply(int64_t bs, int64_t be, SegBuf<V, IX> sb, SegF seg, LdF ld, InsF ins) {
   const int tid = WAVE ? lane_id() : (int)threadIdx.x;
   for (int64_t base = bs; base < be; base += NT) {
     const int64_t b = base + tid;
@@ -1085,14 +1086,27 @@ __global__ void k_part_items(const int32_t* __restrict__ list, int64_t count, in
   }
 }
 
+// CBG_SYM_W8=1: 32-bit segment staging (A.nnz < 2^31) so four 512-thread workgroups fit a CU's LDS, and at most 64
+// VGPRs: 8 waves per SIMD instead of 6
+#ifndef CBG_SYM_W8
+#define CBG_SYM_W8 0
+#endif
+#if CBG_SYM_W8
+typedef int32_t SymIx;
+#define CBG_SYM_WAVES __attribute__((amdgpu_waves_per_eu(8, 8)))
+#else
+typedef int64_t SymIx;
+#define CBG_SYM_WAVES
+#endif
+
 template <int NT>
 constexpr size_t sym_part_lds() {
-  return (size_t)(1 << (kPartLog - 5)) * 4 + (size_t)NT * 21 + (size_t)(NT / kWave + 1) * 8 +
+  return (size_t)(1 << (kPartLog - 5)) * 4 + (size_t)NT * (2 * sizeof(SymIx) + 5) + (size_t)(NT / kWave + 1) * 8 +
          (size_t)((1 << (kPartLog - kSubLogMin)) + 8) * 4 + 64;
 }
 
 template <int NT, bool VEC>
-__global__ void __launch_bounds__(NT) k_sym_part(const PartItem* __restrict__ items, const int* __restrict__ count_dev,
+__global__ void __launch_bounds__(NT) CBG_SYM_WAVES k_sym_part(const PartItem* __restrict__ items, const int* __restrict__ count_dev,
                                                  int64_t annz, const int64_t* __restrict__ Acp, const int32_t* __restrict__ Air,
                                                  const int64_t* __restrict__ Bcp, const int32_t* __restrict__ Bir,
                                                  const int2* __restrict__ span, Split spl, int64_t* __restrict__ nnz,
@@ -1101,15 +1115,15 @@ __global__ void __launch_bounds__(NT) k_sym_part(const PartItem* __restrict__ it
   constexpr int WPT = T / NT;              // words per thread in the subwindow count (<= SUBW / 32)
   static_assert(WPT * 32 <= (1 << kSubLogMin), "a thread's words must lie in one subwindow");
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  int64_t* qb = (int64_t*)smem;                    // NT
-  int64_t* off = qb + NT;                          // NT
-  int64_t* scr = off + NT;                         // NT/64 + 1
+  SymIx* qb = (SymIx*)smem;                        // NT
+  SymIx* off = qb + NT;                            // NT
+  int64_t* scr = (int64_t*)(off + NT);             // NT/64 + 1
   uint32_t* tab = (uint32_t*)(scr + NT / kWave + 1);// T
   int32_t* scnt = (int32_t*)(tab + T);             // part subwindows (<= 2^(kPartLog-kSubLogMin))
   int* misc = scnt + (1 << (kPartLog - kSubLogMin));   // [0] total
   int32_t* lens = misc + 8;                        // NT
   uint8_t* bvs = (uint8_t*)(lens + NT);            // NT
-  const SegBuf<uint8_t> sb{qb, off, bvs, scr, lens};
+  const SegBuf<uint8_t, SymIx> sb{qb, off, bvs, scr, lens};
   const int count = *count_dev;
   STAMP_DECL
   STAMP(31);

@@ -85,20 +85,20 @@ inline void check(cbg_status s, const char* where) {
 }
 
 // One context per process/host thread.  context(d) selects device d; without a choice, an MPI process takes its
-// node-local rank's device (rank within MPI_COMM_TYPE_SHARED, modulo the visible devices: one GPU per rank on an
-// 8-GPU node), any other process device 0.
+// node-local rank's device modulo the visible devices (one GPU per rank on an 8-GPU node), any other process
+// device 0.  The context may be created by one rank alone (e.g. RestrictionOp's layer rank 0), so the local rank
+// comes from the launcher's environment (MPICH MPI_LOCALRANKID, Open MPI OMPI_COMM_WORLD_LOCAL_RANK, Slurm
+// SLURM_LOCALID), else from the world rank -- never from a collective.
 inline int node_local_device() {
-  int init = 0, fin = 0;
+  int32_t n = 0;
+  if (cbg_device_count(&n) != CBG_OK || n <= 0) return 0;
+  for (const char* v : {"MPI_LOCALRANKID", "OMPI_COMM_WORLD_LOCAL_RANK", "SLURM_LOCALID"})
+    if (const char* x = std::getenv(v)) return std::atoi(x) % n;
+  int init = 0, fin = 0, r = 0;
   MPI_Initialized(&init);
   MPI_Finalized(&fin);
-  int32_t n = 0;
-  if (!init || fin || cbg_device_count(&n) != CBG_OK || n <= 0) return 0;
-  MPI_Comm node;
-  MPI_Comm_split_type(MPI_COMM_WORLD, MPI_COMM_TYPE_SHARED, 0, MPI_INFO_NULL, &node);
-  int lr = 0;
-  MPI_Comm_rank(node, &lr);
-  MPI_Comm_free(&node);
-  return lr % n;
+  if (init && !fin) MPI_Comm_rank(MPI_COMM_WORLD, &r);
+  return r % n;
 }
 
 inline cbg_ctx* context(int device = -1) {

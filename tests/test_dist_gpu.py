@@ -18,10 +18,13 @@ def test_summa_layouts_gloo_gpu(world, port):
 MCL_CASES = [(600, 3, 1, (1e-3, 8, 12, 0.9)), (513, 4, 3, (1e-3, 8, 12, 0.9)), (400, 5, 2, (0.05, 5, 9, 0.99))]
 
 
+@pytest.mark.parametrize("kind", ["gpu", "gpu-rccl-net"])
 @pytest.mark.parametrize("world,port", [(2, 29624), (4, 29625), (8, 29626)])
-def test_mcl_expansion_gloo_gpu(world, port):
+def test_mcl_expansion_gloo_gpu(world, port, kind):
+    """Distributed HipMCL expansion (MemEfficientSpGEMM + MCLPruneRecoverySelect) over the host-staged gloo
+    transport and over libcbgpu's RCCL grid (every rank its own RCCL node)."""
     from dist_support import run_mcl_case
-    spawn_case(world, "gpu", MCL_CASES, port, body=run_mcl_case)
+    spawn_case(world, kind, MCL_CASES, port + (100 if kind != "gpu" else 0), body=run_mcl_case)
 
 
 INDEX_CASES = [(300, 250, 0.03, 31), (9, 13, 0.3, 23), (3, 4, 0.5, 25)]
@@ -90,13 +93,15 @@ def test_rmat_pieces_built_per_rank_gloo_gpu(world, port):
     spawn_case(world, "gpu", [("g500_s10", 10), ("g500_s12", 12), ("single-gpu", 16)], port, body=run_rmat_case)
 
 
+@pytest.mark.parametrize("kind", ["gpu", "gpu-rccl-net"])
 @pytest.mark.parametrize("world,port", [(2, 29651), (4, 29652), (8, 29653)])
-def test_memeff3d_phases_match_reference_gloo_gpu(world, port):
+def test_memeff3d_phases_match_reference_gloo_gpu(world, port, kind):
     """MemEfficientSpGEMM3D phasing (ParFriends.h:3214-3705; B pieces per layer chunk, fiber exchange per
     phase, prune per phase): phases 1, 2, 3 reproduce the reference's MemEfficientSpGEMM output
-    (golden/mcl.npz) on every rank's piece, with the same branch counts."""
+    (golden/mcl.npz) on every rank's piece, with the same branch counts -- over gloo and over RCCL."""
     from dist_support import run_mcl_fixture_case
-    spawn_case(world, "gpu", [1, 2, 3, ("mem", 0.0025)], port, body=run_mcl_fixture_case)
+    spawn_case(world, kind, [1, 2, 3, ("mem", 0.0025)], port + (100 if kind != "gpu" else 0),
+               body=run_mcl_fixture_case)
 
 
 @pytest.mark.parametrize("world,port", [(4, 29661), (8, 29662)])

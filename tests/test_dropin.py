@@ -36,7 +36,7 @@ def test_dropin_builds_and_reports_missing_device():
 def test_dropin_matches_reference_on_gpu():
     if not os.path.exists(BIN):
         pytest.skip("dropin_test not built (needs the reference headers in the build container)")
-    r = subprocess.run([BIN], capture_output=True, text=True, timeout=300)
+    r = subprocess.run([BIN], capture_output=True, text=True, timeout=150)
     assert r.returncode == 0 and "DROPIN OK" in r.stdout, r.stdout + r.stderr
 
 
@@ -76,7 +76,7 @@ def test_dropin_distributed_drivers_4_ranks_on_gpu(transport):
     against the reference's MCLPruneRecoverySelect (ParFriends.h:185-353) on the same SpParMat."""
     if not os.path.exists(BIN) or not os.path.exists(MPIRUN):
         pytest.skip("dropin_test or MPICH's mpirun not available")
-    r = subprocess.run(mpi_cmd(4, [], transport), capture_output=True, text=True, timeout=300)
+    r = subprocess.run(mpi_cmd(4, [], transport), capture_output=True, text=True, timeout=150)
     assert r.returncode == 0 and r.stdout.count("DROPIN OK") == 4, r.stdout + r.stderr
     assert_grid(r.stdout, 4, 2, 1, transport)
 
@@ -123,7 +123,7 @@ def test_dropin_3dspgemm_and_summa3d_on_gpu(q, L, transport, tmp_path):
     fa, fc, fg = _fixture_mtx(tmp_path)
     world = q * q * L
     r = subprocess.run(mpi_cmd(world, ["--3d", str(q), str(L), fa, fc, fg], transport), capture_output=True,
-                       text=True, timeout=300)
+                       text=True, timeout=150)
     assert r.returncode == 0 and r.stdout.count("DROPIN3D OK") == world, r.stdout + r.stderr
     assert_grid(r.stdout, world, q, L, transport)
 
@@ -152,5 +152,5 @@ def test_dropin_restriction_op_on_gpu(q, name, tmp_path):
     _write_mtx(fa, n, n, cp, ir, val)
     np.savetxt(fg, z[f"{name}_agg"].astype(np.int64), fmt="%d")
     r = subprocess.run(mpi_cmd(q * q, ["--restrict", str(q), fa, fg], "rccl"), capture_output=True, text=True,
-                       timeout=300)
+                       timeout=150)
     assert r.returncode == 0 and r.stdout.count("DROPINR OK") == q * q, r.stdout + r.stderr

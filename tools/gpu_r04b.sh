@@ -23,3 +23,7 @@ timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/mfetc
 echo "mfetch rc=$?"
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/mwrite -o run -- python3 tools/bench_merge.py --scale 20 --reps 1 > $OUT/mwrite.log 2>&1
 echo "mwrite rc=$?"
+timeout -k 10 300 python3 -u bench.py --no-cpu --steps 10 --warmup 2 > $OUT/s20_main.log 2>&1 && tail -1 $OUT/s20_main.log | cut -c1-900
+timeout -k 10 300 python3 -u tools/var_bench.py sym_w8 -- --no-cpu --steps 10 --warmup 2 > $OUT/s20_symw8.log 2>&1; tail -2 $OUT/s20_symw8.log | cut -c1-900
+timeout -k 10 300 python3 -u bench.py --no-cpu --steps 5 --warmup 2 --scale 21 > $OUT/s21_main.log 2>&1 && tail -1 $OUT/s21_main.log | cut -c1-900
+timeout -k 10 300 python3 -u tools/var_bench.py sym_w8 -- --no-cpu --steps 5 --warmup 2 --scale 21 > $OUT/s21_symw8.log 2>&1; tail -2 $OUT/s21_symw8.log | cut -c1-900
