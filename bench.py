@@ -18,8 +18,13 @@ all ranks' multiplies / that time.
 
 Rank 0 prints ONE JSON line.  N = 1 adds `roofline` for the dominant phase (the heavy-column units:
 k_num_heavy_known, plus k_num_heavy for the few units it does not take, bracketed by HIP events on the
-library stream; algorithmic bytes per SURVEY §8d)
-and `cpu_baseline` (the oracle CPU restatement on a bounded sample of the same product).
+library stream; algorithmic bytes per SURVEY §8d; `roofline.step` = the whole product) and `cpu_baseline`:
+the reference's own LocalSpGEMMHash (oracle/_ref/refbench, built from /root/reference's sources) timed on a
+bounded sample of the same product, its output checksum compared with the GPU product's (the oracle
+restatement, also timed as `cpu_baseline_port`, checks the sample bit for bit).
+
+    python bench.py --rank-share all --gpus-virtual 8 --scale 22
+runs each rank's share of the N-GPU layout on this one GPU (local ms, fiber bytes, peak HBM; no transport).
 """
 import argparse
 import ctypes
@@ -77,6 +82,22 @@ def load_traffic(scale, edgefactor):
     if best is None:
         return None, None
     return best[1]["bytes_per_launch"], os.path.relpath(best[0], HERE)
+
+
+def load_step_traffic(scale, edgefactor):
+    """HBM bytes of one whole product (every kernel) from the newest profiles/*_pmc_product.json for this
+    workload (tools/pmc_heavy.py product), or (None, None)."""
+    best = None
+    for f in sorted(glob.glob(os.path.join(HERE, "profiles", "*_pmc_product.json")), key=round_tag):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if d.get("scale") == scale and d.get("edgefactor") == edgefactor:
+            best = (f, d)
+    if best is None:
+        return None, None
+    return best[1]["bytes_per_product"], os.path.relpath(best[0], HERE)
 
 
 def col_flops(cp, ir):
@@ -262,6 +283,7 @@ def bench_local(args):
     heavy_ms = float(np.mean([p["heavy_ms"] for p in profs]))
     achieved = hb / (heavy_ms / 1e3) / 1e9
     traffic, tsrc = load_traffic(args.scale, args.edgefactor)
+    step_traffic, ssrc = load_step_traffic(args.scale, args.edgefactor)
     cfg = workload(args.scale, args.edgefactor, "single GPU, local hash SpGEMM (BASELINE configs[1])")
     cfg.update({"nnz_A": nnzb, "multiplies": int(mult_step), "nnz_C": int(nnzc_step)})
     out = {
@@ -277,7 +299,11 @@ def bench_local(args):
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "traffic_source": tsrc, "algorithmic_bytes_per_launch": hb, "avg_launch_ms": heavy_ms,
                      "heavy_columns": int(heavy.sum()), "heavy_multiplies": int(flop_col[heavy].sum()),
-                     "heavy_nnz_C": int(nnz_c_col[heavy].sum())},
+                     "heavy_nnz_C": int(nnz_c_col[heavy].sum()),
+                     # the whole product (every kernel): SURVEY 8(d) algorithmic bytes vs PMC FETCH+WRITE
+                     "step": {"algorithmic_bytes": balg_bytes(mult_step, nnzc_step, nnzb, n),
+                              "achieved_GBps": balg_bytes(mult_step, nnzc_step, nnzb, n) / (elapsed / args.steps) / 1e9,
+                              "traffic": step_traffic, "traffic_source": ssrc}},
     }
     out["input"] = input_record(args, cp, ir, val, build_s)
     if not args.no_cpu:

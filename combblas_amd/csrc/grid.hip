@@ -306,9 +306,10 @@ __global__ void k_gap_encode(int64_t ncol, const int64_t* __restrict__ cp, const
   }
 }
 
+// gap[i - gbase]: the gap stream of entries [gbase, ...) (one chunk of a message), cp absolute
 __global__ void k_gap_decode(int64_t ncol, const int64_t* __restrict__ cp, const int64_t* __restrict__ eoff,
                              const unsigned short* __restrict__ gap, const int32_t* __restrict__ esc,
-                             int32_t* __restrict__ ir) {
+                             int32_t* __restrict__ ir, int64_t gbase) {
   const int l = lane_id();
   for (int64_t c = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / kWave; c < ncol;
        c += ((int64_t)gridDim.x * blockDim.x) / kWave) {
@@ -317,7 +318,7 @@ __global__ void k_gap_decode(int64_t ncol, const int64_t* __restrict__ cp, const
     int32_t carry = 0;   // the row before the chunk (0 before the column's first entry)
     for (int64_t i0 = s; i0 < e; i0 += kWave) {
       const int64_t i = i0 + l;
-      const unsigned g = i < e ? gap[i] : 0u;
+      const unsigned g = i < e ? gap[i - gbase] : 0u;
       const bool x = i < e && g == kGapEsc;
       const uint64_t m = __ballot(x);
       const int32_t a = x ? esc[eo + __popcll(m & ((1ull << l) - 1))] : 0;
@@ -1180,6 +1181,9 @@ cbg_status fiber_pipeline(cbg_grid* G, const cbg_dcsc_view& va, const cbg_dcsc_v
   };
   PoolBuf cpm, tiles, scal, raux;
   for (PoolBuf* b : {&cpm, &tiles, &scal, &raux}) b->pool = ctx->pool;
+  // scan tiles for the largest scan, reserved once: growing a pool buffer hands the old one back to the pool while
+  // kernels queued on the stream may still use it
+  HIPCHK(tiles.reserve(8 * ((std::max(myc, ocw) + kScanTile - 1) / kScanTile + 1)));
   std::vector<std::unique_ptr<FiberMsg>> msgs;
   std::shared_ptr<Owner> rx(new Owner(ctx->pool));   // received headers (val), rows + values (ir)
   StreamFence fence(cst, G->cs);   // transfers into / out of the buffers above end before they return to the pool
@@ -1203,7 +1207,7 @@ cbg_status fiber_pipeline(cbg_grid* G, const cbg_dcsc_view& va, const cbg_dcsc_v
   // exclusive scan of n int64 counts into out[0..n], the total into *total (device)
   auto scan = [&](int64_t n, const int64_t* in, int64_t* outp, int64_t* total) -> cbg_status {
     const int64_t nt = (n + kScanTile - 1) / kScanTile;
-    HIPCHK(tiles.reserve(8 * (nt + 1)));
+    if (8 * (nt + 1) > (int64_t)tiles.n) return CBG_EINVAL;   // sized for the largest scan above
     if (n > 0) {
       k_scan_tiles<<<(int)nt, 256, 0, cst>>>(n, in, tiles.as<int64_t>());
       k_scan_sums<<<1, 1024, 0, cst>>>(nt, tiles.as<int64_t>(), total);
@@ -1406,7 +1410,11 @@ cbg_status fiber_pipeline(cbg_grid* G, const cbg_dcsc_view& va, const cbg_dcsc_v
   int64_t rnnz = 0;
   for (auto& mp : msgs) rnnz += mp->rnnz;
   const int64_t ir_bytes = (4 * rnnz + 15) & ~15LL;
-  HIPCHK(rx->ir.reserve(ir_bytes + vs * rnnz + 16));
+  if (rx->ir.reserve(ir_bytes + vs * rnnz + 16) != hipSuccess) {   // next to the two products' pieces: give the
+    (void)hipGetLastError();                                        // idle product workspace back and retry once
+    release_workspace(ctx);
+    HIPCHK(rx->ir.reserve(ir_bytes + vs * rnnz + 16));
+  }
   char* rbase = rx->ir.as<char>();
   int32_t* rir = (int32_t*)rbase;
   char* rv = rbase + ir_bytes;
@@ -1429,7 +1437,7 @@ cbg_status fiber_pipeline(cbg_grid* G, const cbg_dcsc_view& va, const cbg_dcsc_v
       else if (m.rrfmt == 1)
         k_gap_decode<<<(int)grid_for(m.mc, 4, kMaxGrid * 2), 256, 0, cst>>>(m.mc, ccp, m.rauxoff.as<int64_t>(),
                                                                              m.rrow.as<unsigned short>(),
-                                                                             m.resc.as<int32_t>(), rir);
+                                                                             m.resc.as<int32_t>(), rir, eoff);
       else
         k_var_decode<0><<<(int)grid_for(m.mc, 4, kMaxGrid * 2), 256, 0, cst>>>(m.mc, ccp, m.rauxoff.as<int64_t>(),
                                                                                 m.rrow.as<uint8_t>(), rir, nullptr);

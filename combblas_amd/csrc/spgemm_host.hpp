@@ -56,6 +56,11 @@ struct DevBuf {
     return e;
   }
   template <typename T> T* as() const { return (T*)p; }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
 };
 
 inline size_t dt_size(cbg_dtype t) {
@@ -155,6 +160,23 @@ struct cbg_ctx {
   int reserve_cu = 0;                  // CUs the persistent grids leave free (a concurrent RCCL transfer)
   int row_handoff = -1;                // -1: read CBG_ROW_HANDOFF once (default on)
 };
+
+// Give the grow-only product workspace (the symbolic row handoff alone is ~11 GB at s20) and the pool's cached
+// blocks back to the device: called when an output that must fit next to large live pieces (the fiber merge at
+// N = 2, s21) would not.  Synchronises the context's stream first.
+inline void release_workspace(cbg_ctx* c) {
+  (void)hipStreamSynchronize(c->stream);
+  for (DevBuf* b : {&c->flop, &c->span, &c->cnt, &c->list, &c->hist, &c->cursor, &c->scan_tiles, &c->cur, &c->nxt,
+                    &c->ovf_list, &c->split_idx, &c->long_cols, &c->split_tab, &c->heavy_cols, &c->sub, &c->units,
+                    &c->ucnt, &c->uspan, &c->ulist, &c->fb_units, &c->fb_list, &c->uovf_list, &c->nunits, &c->segsz,
+                    &c->segoff, &c->useg, &c->icnt, &c->itemoff, &c->items, &c->parts, &c->wide_win, &c->hrows,
+                    &c->hmode, &c->hpoff, &c->urows, &c->oitems, &c->aos})
+    b->release();
+  for (DevBuf& b : c->stageA) b.release();
+  for (DevBuf& b : c->stageB) b.release();
+  for (DevBuf& b : c->gal) b.release();
+  c->pool->trim();
+}
 
 // pinned read-back slots (byte offsets into ctx->pin); a D2H copy into pageable memory goes through a staging
 // buffer and costs tens of microseconds per host sync on small products
@@ -839,10 +861,12 @@ __device__ __forceinline__ V merge_pair(V a, V b) {
 #define CBG_MERGE_PL 4   // merged positions per lane per window (window = 64 * CBG_MERGE_PL)
 #endif
 #ifndef CBG_MERGE_LDS
-#define CBG_MERGE_LDS 1   // fill pass: values staged in LDS, merged output staged in LDS, coalesced loads/stores
+#define CBG_MERGE_LDS 0   // 1: fill pass with values and merged output staged in LDS for coalesced loads/stores
+                          // (measured slower: s22 rank share 85.7 vs 67.8 ms, 24 KB of LDS per block)
 #endif
 constexpr int kMergePL = CBG_MERGE_PL;
 constexpr int kMergeW = kWave * kMergePL;
+static_assert(kMergeW < 1024, "the merge window's counts are packed in 10-bit fields");
 
 template <int SRI, typename V, bool FILL>
 __global__ void __launch_bounds__(256) k_merge2(int64_t ncol, const int64_t* __restrict__ acp,
@@ -921,12 +945,14 @@ __global__ void __launch_bounds__(256) k_merge2(int64_t ncol, const int64_t* __r
         na += in && src[e] >= 0;
         if (!FILL && in && pair[e]) ++nd;
       }
-      const int incl = wave_incl_scan(c);
-      const int tot = __shfl(incl, kWave - 1, kWave);
       int nin = 0;
 #pragma unroll
       for (int e = 0; e < PL; ++e) nin += d0 + e < K && row[e] != INT32_MAX;
-      const int ta = (int)wave_sum64(na), tin = (int)wave_sum64(nin);
+      // one wave scan for the three window counts (each <= W < 1024): heads | part-0 taken << 10 | in window << 20
+      const int pk = wave_incl_scan(c | (na << 10) | (nin << 20));
+      const int incl = pk & 1023;
+      const int ptot = __shfl(pk, kWave - 1, kWave);
+      const int tot = ptot & 1023, ta = (ptot >> 10) & 1023, tin = ptot >> 20;
       if (FILL && !SV) {
         int64_t pos = o + incl - c;
 #pragma unroll
@@ -1022,8 +1048,12 @@ cbg_status merge2_sr(cbg_ctx* ctx, const cbg_csc_result* parts, cbg_csc_result* 
   if (h[2]) return CBG_EINVAL;   // a partial is not row-sorted: the caller takes the hash merge
   if (add_is_error && h[0]) return CBG_EADD;   // BoolCopy add() would have been called (it throws)
   const int64_t nnz = (int64_t)h[1];
-  HIPCHK(own->ir.reserve(4 * (nnz + 1)));
-  HIPCHK(own->val.reserve(sizeof(V) * (nnz + 1)));
+  if (own->ir.reserve(4 * (nnz + 1)) != hipSuccess || own->val.reserve(sizeof(V) * (nnz + 1)) != hipSuccess) {
+    (void)hipGetLastError();
+    release_workspace(ctx);   // the product workspace is idle between calls: give it back and retry once
+    HIPCHK(own->ir.reserve(4 * (nnz + 1)));
+    HIPCHK(own->val.reserve(sizeof(V) * (nnz + 1)));
+  }
   k_merge2<SRI, V, true><<<g, 256, 0, st>>>(ncol, parts[0].colptr, parts[0].row, av, parts[1].colptr, parts[1].row, bv,
                                             nullptr, own->cp.as<int64_t>(), own->ir.as<int32_t>(), own->val.as<V>(),
                                             nullptr, nullptr);

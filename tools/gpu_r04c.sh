@@ -17,6 +17,8 @@ timeout -k 10 300 python3 -u bench.py --no-cpu --steps 10 --warmup 2 > $OUT/s20_
 timeout -k 10 300 python3 -u tools/var_bench.py sym_w8 -- --no-cpu --steps 10 --warmup 2 > $OUT/s20_symw8.log 2>&1 || exit 5
 timeout -k 10 300 python3 -u bench.py --no-cpu --steps 5 --warmup 2 --scale 21 > $OUT/s21_main.log 2>&1 || exit 5
 timeout -k 10 300 python3 -u tools/var_bench.py sym_w8 -- --no-cpu --steps 5 --warmup 2 --scale 21 > $OUT/s21_symw8.log 2>&1 || exit 5
+timeout -k 10 300 python3 -u tools/var_bench.py part19 -- --no-cpu --steps 5 --warmup 2 --scale 21 > $OUT/s21_part19.log 2>&1 || exit 5
+timeout -k 10 300 python3 -u tools/var_bench.py part19 -- --no-cpu --steps 10 --warmup 2 > $OUT/s20_part19.log 2>&1 || exit 5
 for v in "chunks2:CBG_FIBER_CHUNKS=2" "chunks1:CBG_FIBER_CHUNKS=1" "nopipe:CBG_FIBER_PIPE=0"; do
   name=${v%%:*}; envv=${v#*:}
   env $envv TAG=r04c/reh_${name}_s18 PORT=29750 bash tools/gpu_dist_rehearsal.sh 2 18 >> $OUT/rehearsal.txt 2>&1 || exit 6
