@@ -579,7 +579,7 @@ def _vlen(x):
     return 1 + (x >= 1 << 7).long() + (x >= 1 << 14).long() + (x >= 1 << 21).long() + (x >= 1 << 28).long()
 
 
-def fiber_wire_bytes(P):
+def fiber_wire_bytes(P, chunk=1 << 28):
     """Bytes the fiber pipeline (grid.hip fiber_pipeline) puts on the link for partial P, choosing per message as
     k_code_count's totals do: per-column headers (8 B), rows as varint gaps, 16-bit gaps + 4 B per escaped row (gap >
     65534) or int32, values as varint integers (+8 B per column), u16, f32 or f64 -- the smallest lossless form."""
@@ -587,6 +587,23 @@ def fiber_wire_bytes(P):
     n, nc = P.nnz, P.ncol
     if n == 0:
         return {"nnz": 0, "bytes": 8 * nc}
+    if n > chunk and nc > 1:   # column chunks of ~`chunk` entries: bounded temporaries
+        cp_h = P.cp.cpu().numpy()
+        import numpy as np
+        cuts = [0]
+        while cuts[-1] < nc:
+            c = int(np.searchsorted(cp_h, cp_h[cuts[-1]] + chunk, side="right")) - 1
+            cuts.append(min(nc, max(c, cuts[-1] + 1)))
+        parts = [fiber_wire_bytes(_col_slice_block(P, a, b), chunk) for a, b in zip(cuts[:-1], cuts[1:])]
+        rows = {k: sum(p["row_bytes"].get(k, 0) for p in parts if p["nnz"]) for k in ("int32", "gap16", "varint")}
+        vals = {"f64": 8 * n}
+        for k in ("f32", "u16", "varint"):
+            if all(k in p["value_bytes"] for p in parts if p["nnz"]):
+                vals[k] = sum(p["value_bytes"][k] for p in parts if p["nnz"])
+        rf, vf = min(rows, key=rows.get), min(vals, key=vals.get)
+        return {"nnz": n, "escapes": sum(p.get("escapes", 0) for p in parts), "rows": rf, "values": vf,
+                "row_bytes": rows, "value_bytes": vals, "bytes": 8 * nc + rows[rf] + vals[vf],
+                "bytes_per_entry": round((8 * nc + rows[rf] + vals[vf]) / n, 3)}
     cnt = torch.diff(P.cp)
     starts = P.cp[:-1][cnt > 0]
     ir = P.ir.to(torch.int64)
@@ -657,14 +674,18 @@ def bench_rank_share(args):
         build_s = time.perf_counter() - t0
         rec = {"rank": r, "layout": f"{L}x{q}x{q}", "l_i_j": [l, i, j], "scale": args.scale,
                "nnz_A_panel": AP.nnz, "nnz_B_panel": BP.nnz, "panel_build_s": round(build_s, 3)}
-        Pr = None
-        if L == 2:   # the partner's message (its product of this rank's column half), made first
-            PA, PB = panels(other, i, j)
-            Pr = be.multiply(PA, _col_slice_block(PB, *halves[me]), SR)
-            del PA, PB
-            rec["recv_nnz"] = Pr.nnz
         torch.cuda.empty_cache()
         sample()
+
+        def partner_piece():
+            """The partner's message: its product of this rank's column half (made after the own half, as it
+            arrives in the pipeline, so it is not held during this rank's products)."""
+            PA, PB = panels(other, i, j)
+            P = be.multiply(PA, _col_slice_block(PB, *halves[me]), SR)
+            del PA, PB
+            return P
+
+        phase_keys = ("flops_ms", "bin_ms", "symbolic_ms", "scan_ms", "numeric_ms", "heavy_ms", "total_ms")
         for rep in range(2):   # the second repetition is recorded (code objects loaded, pool warm)
             floor[0] = torch.cuda.mem_get_info()[0]
             st = {}
@@ -682,13 +703,17 @@ def bench_rank_share(args):
                 sample()
                 t3 = time.perf_counter()
                 p_mine = ctx.last_profile()
+                Pr = partner_piece()
+                rec["recv_nnz"] = Pr.nnz
+                torch.cuda.synchronize()
+                t4 = time.perf_counter()
                 M = be.merge([Pm, Pr] if me == 0 else [Pr, Pm], SR)
                 sample()
-                t4 = time.perf_counter()
+                t5 = time.perf_counter()
                 local_ms = 1e3 * ((t1 - t0) + (t3 - t2))
-                merge_ms = 1e3 * (t4 - t3)
+                merge_ms = 1e3 * (t5 - t4)
                 nnz_out = M.nnz
-                del Pm, M
+                del Pm, M, Pr
                 profs = [p_other, p_mine]
             else:
                 Pm = be.multiply(AP, BP, SR, st)
@@ -699,6 +724,8 @@ def bench_rank_share(args):
                 profs = [ctx.last_profile()]
                 del Pm
             torch.cuda.synchronize()
+            torch.cuda.empty_cache()
+        rec["phases_ms"] = [{k: round(float(pp[k]), 3) for k in phase_keys} for pp in profs]
         rec.update({"multiplies": st.get("multiplies", 0), "local_ms": round(local_ms, 3),
                     "merge_ms": round(merge_ms, 3), "nnz_C_piece": nnz_out,
                     "heavy_ms": round(sum(p["heavy_ms"] for p in profs), 3),
@@ -706,7 +733,7 @@ def bench_rank_share(args):
                     "fiber": wire,
                     "peak_hbm_GB": round((total - floor[0]) / 1e9, 2), "hbm_total_GB": round(total / 1e9, 1)})
         print(json.dumps(rec), flush=True)
-        del AP, BP, Pr
+        del AP, BP
         torch.cuda.empty_cache()
     dist.destroy_process_group()
     if os.path.exists(store.name):

@@ -46,6 +46,10 @@ def test_fiber_wire_bytes_counts_gaps_escapes_and_values():
     assert w["value_bytes"]["u16"] == 2 * 67 and w["value_bytes"]["varint"] == 66 + 2 + 8 * 3
     assert (w["rows"], w["values"]) == ("varint", "varint")
     assert w["bytes"] == 8 * 3 + 69 + 92
+    # the same accounting in column chunks (bounded temporaries for billions of entries) adds up the same
+    c = bench.fiber_wire_bytes(b, chunk=4)
+    assert (c["row_bytes"], c["rows"], c["values"], c["escapes"]) == (w["row_bytes"], "varint", "varint", 1)
+    assert c["value_bytes"]["varint"] == 66 + 2 + 8 * 3 and c["bytes"] == w["bytes"]
 
 
 def test_round_tag_orders_evidence_files():

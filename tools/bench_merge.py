@@ -49,10 +49,22 @@ def main():
         C.free()
     t = min(ts[1:])
     nparts = [p.getnnz() for p in parts]
+    # merged positions per column (the two-way merge walks one column per wave): how skewed is the work?
+    import numpy as np
+    import ctypes
+
+    def colptr(p):   # the colptr alone (rows and values stay on the device)
+        cp = np.empty(p.getncol() + 1, np.int64)
+        _abi.check(ctx._lib.cbg_result_to_host(ctx._ptr, ctypes.byref(p._res), cp.ctypes.data, None, None), "colptr")
+        return cp
+    lens = sum(np.diff(colptr(p)) for p in parts)
+    tail = {"max_column_positions": int(lens.max()), "columns_over_16k": int((lens > 16384).sum()),
+            "positions_in_columns_over_16k": int(lens[lens > 16384].sum()), "positions": int(lens.sum())}
     byts = sum(nparts) * 12 * 2 + nnzc * 12
     print(json.dumps({"what": "cbg_merge of the two 1x1x2 layer partials", "scale": a.scale, "lib": a.lib,
                       "nnz_partials": nparts, "nnz_C": nnzc, "merge_ms": t * 1e3,
-                      "merge_bytes": byts, "merge_GBps": byts / t / 1e9, "reps_ms": [x * 1e3 for x in ts]}),
+                      "merge_bytes": byts, "merge_GBps": byts / t / 1e9, "reps_ms": [x * 1e3 for x in ts],
+                      "column_skew": tail}),
           flush=True)
 
 
