@@ -324,19 +324,25 @@ template <int NT>
 hipError_t launch_sym_part(hipStream_t st, const PartItem* items, const int* count_dev, int64_t cap, int64_t annz,
                            const int64_t* Acp, const int32_t* Air, const int64_t* Bcp, const int32_t* Bir,
                            const int2* span, const Split& spl, int64_t* nnz, const HeavyOut& ho) {
-  const size_t lds = sym_part_lds<NT>();
-  if (sizeof(SymIx) == 4 && annz >= INT32_MAX) return hipErrorInvalidValue;   // 32-bit staging build
-  // 16-byte row loads (RowLd4) unless CBG_SYM_VEC4=0 or A has fewer than 4 entries
+  // 16-byte row loads (RowLd4) unless CBG_SYM_VEC4=0 or A has fewer than 4 entries; 32-bit segment staging (8 waves
+  // per SIMD) unless A.nnz >= 2^31
   static const bool vec_env = [] { const char* e = std::getenv("CBG_SYM_VEC4"); return !(e && e[0] == '0'); }();
   const bool vec = vec_env && kGroupSym == 4 && annz >= 4;
-  const void* kf = vec ? (const void*)k_sym_part<NT, true> : (const void*)k_sym_part<NT, false>;
+  const bool w32 = annz < INT32_MAX;
+  const size_t lds = w32 ? sym_part_lds<NT, int32_t>() : sym_part_lds<NT, int64_t>();
+  const void* kf = w32 ? (vec ? (const void*)k_sym_part<NT, true, int32_t> : (const void*)k_sym_part<NT, false, int32_t>)
+                       : (vec ? (const void*)k_sym_part<NT, true, int64_t> : (const void*)k_sym_part<NT, false, int64_t>);
   hipError_t e = launch_cfg_lds(kf, lds);
   if (e != hipSuccess) return e;
   const int g = (int)grid_for(cap, 1, kMaxGrid * 2);
-  if (vec)
-    k_sym_part<NT, true><<<g, NT, lds, st>>>(items, count_dev, annz, Acp, Air, Bcp, Bir, span, spl, nnz, ho);
+  if (w32 && vec)
+    k_sym_part<NT, true, int32_t><<<g, NT, lds, st>>>(items, count_dev, annz, Acp, Air, Bcp, Bir, span, spl, nnz, ho);
+  else if (w32)
+    k_sym_part<NT, false, int32_t><<<g, NT, lds, st>>>(items, count_dev, annz, Acp, Air, Bcp, Bir, span, spl, nnz, ho);
+  else if (vec)
+    k_sym_part<NT, true, int64_t><<<g, NT, lds, st>>>(items, count_dev, annz, Acp, Air, Bcp, Bir, span, spl, nnz, ho);
   else
-    k_sym_part<NT, false><<<g, NT, lds, st>>>(items, count_dev, annz, Acp, Air, Bcp, Bir, span, spl, nnz, ho);
+    k_sym_part<NT, false, int64_t><<<g, NT, lds, st>>>(items, count_dev, annz, Acp, Air, Bcp, Bir, span, spl, nnz, ho);
   return hipGetLastError();
 }
 template <int LOGT, class SRT, typename V, bool UNIT>

@@ -1086,31 +1086,21 @@ __global__ void k_part_items(const int32_t* __restrict__ list, int64_t count, in
   }
 }
 
-// CBG_SYM_W8=1: 32-bit segment staging (A.nnz < 2^31) so four 512-thread workgroups fit a CU's LDS, and at most 64
-// VGPRs: 8 waves per SIMD instead of 6
-#ifndef CBG_SYM_W8
-#define CBG_SYM_W8 0
-#endif
-#if CBG_SYM_W8
-typedef int32_t SymIx;
-#define CBG_SYM_WAVES __attribute__((amdgpu_waves_per_eu(8, 8)))
-#else
-typedef int64_t SymIx;
-#define CBG_SYM_WAVES
-#endif
-
-template <int NT>
+// Segment staging of k_sym_part: 32-bit (A.nnz < 2^31; a chunk's segments are distinct A columns, so their offsets
+// stay below A.nnz) lets four 512-thread workgroups share a CU's LDS and the kernel run at <= 64 VGPRs: 8 waves per
+// SIMD instead of 6 (s20 symbolic 23.4 -> 22.1 ms, s21 80.5 -> 75.8 ms, profiles/r04e_*); 64-bit otherwise.
+template <int NT, typename IX>
 constexpr size_t sym_part_lds() {
-  return (size_t)(1 << (kPartLog - 5)) * 4 + (size_t)NT * (2 * sizeof(SymIx) + 5) + (size_t)(NT / kWave + 1) * 8 +
+  return (size_t)(1 << (kPartLog - 5)) * 4 + (size_t)NT * (2 * sizeof(IX) + 5) + (size_t)(NT / kWave + 1) * 8 +
          (size_t)((1 << (kPartLog - kSubLogMin)) + 8) * 4 + 64;
 }
 
-template <int NT, bool VEC>
-__global__ void __launch_bounds__(NT) CBG_SYM_WAVES k_sym_part(const PartItem* __restrict__ items, const int* __restrict__ count_dev,
-                                                 int64_t annz, const int64_t* __restrict__ Acp, const int32_t* __restrict__ Air,
-                                                 const int64_t* __restrict__ Bcp, const int32_t* __restrict__ Bir,
-                                                 const int2* __restrict__ span, Split spl, int64_t* __restrict__ nnz,
-                                                 HeavyOut ho) {
+template <int NT, bool VEC, typename SymIx>
+__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(sizeof(SymIx) == 4 ? 8 : 1, 8)))
+k_sym_part(const PartItem* __restrict__ items, const int* __restrict__ count_dev, int64_t annz,
+           const int64_t* __restrict__ Acp, const int32_t* __restrict__ Air, const int64_t* __restrict__ Bcp,
+           const int32_t* __restrict__ Bir, const int2* __restrict__ span, Split spl, int64_t* __restrict__ nnz,
+           HeavyOut ho) {
   constexpr int T = 1 << (kPartLog - 5);   // bitmap words
   constexpr int WPT = T / NT;              // words per thread in the subwindow count (<= SUBW / 32)
   static_assert(WPT * 32 <= (1 << kSubLogMin), "a thread's words must lie in one subwindow");
