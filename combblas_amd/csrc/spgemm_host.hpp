@@ -1020,8 +1020,464 @@ __global__ void __launch_bounds__(256) k_merge2(int64_t ncol, const int64_t* __r
   }
 }
 
+// ---- flat two-way merge (default; CBG_MERGE_FLAT=0 takes the per-column k_merge2 above) ----
+// The merged sequence of both partials -- keys (column, row), duplicates kept, column c starting at merged position
+// acp[c] + bcp[c] -- is cut into tiles of kFlatT positions regardless of column lengths, so every workgroup moves
+// the same number of entries: one 330k-position column is ~320 tiles, a run of short columns shares one tile.
+// k_flat_split finds each tile boundary (binary search over the column starts, then a merge-path search inside the
+// column) and moves it one position back when it would separate a (part 0, part 1) pair of equal keys.  A tile
+// stages both of its key runs in LDS -- the column of every entry from the column starts inside the tile (marks +
+// a block max-scan) -- each thread takes kFlatPT merged positions by a merge-path search, heads of equal-key runs
+// are counted (count pass) or written at the scanned offsets with the column pointers that start inside the tile
+// (fill pass).  The count pass reads rows only; the fill pass reads rows and values once and writes C once.
+// tile boundaries every kFlatT = kFlatNT * kFlatPT - 1 positions: a boundary moved back by a pair makes its tile one
+// position longer, so a tile holds at most kFlatNT * kFlatPT positions -- one per thread slot
+constexpr int kFlatNT = 256, kFlatPT = 4, kFlatT = kFlatNT * kFlatPT - 1;
+constexpr int kFlatCH = (kFlatT + 2 + kFlatNT - 1) / kFlatNT;   // staged entries per thread in the column scan
+
+static __global__ void k_flat_split(int64_t ncol, const int64_t* __restrict__ acp, const int32_t* __restrict__ air,
+                             const int64_t* __restrict__ bcp, const int32_t* __restrict__ bir, int64_t ntiles,
+                             int64_t* __restrict__ sa, int64_t* __restrict__ sb, int32_t* __restrict__ sc) {
+  const int64_t na = acp[ncol], nb = bcp[ncol], dt = na + nb;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t <= ntiles; t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t d = t * kFlatT;
+    if (d >= dt) {
+      sa[t] = na; sb[t] = nb; sc[t] = (int32_t)ncol;
+      continue;
+    }
+    int64_t lo = 0, hi = ncol - 1;   // the last column starting at or before d (it holds position d)
+    while (lo < hi) {
+      const int64_t mid = (lo + hi + 1) >> 1;
+      if (acp[mid] + bcp[mid] <= d) lo = mid; else hi = mid - 1;
+    }
+    const int64_t c = lo, ca = acp[c], cb = bcp[c];
+    const int64_t la = acp[c + 1] - ca, lb = bcp[c + 1] - cb, k = d - ca - cb;
+    int64_t i0 = k > lb ? k - lb : 0, i1 = k < la ? k : la;
+    while (i0 < i1) {   // part-0 entries among the column's first k merged positions (ties: part 0 first)
+      const int64_t mid = (i0 + i1) >> 1;
+      if (air[ca + mid] <= bir[cb + k - 1 - mid]) i0 = mid + 1; else i1 = mid;
+    }
+    int64_t i = i0;
+    const int64_t j = k - i;
+    if (i > 0 && j < lb && air[ca + i - 1] == bir[cb + j]) --i;   // keep the pair together
+    sa[t] = ca + i; sb[t] = cb + j; sc[t] = (int32_t)c;
+  }
+}
+
+__device__ __forceinline__ int wave_incl_max(int v) {
+  const int l = lane_id();
+#pragma unroll
+  for (int d = 1; d < kWave; d <<= 1) {
+    const int t = __shfl_up(v, d, kWave);
+    if (l >= d) v = max(v, t);
+  }
+  return v;
+}
+
+// col[x] = max(col[0..x]) over the staged part-0 run col[0..na) and, separately, the part-1 run cb[0..nb)
+// (column starts were marked at their first entry); two barriers for both runs
+__device__ __forceinline__ void block_col_scan2(int32_t* ca, int na, int32_t* cb, int nb, int* scratch) {
+  constexpr int NW = kFlatNT / kWave;
+  const int x0 = threadIdx.x * kFlatCH, w = threadIdx.x / kWave, l = lane_id();
+  int ma = INT_MIN, mb = INT_MIN;
+#pragma unroll
+  for (int e = 0; e < kFlatCH; ++e) {
+    if (x0 + e < na) ma = max(ma, ca[x0 + e]);
+    if (x0 + e < nb) mb = max(mb, cb[x0 + e]);
+  }
+  const int ia = wave_incl_max(ma), ib = wave_incl_max(mb);
+  if (l == kWave - 1) {
+    scratch[w] = ia;
+    scratch[NW + w] = ib;
+  }
+  __syncthreads();
+  int ra = __shfl_up(ia, 1, kWave), rb = __shfl_up(ib, 1, kWave);
+  if (l == 0) ra = rb = INT_MIN;
+  for (int q = 0; q < w; ++q) {
+    ra = max(ra, scratch[q]);
+    rb = max(rb, scratch[NW + q]);
+  }
+#pragma unroll
+  for (int e = 0; e < kFlatCH; ++e) {
+    if (x0 + e < na) {
+      ra = max(ra, ca[x0 + e]);
+      ca[x0 + e] = ra;
+    }
+    if (x0 + e < nb) {
+      rb = max(rb, cb[x0 + e]);
+      cb[x0 + e] = rb;
+    }
+  }
+  __syncthreads();
+}
+
+// tile prefix states of the one-pass merge: flag (bits 62-63) | value; flag 1 = the tile's count, 2 = inclusive prefix
+constexpr unsigned long long kFlagAgg = 1ull << 62, kFlagIncl = 2ull << 62, kFlagVal = (1ull << 62) - 1;
+__device__ __forceinline__ unsigned long long flat_state_load(const unsigned long long* p) {
+  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void flat_state_store(unsigned long long* p, unsigned long long v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// MODE 0: count pass (cnt[t] = heads of tile t); MODE 1: fill pass at the scanned offsets toff[t]; MODE 2: one pass --
+// tiles are claimed in order from a device ticket, each publishes its count and finds its offset by a decoupled
+// look-back over its predecessors' states (one wave reads 64 states per step), into an output sized for the
+// duplicate-free bound nnz(P0) + nnz(P1); nnz(C) = the last tile's inclusive prefix (-> *nnz_out)
+template <int SRI, typename V, int MODE>
+__global__ void __launch_bounds__(kFlatNT) __attribute__((amdgpu_waves_per_eu(8, 8))) k_flat_merge(
+    int64_t ncol, const int64_t* __restrict__ acp, const int32_t* __restrict__ air, const V* __restrict__ aval,
+    const int64_t* __restrict__ bcp, const int32_t* __restrict__ bir, const V* __restrict__ bval,
+    const int64_t* __restrict__ sa, const int64_t* __restrict__ sb, const int32_t* __restrict__ sc, int64_t ntiles,
+    int64_t* __restrict__ cnt, const int64_t* __restrict__ toff, int64_t* __restrict__ ccp,
+    int32_t* __restrict__ crow, V* __restrict__ cval, unsigned long long* __restrict__ dups,
+    unsigned long long* __restrict__ disorder, bool stage_out, unsigned long long* __restrict__ state,
+    unsigned long long* __restrict__ ticket, unsigned long long* __restrict__ nnz_out) {
+  constexpr bool FILL = MODE != 0, ONE = MODE == 2;
+  constexpr int T = kFlatT, PT = kFlatPT, NT = kFlatNT;
+  static_assert(NT * PT >= T + 1, "every position of a tile has a thread slot");
+  static_assert(NT * PT <= 32767, "16-bit head positions");
+  // one key array for both runs: part 0 at [0, na), a sentinel, part 1 at [na + 1, n + 1), a sentinel -- 14 KB of
+  // LDS per workgroup, so 8 workgroups (the wave limit) fit a CU
+  __shared__ uint64_t keys[T + 4];
+  __shared__ int32_t cols[T + 4];
+  __shared__ int16_t hpos[T + 2];
+  __shared__ int scr[2 * (NT / kWave) + 2];
+  __shared__ int64_t s_tile[2];   // one pass: the claimed next tile; this tile's offset
+  const int tid = threadIdx.x;
+  unsigned long long bad = 0, ndup = 0;   // summed over the block's tiles, one atomic per wave at the end
+  int64_t t = blockIdx.x;
+  if (ONE) {
+    if (tid == 0) s_tile[0] = (int64_t)atomicAdd(ticket, 1ull);
+    __syncthreads();
+    t = s_tile[0];
+    __syncthreads();
+  }
+  int64_t a0 = 0, b0 = 0, a1 = 0, b1 = 0;
+  int32_t c0 = 0, ce = 0;
+  if (t < ntiles) {
+    a0 = sa[t]; a1 = sa[t + 1]; b0 = sb[t]; b1 = sb[t + 1]; c0 = sc[t]; ce = sc[t + 1];
+  }
+  while (t < ntiles) {
+    // the next tile (one pass: claimed now, in order) and its boundaries, loaded while this one is merged
+    int64_t tn = t + gridDim.x;
+    if (ONE) {
+      if (tid == 0) s_tile[0] = (int64_t)atomicAdd(ticket, 1ull);
+      __syncthreads();
+      tn = s_tile[0];
+    }
+    int64_t na0 = 0, nb0 = 0, na1 = 0, nb1 = 0;
+    int32_t nc0 = 0, nce = 0;
+    if (tn < ntiles) {
+      na0 = sa[tn]; na1 = sa[tn + 1]; nb0 = sb[tn]; nb1 = sb[tn + 1]; nc0 = sc[tn]; nce = sc[tn + 1];
+    }
+    const int64_t ta = a1 - a0, tb = b1 - b0;
+    if (ta < 0 || tb < 0 || ta + tb > T + 1) {   // boundaries out of order: only a partial with unsorted rows
+      if (!FILL && tid == 0) {
+        cnt[t] = 0;
+        ++bad;
+      }
+      if (ONE && tid == 0) {   // the chain goes on (the merge is declined afterwards)
+        ++bad;
+        unsigned long long ex = 0;
+        if (t > 0) {
+          unsigned long long v;
+          while (((v = flat_state_load(state + t - 1)) & kFlagIncl) == 0) __builtin_amdgcn_s_sleep(1);
+          ex = v & kFlagVal;
+        }
+        flat_state_store(state + t, kFlagIncl | ex);
+        if (t == ntiles - 1) *nnz_out = ex;
+      }
+    } else {
+      const int na = (int)ta, nb = (int)tb, n = na + nb;
+      uint64_t* ka = keys;
+      uint64_t* kb = keys + na + 1;
+      int32_t* ca = cols;
+      int32_t* cb = cols + na + 1;
+      // a column boundary inside the tile?  (uniform) -- tiles inside one long column skip the column scan
+      const int32_t cl = ce < ncol ? ce : (int32_t)(ncol - 1);
+      const bool multi = cl > c0;
+      // tile-edge order check: the entry before each run, when it lies in the run's first column
+      int32_t pra = -1, prb = -1;
+      int64_t acp0 = 0, bcp0 = 0;
+      if ((!FILL || ONE) && tid == 0) {
+        acp0 = acp[c0]; bcp0 = bcp[c0];
+        if (a0 > 0) pra = air[a0 - 1];
+        if (b0 > 0) prb = bir[b0 - 1];
+      }
+      if (multi) {
+        for (int x = tid; x < na; x += NT) ca[x] = c0;
+        for (int x = tid; x < nb; x += NT) cb[x] = c0;
+        __syncthreads();
+        for (int64_t c = (int64_t)c0 + 1 + tid; c <= cl; c += NT) {   // columns starting inside the tile
+          const int64_t pa = acp[c] - a0, pb = bcp[c] - b0;
+          if (pa < na) atomicMax(&ca[pa], (int)c);
+          if (pb < nb) atomicMax(&cb[pb], (int)c);
+        }
+        __syncthreads();
+        block_col_scan2(ca, na, cb, nb, scr);
+      }
+      for (int x = tid; x < na; x += NT)
+        ka[x] = ((uint64_t)(uint32_t)(multi ? ca[x] : c0) << 32) | (uint32_t)air[a0 + x];
+      for (int x = tid; x < nb; x += NT)
+        kb[x] = ((uint64_t)(uint32_t)(multi ? cb[x] : c0) << 32) | (uint32_t)bir[b0 + x];
+      if (tid == 0) {
+        ka[na] = ~0ull;
+        kb[nb] = ~0ull;
+      }
+      __syncthreads();
+      if (!FILL || ONE) {   // the merge needs strictly ascending rows per column
+        for (int x = tid + 1; x < na; x += NT) bad += ka[x] <= ka[x - 1];
+        for (int x = tid + 1; x < nb; x += NT) bad += kb[x] <= kb[x - 1];
+        if (tid == 0) {
+          if (na > 0 && (uint32_t)(ka[0] >> 32) == (uint32_t)c0 && a0 > acp0) bad += (uint32_t)ka[0] <= (uint32_t)pra;
+          if (nb > 0 && (uint32_t)(kb[0] >> 32) == (uint32_t)c0 && b0 > bcp0) bad += (uint32_t)kb[0] <= (uint32_t)prb;
+        }
+      }
+      // this thread's merged positions d0 .. d0+PT-1
+      const int d0 = tid * PT;
+      int lo = d0 > nb ? d0 - nb : 0, hi = d0 < na ? d0 : na;
+      if (d0 > n) lo = hi = 0;   // idle thread (n < T): no position, no reads
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (ka[mid] <= kb[d0 - 1 - mid]) lo = mid + 1; else hi = mid;
+      }
+      int i = lo, j = d0 - lo;
+      // key at position d0 - 1: the larger of the last part-0 and part-1 keys taken so far
+      uint64_t prev = 0;
+      bool has_prev = d0 > 0 && d0 <= n;
+      if (has_prev) {
+        const uint64_t pa = i > 0 ? ka[i - 1] : 0, pb = j > 0 ? kb[j - 1] : 0;
+        prev = pa > pb ? pa : pb;
+      }
+      uint32_t row[PT];
+      int src[PT];   // part-0 index, or -1 - part-1 index
+      bool head[PT], pair[PT];
+      int c = 0, nd = 0;
+#pragma unroll
+      for (int e = 0; e < PT; ++e) {
+        const bool in = d0 + e < n;   // then i < na or j < nb
+        const bool take_a = in && i < na && (j >= nb || ka[i] <= kb[j]);
+        const uint64_t key = !in ? ~0ull : take_a ? ka[i] : kb[j];
+        row[e] = (uint32_t)key;
+        src[e] = take_a ? i : -1 - j;
+        pair[e] = take_a && j < nb && kb[j] == key;
+        head[e] = in && (!has_prev || key != prev);
+        has_prev = true;
+        prev = key;
+        if (in) { if (take_a) ++i; else ++j; }
+        c += head[e];
+        nd += pair[e];
+      }
+      if (!FILL) {
+        int tot;
+        (void)block_excl_scan<NT>(c, scr, &tot);
+        ndup += nd;
+        if (tid == 0) cnt[t] = tot;
+      } else {
+        V v[PT];   // the values are gathered before the scan's barriers
+#pragma unroll
+        for (int e = 0; e < PT; ++e) {
+          v[e] = V(0);
+          if (head[e]) {
+            const int s = src[e];
+            v[e] = s >= 0 ? (aval ? aval[a0 + s] : V(1)) : (bval ? bval[b0 + (-1 - s)] : V(1));
+            if (pair[e]) v[e] = merge_pair<SRI, V>(v[e], bval ? bval[b0 + (d0 + e - s)] : V(1));
+          }
+        }
+        int tot;
+        const int ex = block_excl_scan<NT>(c, scr, &tot);   // its barriers also end every read of keys / cols
+        int64_t o;
+        if (ONE) {
+          ndup += nd;
+          if (tid < kWave) {   // wave 0: publish the count, then look back for the offset
+            if (tid == 0) flat_state_store(state + t, (t == 0 ? kFlagIncl : kFlagAgg) | (unsigned long long)tot);
+            unsigned long long acc = 0;
+            for (int64_t p = t - 1; p >= 0; p -= kWave) {
+              const int64_t q = p - tid;
+              unsigned long long v = kFlagIncl;   // before tile 0: inclusive 0
+              if (q >= 0)
+                while (((v = flat_state_load(state + q)) >> 62) == 0) __builtin_amdgcn_s_sleep(1);
+              const unsigned long long incl = __ballot((v & kFlagIncl) != 0);
+              const int f = incl ? __ffsll((long long)incl) - 1 : kWave;   // nearest inclusive predecessor
+              const int64_t part = wave_sum64(tid <= f ? (int64_t)(v & kFlagVal) : 0);
+              acc += (unsigned long long)part;
+              if (incl) break;
+            }
+            if (t > 0 && tid == 0) flat_state_store(state + t, kFlagIncl | (acc + (unsigned long long)tot));
+            if (tid == 0) {
+              s_tile[1] = (int64_t)acc;
+              if (t == ntiles - 1) *nnz_out = acc + (unsigned long long)tot;
+            }
+          }
+          __syncthreads();
+          o = s_tile[1];
+        } else {
+          o = toff[t];
+        }
+        int q = ex;
+        if (stage_out) {   // the tile's output through LDS (over the staged keys): coalesced stores
+          int32_t* orow = cols;
+          V* oval = (V*)keys;
+#pragma unroll
+          for (int e = 0; e < PT; ++e) {
+            if (d0 + e < n) hpos[d0 + e] = (int16_t)q;
+            if (head[e]) {
+              orow[q] = (int32_t)row[e];
+              oval[q] = v[e];
+              ++q;
+            }
+          }
+          if (tid == 0) hpos[n] = (int16_t)tot;
+          __syncthreads();
+          for (int x = tid; x < tot; x += NT) {
+            crow[o + x] = orow[x];
+            cval[o + x] = oval[x];
+          }
+        } else {
+#pragma unroll
+          for (int e = 0; e < PT; ++e) {
+            if (d0 + e < n) hpos[d0 + e] = (int16_t)q;
+            if (head[e]) {
+              crow[o + q] = (int32_t)row[e];
+              cval[o + q] = v[e];
+              ++q;
+            }
+          }
+          if (tid == 0) hpos[n] = (int16_t)tot;
+          __syncthreads();
+        }
+        // column pointers of the columns starting in this tile (a column starting exactly at the tile's end is
+        // written by both neighbours, with the same value); tile 0 also owns the empty columns before c0
+        const int64_t dbase = a0 + b0;
+        const int64_t cs = t == 0 ? 0 : c0, cend = ce < ncol ? ce : ncol;
+        for (int64_t cc = cs + tid; cc <= cend; cc += NT) {
+          const int64_t dl = acp[cc] + bcp[cc] - dbase;
+          if (dl >= 0 && dl <= n) ccp[cc] = o + hpos[dl];
+        }
+      }
+    }
+    __syncthreads();   // the tile's LDS (and the claimed ticket slot) are free for the next one
+    t = tn;
+    a0 = na0; a1 = na1; b0 = nb0; b1 = nb1; c0 = nc0; ce = nce;
+  }
+  if (!FILL || ONE) {
+    const int64_t d = wave_sum64((int64_t)ndup), x = wave_sum64((int64_t)bad);
+    if (lane_id() == 0) {
+      if (d) atomicAdd(dups, (unsigned long long)d);
+      if (x) atomicAdd(disorder, (unsigned long long)x);
+    }
+  }
+}
+
+template <int SRI, typename V>
+cbg_status merge2_flat(cbg_ctx* ctx, const cbg_csc_result* parts, cbg_csc_result* C) {
+  hipStream_t st = ctx->stream;
+  const int64_t ncol = parts[0].ncol;
+  const bool add_is_error = SRI == SR_BOOL_COPY1ST || SRI == SR_BOOL_COPY2ND;
+  const int64_t dt = parts[0].nnz + parts[1].nnz;
+  const char* se = std::getenv("CBG_MERGE_STAGE");   // 0: the fill pass stores from registers
+  const bool stage = !se || std::atoi(se) != 0;
+  if (ncol >= INT32_MAX) return CBG_EINVAL;   // the staged keys carry 32-bit columns: the per-column merge runs
+  std::unique_ptr<Owner> own(new Owner(ctx->pool));
+  HIPCHK(own->cp.reserve(8 * (ncol + 1)));
+  const V* av = (const V*)parts[0].val;
+  const V* bv = (const V*)parts[1].val;
+  int64_t nnz = 0;
+  if (ncol == 0 || dt == 0) {
+    HIPCHK(hipMemsetAsync(own->cp.p, 0, 8 * (ncol + 1), st));
+    HIPCHK(own->ir.reserve(4));
+    HIPCHK(own->val.reserve(sizeof(V)));
+    HIPCHK(hipStreamSynchronize(st));
+  } else {
+    const int64_t ntiles = (dt + kFlatT - 1) / kFlatT;
+    PoolBuf cnt, tiles, spl;
+    cnt.pool = tiles.pool = spl.pool = ctx->pool;
+    HIPCHK(spl.reserve(20 * (ntiles + 1) + 16));
+    HIPCHK(cnt.reserve(16 * (ntiles + 1)));   // tile counts, then their exclusive offsets
+    int64_t* toff = cnt.as<int64_t>() + ntiles + 1;
+    const int64_t nst = (ntiles + kScanTile - 1) / kScanTile;
+    HIPCHK(tiles.reserve(8 * (nst + 1)));
+    HIPCHK(ctx->scalars.reserve(256));
+    unsigned long long* sc = ctx->scalars.as<unsigned long long>();
+    HIPCHK(hipMemsetAsync(sc, 0, 32, st));
+    int64_t* sa = spl.as<int64_t>();
+    int64_t* sb = sa + ntiles + 1;
+    int32_t* scol = (int32_t*)(sb + ntiles + 1);
+    k_flat_split<<<(int)grid_for(ntiles + 1, 256, kMaxGrid * 4), 256, 0, st>>>(
+        ncol, parts[0].colptr, parts[0].row, parts[1].colptr, parts[1].row, ntiles, sa, sb, scol);
+    const int g = (int)grid_for(ntiles, 1, kMaxGrid * 8);
+    // one pass (default; CBG_MERGE_ONEPASS=0: count pass, scan, fill pass) into an output sized for nnz(P0) + nnz(P1)
+    const char* oe = std::getenv("CBG_MERGE_ONEPASS");
+    bool one = !oe || std::atoi(oe) != 0;
+    if (one && (own->ir.reserve(4 * (dt + 1)) != hipSuccess || own->val.reserve(sizeof(V) * (dt + 1)) != hipSuccess)) {
+      (void)hipGetLastError();
+      release_workspace(ctx);   // the product workspace is idle between calls: give it back and retry once
+      if (own->ir.reserve(4 * (dt + 1)) != hipSuccess || own->val.reserve(sizeof(V) * (dt + 1)) != hipSuccess) {
+        (void)hipGetLastError();
+        one = false;   // the exact-size two-pass merge may still fit
+      }
+    }
+    unsigned long long* h = pinned<unsigned long long>(ctx, kPinMerge);   // pairs, nnz(C), disorder
+    if (one) {
+      PoolBuf state;
+      state.pool = ctx->pool;
+      HIPCHK(state.reserve(8 * (ntiles + 1)));
+      HIPCHK(hipMemsetAsync(state.p, 0, 8 * (ntiles + 1), st));
+      HIPCHK(hipMemsetAsync(sc + 3, 0, 8, st));   // the tile ticket
+      const int g1 = (int)std::min<int64_t>(ntiles, 4096);
+      k_flat_merge<SRI, V, 2><<<g1, kFlatNT, 0, st>>>(ncol, parts[0].colptr, parts[0].row, av, parts[1].colptr,
+                                                      parts[1].row, bv, sa, sb, scol, ntiles, nullptr, nullptr,
+                                                      own->cp.as<int64_t>(), own->ir.as<int32_t>(), own->val.as<V>(),
+                                                      sc, sc + 2, stage, state.as<unsigned long long>(), sc + 3,
+                                                      sc + 1);
+      HIPCHK(hipGetLastError());
+      HIPCHK(hipMemcpyAsync(h, sc, 24, hipMemcpyDeviceToHost, st));
+      HIPCHK(hipStreamSynchronize(st));
+      if (h[2]) return CBG_EINVAL;   // a partial is not row-sorted: the caller takes the hash merge
+      if (add_is_error && h[0]) return CBG_EADD;
+      nnz = (int64_t)h[1];
+    } else {
+    k_flat_merge<SRI, V, 0><<<g, kFlatNT, 0, st>>>(ncol, parts[0].colptr, parts[0].row, av, parts[1].colptr,
+                                                   parts[1].row, bv, sa, sb, scol, ntiles, cnt.as<int64_t>(),
+                                                   nullptr, nullptr, nullptr, nullptr, sc, sc + 2, false, nullptr,
+                                                   nullptr, nullptr);
+    k_scan_tiles<<<(int)nst, 256, 0, st>>>(ntiles, cnt.as<int64_t>(), tiles.as<int64_t>());
+    k_scan_sums<<<1, 1024, 0, st>>>(nst, tiles.as<int64_t>(), (int64_t*)(sc + 1));
+    k_scan_apply<<<(int)nst, 256, 0, st>>>(ntiles, cnt.as<int64_t>(), tiles.as<int64_t>(), toff);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(h, sc, 24, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    if (h[2]) return CBG_EINVAL;   // a partial is not row-sorted: the caller takes the hash merge
+    if (add_is_error && h[0]) return CBG_EADD;
+    nnz = (int64_t)h[1];
+    if (own->ir.reserve(4 * (nnz + 1)) != hipSuccess || own->val.reserve(sizeof(V) * (nnz + 1)) != hipSuccess) {
+      (void)hipGetLastError();
+      release_workspace(ctx);
+      HIPCHK(own->ir.reserve(4 * (nnz + 1)));
+      HIPCHK(own->val.reserve(sizeof(V) * (nnz + 1)));
+    }
+    k_flat_merge<SRI, V, 1><<<g, kFlatNT, 0, st>>>(ncol, parts[0].colptr, parts[0].row, av, parts[1].colptr,
+                                                   parts[1].row, bv, sa, sb, scol, ntiles, nullptr, toff,
+                                                   own->cp.as<int64_t>(), own->ir.as<int32_t>(), own->val.as<V>(),
+                                                   nullptr, nullptr, stage, nullptr, nullptr, nullptr);
+    }
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(st));   // split / cnt / tiles go back to the pool on return
+  }
+  memset(C, 0, sizeof(*C));
+  C->nrow = parts[0].nrow; C->ncol = ncol; C->nnz = nnz;
+  C->colptr = own->cp.as<int64_t>(); C->row = own->ir.as<int32_t>(); C->val = own->val.p;
+  C->val_type = DtOf<V>::value;
+  C->_owner = own.release();
+  return CBG_OK;
+}
+
 template <int SRI, typename V>
 cbg_status merge2_sr(cbg_ctx* ctx, const cbg_csc_result* parts, cbg_csc_result* C) {
+  const char* fe = std::getenv("CBG_MERGE_FLAT");
+  const bool flat = !fe || std::atoi(fe) != 0;
+  if (flat && parts[0].ncol < INT32_MAX) return merge2_flat<SRI, V>(ctx, parts, C);
   hipStream_t st = ctx->stream;
   const int64_t ncol = parts[0].ncol;
   const bool add_is_error = SRI == SR_BOOL_COPY1ST || SRI == SR_BOOL_COPY2ND;

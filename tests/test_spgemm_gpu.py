@@ -473,3 +473,47 @@ def test_gpu_two_way_merge_edge_cases(gpu_ctx):
     with pytest.raises(cb.CbgError) as ei:
         cb.MultiwayMerge(SRCLS["bool_copy1st"]("i64"), [upload(gpu_ctx, P0), upload(gpu_ctx, P1)])
     assert ei.value.status == 13
+
+
+@pytest.mark.parametrize("flat", ["1", "0"])
+@pytest.mark.parametrize("sr,dt", [("plus_times", "f64"), ("plus_times", "i64"), ("min_plus", "i64"),
+                                   ("select2nd", "i64"), ("select_max", "f64")])
+def test_gpu_flat_merge_tiles(gpu_ctx, monkeypatch, flat, sr, dt):
+    """The flat two-way merge (1023-position tiles over the whole merged sequence, one pass or count + fill) and the per-column one give
+    the oracle's MultiwayMerge: leading / inner / trailing runs of empty columns, a one-entry column before a
+    10k-row column whose rows all pair up (every tile boundary falls inside a pair and moves back), short
+    columns sharing tiles, one-sided columns, and an empty partial."""
+    from helpers import oracle_merge
+    monkeypatch.setenv("CBG_MERGE_FLAT", flat)
+    rng = np.random.default_rng(zlib.crc32(repr((sr, dt)).encode()))
+    n = 20000
+    lens = [(0, 0)] * 5 + [(1, 0), (10000, 10000), (0, 0), (3, 4), (0, 7), (9, 0)] + [(0, 0)] * 300 + \
+           [(int(a), int(b)) for a, b in rng.integers(0, 40, (2000, 2))] + [(2500, 1700), (1, 1)] + [(0, 0)] * 50
+    cols_a, cols_b = [], []
+    for j, (la, lb) in enumerate(lens):
+        if j == 6:   # identical rows: every entry is a pair
+            a = np.sort(rng.choice(n, la, replace=False))
+            cols_a.append(a); cols_b.append(a.copy())
+            continue
+        base = rng.choice(n, la + lb, replace=False)
+        a = np.sort(base[:la])
+        share = rng.choice(a, min(la, lb // 2), replace=False) if la else np.zeros(0, np.int64)
+        b = np.unique(np.concatenate([share, base[la:la + lb - len(share)]]))[:lb]
+        cols_a.append(a); cols_b.append(np.sort(b))
+    m = len(lens)
+    npdt = np.float64 if dt == "f64" else np.int64
+
+    def mk(cols):
+        cp = np.concatenate([[0], np.cumsum([len(c) for c in cols])]).astype(np.int64)
+        ir = np.concatenate(cols).astype(np.int32)
+        v = rng.random(len(ir)) + 0.5 if dt == "f64" else rng.integers(1, 9, len(ir))
+        return Csc(n, m, cp, ir, v.astype(npdt))
+    P0, P1 = mk(cols_a), mk(cols_b)
+    E = Csc(n, m, np.zeros(m + 1, np.int64), np.zeros(0, np.int32), np.zeros(0, npdt))
+    for parts in ([P0, P1], [P1, P0], [P0, E], [E, P1], [E, E]):
+        R, rc = oracle_merge(parts, sr, dt)
+        assert rc == 0
+        M = cb.MultiwayMerge(SRCLS[sr](dt), [upload(gpu_ctx, P) for P in parts])
+        cp, ir, val = M.to_host()
+        assert_same_product(Csc(n, m, cp, ir, val), R, dt, scale=np.abs(R.val) * 2 if dt == "f64" else None,
+                            what=f"flat={flat} merge {sr}")
