@@ -1112,18 +1112,9 @@ __device__ __forceinline__ void block_col_scan2(int32_t* ca, int na, int32_t* cb
 }
 
 // tile prefix states of the one-pass merge: flag (bits 62-63) | value; flag 1 = the tile's count, 2 = inclusive prefix
-constexpr unsigned long long kFlagAgg = 1ull << 62, kFlagIncl = 2ull << 62, kFlagVal = (1ull << 62) - 1;
-__device__ __forceinline__ unsigned long long flat_state_load(const unsigned long long* p) {
-  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void flat_state_store(unsigned long long* p, unsigned long long v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// MODE 0: count pass (cnt[t] = heads of tile t); MODE 1: fill pass at the scanned offsets toff[t]; MODE 2: one pass --
-// tiles are claimed in order from a device ticket, each publishes its count and finds its offset by a decoupled
-// look-back over its predecessors' states (one wave reads 64 states per step), into an output sized for the
-// duplicate-free bound nnz(P0) + nnz(P1); nnz(C) = the last tile's inclusive prefix (-> *nnz_out)
+// MODE 0: count pass (cnt[t] = heads of tile t); MODE 1: fill pass at the scanned offsets toff[t].  (A one-pass
+// variant -- tiles claimed in order, offsets by a decoupled look-back -- measured 146 ms against 36.7 for the two
+// passes at s20: the look-back chain serialises the tiles; staging the values in LDS too: 42.4 ms, r04k.)
 template <int SRI, typename V, int MODE>
 __global__ void __launch_bounds__(kFlatNT) __attribute__((amdgpu_waves_per_eu(8, 8))) k_flat_merge(
     int64_t ncol, const int64_t* __restrict__ acp, const int32_t* __restrict__ air, const V* __restrict__ aval,
@@ -1131,9 +1122,8 @@ __global__ void __launch_bounds__(kFlatNT) __attribute__((amdgpu_waves_per_eu(8,
     const int64_t* __restrict__ sa, const int64_t* __restrict__ sb, const int32_t* __restrict__ sc, int64_t ntiles,
     int64_t* __restrict__ cnt, const int64_t* __restrict__ toff, int64_t* __restrict__ ccp,
     int32_t* __restrict__ crow, V* __restrict__ cval, unsigned long long* __restrict__ dups,
-    unsigned long long* __restrict__ disorder, bool stage_out, unsigned long long* __restrict__ state,
-    unsigned long long* __restrict__ ticket, unsigned long long* __restrict__ nnz_out) {
-  constexpr bool FILL = MODE != 0, ONE = MODE == 2;
+    unsigned long long* __restrict__ disorder, bool stage_out) {
+  constexpr bool FILL = MODE != 0;
   constexpr int T = kFlatT, PT = kFlatPT, NT = kFlatNT;
   static_assert(NT * PT >= T + 1, "every position of a tile has a thread slot");
   static_assert(NT * PT <= 32767, "16-bit head positions");
@@ -1143,29 +1133,17 @@ __global__ void __launch_bounds__(kFlatNT) __attribute__((amdgpu_waves_per_eu(8,
   __shared__ int32_t cols[T + 4];
   __shared__ int16_t hpos[T + 2];
   __shared__ int scr[2 * (NT / kWave) + 2];
-  __shared__ int64_t s_tile[2];   // one pass: the claimed next tile; this tile's offset
   const int tid = threadIdx.x;
   unsigned long long bad = 0, ndup = 0;   // summed over the block's tiles, one atomic per wave at the end
   int64_t t = blockIdx.x;
-  if (ONE) {
-    if (tid == 0) s_tile[0] = (int64_t)atomicAdd(ticket, 1ull);
-    __syncthreads();
-    t = s_tile[0];
-    __syncthreads();
-  }
   int64_t a0 = 0, b0 = 0, a1 = 0, b1 = 0;
   int32_t c0 = 0, ce = 0;
   if (t < ntiles) {
     a0 = sa[t]; a1 = sa[t + 1]; b0 = sb[t]; b1 = sb[t + 1]; c0 = sc[t]; ce = sc[t + 1];
   }
   while (t < ntiles) {
-    // the next tile (one pass: claimed now, in order) and its boundaries, loaded while this one is merged
-    int64_t tn = t + gridDim.x;
-    if (ONE) {
-      if (tid == 0) s_tile[0] = (int64_t)atomicAdd(ticket, 1ull);
-      __syncthreads();
-      tn = s_tile[0];
-    }
+    // the next tile's boundaries, loaded while this one is merged
+    const int64_t tn = t + gridDim.x;
     int64_t na0 = 0, nb0 = 0, na1 = 0, nb1 = 0;
     int32_t nc0 = 0, nce = 0;
     if (tn < ntiles) {
@@ -1176,17 +1154,6 @@ __global__ void __launch_bounds__(kFlatNT) __attribute__((amdgpu_waves_per_eu(8,
       if (!FILL && tid == 0) {
         cnt[t] = 0;
         ++bad;
-      }
-      if (ONE && tid == 0) {   // the chain goes on (the merge is declined afterwards)
-        ++bad;
-        unsigned long long ex = 0;
-        if (t > 0) {
-          unsigned long long v;
-          while (((v = flat_state_load(state + t - 1)) & kFlagIncl) == 0) __builtin_amdgcn_s_sleep(1);
-          ex = v & kFlagVal;
-        }
-        flat_state_store(state + t, kFlagIncl | ex);
-        if (t == ntiles - 1) *nnz_out = ex;
       }
     } else {
       const int na = (int)ta, nb = (int)tb, n = na + nb;
@@ -1200,7 +1167,7 @@ __global__ void __launch_bounds__(kFlatNT) __attribute__((amdgpu_waves_per_eu(8,
       // tile-edge order check: the entry before each run, when it lies in the run's first column
       int32_t pra = -1, prb = -1;
       int64_t acp0 = 0, bcp0 = 0;
-      if ((!FILL || ONE) && tid == 0) {
+      if (!FILL && tid == 0) {
         acp0 = acp[c0]; bcp0 = bcp[c0];
         if (a0 > 0) pra = air[a0 - 1];
         if (b0 > 0) prb = bir[b0 - 1];
@@ -1226,7 +1193,7 @@ __global__ void __launch_bounds__(kFlatNT) __attribute__((amdgpu_waves_per_eu(8,
         kb[nb] = ~0ull;
       }
       __syncthreads();
-      if (!FILL || ONE) {   // the merge needs strictly ascending rows per column
+      if (!FILL) {   // the merge needs strictly ascending rows per column
         for (int x = tid + 1; x < na; x += NT) bad += ka[x] <= ka[x - 1];
         for (int x = tid + 1; x < nb; x += NT) bad += kb[x] <= kb[x - 1];
         if (tid == 0) {
@@ -1287,34 +1254,7 @@ __global__ void __launch_bounds__(kFlatNT) __attribute__((amdgpu_waves_per_eu(8,
         }
         int tot;
         const int ex = block_excl_scan<NT>(c, scr, &tot);   // its barriers also end every read of keys / cols
-        int64_t o;
-        if (ONE) {
-          ndup += nd;
-          if (tid < kWave) {   // wave 0: publish the count, then look back for the offset
-            if (tid == 0) flat_state_store(state + t, (t == 0 ? kFlagIncl : kFlagAgg) | (unsigned long long)tot);
-            unsigned long long acc = 0;
-            for (int64_t p = t - 1; p >= 0; p -= kWave) {
-              const int64_t q = p - tid;
-              unsigned long long v = kFlagIncl;   // before tile 0: inclusive 0
-              if (q >= 0)
-                while (((v = flat_state_load(state + q)) >> 62) == 0) __builtin_amdgcn_s_sleep(1);
-              const unsigned long long incl = __ballot((v & kFlagIncl) != 0);
-              const int f = incl ? __ffsll((long long)incl) - 1 : kWave;   // nearest inclusive predecessor
-              const int64_t part = wave_sum64(tid <= f ? (int64_t)(v & kFlagVal) : 0);
-              acc += (unsigned long long)part;
-              if (incl) break;
-            }
-            if (t > 0 && tid == 0) flat_state_store(state + t, kFlagIncl | (acc + (unsigned long long)tot));
-            if (tid == 0) {
-              s_tile[1] = (int64_t)acc;
-              if (t == ntiles - 1) *nnz_out = acc + (unsigned long long)tot;
-            }
-          }
-          __syncthreads();
-          o = s_tile[1];
-        } else {
-          o = toff[t];
-        }
+        const int64_t o = toff[t];
         int q = ex;
         if (stage_out) {   // the tile's output through LDS (over the staged keys): coalesced stores
           int32_t* orow = cols;
@@ -1357,11 +1297,11 @@ __global__ void __launch_bounds__(kFlatNT) __attribute__((amdgpu_waves_per_eu(8,
         }
       }
     }
-    __syncthreads();   // the tile's LDS (and the claimed ticket slot) are free for the next one
+    __syncthreads();   // the tile's LDS is free for the next one
     t = tn;
     a0 = na0; a1 = na1; b0 = nb0; b1 = nb1; c0 = nc0; ce = nce;
   }
-  if (!FILL || ONE) {
+  if (!FILL) {
     const int64_t d = wave_sum64((int64_t)ndup), x = wave_sum64((int64_t)bad);
     if (lane_id() == 0) {
       if (d) atomicAdd(dups, (unsigned long long)d);
@@ -1400,48 +1340,17 @@ cbg_status merge2_flat(cbg_ctx* ctx, const cbg_csc_result* parts, cbg_csc_result
     HIPCHK(tiles.reserve(8 * (nst + 1)));
     HIPCHK(ctx->scalars.reserve(256));
     unsigned long long* sc = ctx->scalars.as<unsigned long long>();
-    HIPCHK(hipMemsetAsync(sc, 0, 32, st));
+    HIPCHK(hipMemsetAsync(sc, 0, 24, st));
     int64_t* sa = spl.as<int64_t>();
     int64_t* sb = sa + ntiles + 1;
     int32_t* scol = (int32_t*)(sb + ntiles + 1);
     k_flat_split<<<(int)grid_for(ntiles + 1, 256, kMaxGrid * 4), 256, 0, st>>>(
         ncol, parts[0].colptr, parts[0].row, parts[1].colptr, parts[1].row, ntiles, sa, sb, scol);
     const int g = (int)grid_for(ntiles, 1, kMaxGrid * 8);
-    // one pass (default; CBG_MERGE_ONEPASS=0: count pass, scan, fill pass) into an output sized for nnz(P0) + nnz(P1)
-    const char* oe = std::getenv("CBG_MERGE_ONEPASS");
-    bool one = !oe || std::atoi(oe) != 0;
-    if (one && (own->ir.reserve(4 * (dt + 1)) != hipSuccess || own->val.reserve(sizeof(V) * (dt + 1)) != hipSuccess)) {
-      (void)hipGetLastError();
-      release_workspace(ctx);   // the product workspace is idle between calls: give it back and retry once
-      if (own->ir.reserve(4 * (dt + 1)) != hipSuccess || own->val.reserve(sizeof(V) * (dt + 1)) != hipSuccess) {
-        (void)hipGetLastError();
-        one = false;   // the exact-size two-pass merge may still fit
-      }
-    }
     unsigned long long* h = pinned<unsigned long long>(ctx, kPinMerge);   // pairs, nnz(C), disorder
-    if (one) {
-      PoolBuf state;
-      state.pool = ctx->pool;
-      HIPCHK(state.reserve(8 * (ntiles + 1)));
-      HIPCHK(hipMemsetAsync(state.p, 0, 8 * (ntiles + 1), st));
-      HIPCHK(hipMemsetAsync(sc + 3, 0, 8, st));   // the tile ticket
-      const int g1 = (int)std::min<int64_t>(ntiles, 4096);
-      k_flat_merge<SRI, V, 2><<<g1, kFlatNT, 0, st>>>(ncol, parts[0].colptr, parts[0].row, av, parts[1].colptr,
-                                                      parts[1].row, bv, sa, sb, scol, ntiles, nullptr, nullptr,
-                                                      own->cp.as<int64_t>(), own->ir.as<int32_t>(), own->val.as<V>(),
-                                                      sc, sc + 2, stage, state.as<unsigned long long>(), sc + 3,
-                                                      sc + 1);
-      HIPCHK(hipGetLastError());
-      HIPCHK(hipMemcpyAsync(h, sc, 24, hipMemcpyDeviceToHost, st));
-      HIPCHK(hipStreamSynchronize(st));
-      if (h[2]) return CBG_EINVAL;   // a partial is not row-sorted: the caller takes the hash merge
-      if (add_is_error && h[0]) return CBG_EADD;
-      nnz = (int64_t)h[1];
-    } else {
     k_flat_merge<SRI, V, 0><<<g, kFlatNT, 0, st>>>(ncol, parts[0].colptr, parts[0].row, av, parts[1].colptr,
                                                    parts[1].row, bv, sa, sb, scol, ntiles, cnt.as<int64_t>(),
-                                                   nullptr, nullptr, nullptr, nullptr, sc, sc + 2, false, nullptr,
-                                                   nullptr, nullptr);
+                                                   nullptr, nullptr, nullptr, nullptr, sc, sc + 2, false);
     k_scan_tiles<<<(int)nst, 256, 0, st>>>(ntiles, cnt.as<int64_t>(), tiles.as<int64_t>());
     k_scan_sums<<<1, 1024, 0, st>>>(nst, tiles.as<int64_t>(), (int64_t*)(sc + 1));
     k_scan_apply<<<(int)nst, 256, 0, st>>>(ntiles, cnt.as<int64_t>(), tiles.as<int64_t>(), toff);
@@ -1460,8 +1369,7 @@ cbg_status merge2_flat(cbg_ctx* ctx, const cbg_csc_result* parts, cbg_csc_result
     k_flat_merge<SRI, V, 1><<<g, kFlatNT, 0, st>>>(ncol, parts[0].colptr, parts[0].row, av, parts[1].colptr,
                                                    parts[1].row, bv, sa, sb, scol, ntiles, nullptr, toff,
                                                    own->cp.as<int64_t>(), own->ir.as<int32_t>(), own->val.as<V>(),
-                                                   nullptr, nullptr, stage, nullptr, nullptr, nullptr);
-    }
+                                                   nullptr, nullptr, stage);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(st));   // split / cnt / tiles go back to the pool on return
   }
