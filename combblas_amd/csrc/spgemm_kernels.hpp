@@ -64,7 +64,10 @@ constexpr int kUnrollHeavy = CBG_UNROLL_HEAVY;    // same, k_num_heavy
 constexpr int kGroupSym = CBG_GROUP_SYM;  // consecutive A entries per lane group (one segment search each), symbolic
 constexpr int kGroupNum = CBG_GROUP_NUM;  // same, numeric
 constexpr int kGroupHeavy = CBG_GROUP_HEAVY;     // same, k_num_heavy
-constexpr int64_t kHeavy = 4096;   // nnz(C(:,j)) above which a column is split into units
+#ifndef CBG_HEAVY_MIN
+#define CBG_HEAVY_MIN 4096
+#endif
+constexpr int64_t kHeavy = CBG_HEAVY_MIN;   // nnz(C(:,j)) above which a column is split into units
 // k_num_heavy geometry: table 2^CBG_HEAVY_LOGT slots, CBG_HEAVY_NT threads (LDS decides WGs per CU)
 #ifndef CBG_HEAVY_LOGT
 #define CBG_HEAVY_LOGT 13
