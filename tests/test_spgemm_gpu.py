@@ -479,7 +479,7 @@ def test_gpu_two_way_merge_edge_cases(gpu_ctx):
 @pytest.mark.parametrize("sr,dt", [("plus_times", "f64"), ("plus_times", "i64"), ("min_plus", "i64"),
                                    ("select2nd", "i64"), ("select_max", "f64")])
 def test_gpu_flat_merge_tiles(gpu_ctx, monkeypatch, flat, sr, dt):
-    """The flat two-way merge (1023-position tiles over the whole merged sequence, one pass or count + fill) and the per-column one give
+    """The flat two-way merge (1023-position tiles over the whole merged sequence: count pass, scan, fill pass) and the per-column one give
     the oracle's MultiwayMerge: leading / inner / trailing runs of empty columns, a one-entry column before a
     10k-row column whose rows all pair up (every tile boundary falls inside a pair and moves back), short
     columns sharing tiles, one-sided columns, and an empty partial."""
