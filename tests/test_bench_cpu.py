@@ -1,12 +1,16 @@
 """bench.py's host helpers on CPU tensors: the rank-share panels (A pieces side by side, B pieces stacked by rows,
 as grid.hip's panel_cols / panel_rows lay them out), the fiber wire-byte count, the evidence-file order and the
-entry checksum shared with oracle/ref/refbench.cpp."""
+entry checksum shared with oracle/ref/refbench.cpp, and tools/predict_scaling.py's step model."""
+import os
+
 import numpy as np
 import scipy.sparse as sp
 import torch
 
 import bench
 from combblas_amd import dist as cbd
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _block(M):
@@ -67,3 +71,25 @@ def test_entry_checksum_is_order_independent():
     # same entries, rows of column 0 swapped: a different CSC order, the same multiset
     assert a == bench.entry_checksum(cp, np.array([5, 1, 0], np.int32), np.array([2.0, 1.0, 3.0]))
     assert a != bench.entry_checksum(cp, ir, np.array([1.0, 2.0, 4.0]))
+
+
+def test_predict_scaling_model():
+    """tools/predict_scaling.py: a fast link hides the fiber behind the own half, a slow one exposes it (less with
+    more chunks); one-layer layouts pay broadcasts and one product only."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("predict_scaling", os.path.join(ROOT, "tools", "predict_scaling.py"))
+    ps = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(ps)
+    ph = [{"total_ms": 50.0}, {"total_ms": 50.0}]
+    r2 = {"rank": 0, "layout": "2x1x1", "scale": 21, "nnz_A_panel": 10, "nnz_B_panel": 10, "phases_ms": ph,
+          "fiber": {"bytes": 5e9}, "recv_nnz": 0, "merge_ms": 20.0, "multiplies": 1e10}
+    fast = ps.predict([r2], link_gbps=1000.0)
+    assert fast["parts_ms"]["fiber_exposed"] == 0.0 and abs(fast["step_ms"] - 121.0) < 0.5
+    slow2 = ps.predict([r2], link_gbps=50.0, chunks=2)["parts_ms"]["fiber_exposed"]
+    slow4 = ps.predict([r2], link_gbps=50.0, chunks=4)["parts_ms"]["fiber_exposed"]
+    assert slow2 > slow4 > 0   # 5 GB at 50 GB/s = 100 ms against 75 ms of compute after the first chunk
+    r4 = {"rank": 0, "layout": "1x2x2", "scale": 21, "nnz_A_panel": 1e7, "nnz_B_panel": 1e7,
+          "phases_ms": [{"total_ms": 55.0}], "fiber": None, "merge_ms": 0.0, "multiplies": 5e9}
+    p4 = ps.predict([r4, dict(r4, rank=1)], link_gbps=60.0)
+    assert p4["parts_ms"]["merge"] == 0.0 and abs(p4["parts_ms"]["bcast"] - 2.0) < 1e-6   # 120 MB at 60 GB/s
+    assert p4["multiplies"] == 1e10

@@ -1,0 +1,66 @@
+#!/usr/bin/env python3
+"""Predicted N-GPU step time of the mandated layouts from the one-GPU rank shares (`bench.py --rank-share`).
+
+Per rank: the panel broadcasts (its A and B panels less the pieces it owns, over one link), then on two-layer grids
+the fiber pipeline -- the other layer's column half multiplied in C chunks, each chunk's message sent as soon as it
+is made while the next chunk and then the own half multiply (one link per direction, the partner's message arriving
+on the same schedule) -- then the decode of the received message and the merge; one-layer grids multiply once.
+The step is the slowest rank's; the value is the multiplies of all ranks over it.
+
+usage: python tools/predict_scaling.py profiles/r04l_rank_share_s22_n8.jsonl [--link-GBps 64] [--chunks 2]
+"""
+import argparse
+import json
+
+
+def rank_step(rec, link_gbps, chunks, decode_gbps=5000.0, entry_bytes=12):
+    """Milliseconds of one rank's step (see the module docstring); returns (total, parts)."""
+    bw = link_gbps * 1e9 / 1e3   # bytes per ms
+    L = int(rec["layout"].split("x")[0])
+    q = int(rec["layout"].split("x")[1])
+    # panels: q pieces of A along the grid row and q of B along the grid column arrive, the own ones do not move
+    panel_bytes = (rec["nnz_A_panel"] + rec["nnz_B_panel"]) * entry_bytes * (q - 1) / q
+    bcast = panel_bytes / bw
+    ph = rec["phases_ms"]
+    if L == 1 or not rec.get("fiber"):
+        compute = sum(p["total_ms"] for p in ph)
+        return bcast + compute, {"bcast": bcast, "compute": compute, "fiber_exposed": 0.0, "decode": 0.0, "merge": 0.0}
+    t_other, t_mine = ph[0]["total_ms"], ph[1]["total_ms"]
+    wire = rec["fiber"]["bytes"]
+    x = wire / chunks / bw
+    send_end = 0.0
+    for c in range(1, chunks + 1):
+        send_end = max(c * t_other / chunks, send_end) + x
+    compute_end = t_other + t_mine
+    fiber_exposed = max(0.0, send_end - compute_end)
+    # decode: read the wire bytes, write the piece's rows and values
+    decode = (wire + rec.get("recv_nnz", 0) * entry_bytes) / (decode_gbps * 1e9 / 1e3)
+    merge = rec["merge_ms"]
+    total = bcast + compute_end + fiber_exposed + decode + merge
+    return total, {"bcast": bcast, "compute": compute_end, "fiber_exposed": fiber_exposed, "decode": decode,
+                   "merge": merge}
+
+
+def predict(records, link_gbps=64.0, chunks=2):
+    steps = [rank_step(r, link_gbps, chunks) for r in records]
+    worst = max(range(len(steps)), key=lambda i: steps[i][0])
+    mult = sum(r["multiplies"] for r in records)
+    ms = steps[worst][0]
+    return {"ranks": len(records), "layout": records[0]["layout"], "scale": records[0]["scale"],
+            "link_GBps": link_gbps, "chunks": chunks, "step_ms": round(ms, 2),
+            "multiplies": mult, "multiplies_per_s": mult / (ms / 1e3),
+            "slowest_rank": records[worst]["rank"], "parts_ms": {k: round(v, 2) for k, v in steps[worst][1].items()}}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("jsonl")
+    ap.add_argument("--link-GBps", type=float, default=64.0)
+    ap.add_argument("--chunks", type=int, default=2)
+    a = ap.parse_args()
+    recs = [json.loads(l) for l in open(a.jsonl) if l.startswith("{")]
+    print(json.dumps(predict(recs, a.link_GBps, a.chunks)))
+
+
+if __name__ == "__main__":
+    main()
