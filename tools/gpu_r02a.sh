@@ -18,7 +18,7 @@ rc=$?; echo "pytest rc=$rc"; tail -4 "$OUT/gpu_tests.log"
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 
 step bench
-timeout -k 10 600 python -u bench.py > "$OUT/bench.log" 2>&1 || { echo "bench failed"; tail -20 "$OUT/bench.log"; exit 3; }
+timeout -k 10 600 python -u bench.py > "$OUT/bench.log" 2>&1 || { echo "bench failed"; tail -20 "$OUT/bench.log"; exit 13; }
 tail -1 "$OUT/bench.log"
 
 step kernel-stats

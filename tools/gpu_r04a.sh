@@ -8,7 +8,7 @@ mkdir -p $OUT
 export TMPDIR=/tmp
 timeout -k 10 600 python -u -m pytest tests/test_spgemm_gpu.py -x -q --timeout 120 --timeout-method thread > $OUT/tests.log 2>&1
 rc=$?; tail -2 $OUT/tests.log; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 600 python -u bench.py > $OUT/bench.log 2>&1 || { echo "bench failed"; tail -5 $OUT/bench.log | cut -c1-800; exit 3; }
+timeout -k 10 600 python -u bench.py > $OUT/bench.log 2>&1 || { echo "bench failed"; tail -5 $OUT/bench.log | cut -c1-800; exit 13; }
 tail -1 $OUT/bench.log | cut -c1-2500
 for v in "dyn:" "static:tools/var/static/libcbgpu.so" ; do
   name=${v%%:*}; lib=${v#*:}

@@ -7,9 +7,9 @@ mkdir -p $OUT
 export TMPDIR=/tmp
 timeout -k 10 1000 python -u -m pytest tests/test_dist_gpu.py tests/test_dropin.py -x -v --timeout 300 --timeout-method thread > $OUT/dist_tests.log 2>&1
 rc=$?; grep -E "passed|failed|PASS|FAIL" $OUT/dist_tests.log | tail -40; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 600 python -u bench.py --rank-share 0,4 --gpus-virtual 8 --scale 22 > $OUT/rank_share_s22.jsonl 2> $OUT/rank_share.err || { tail -5 $OUT/rank_share.err; exit 3; }
+timeout -k 10 600 python -u bench.py --rank-share 0,4 --gpus-virtual 8 --scale 22 > $OUT/rank_share_s22.jsonl 2> $OUT/rank_share.err || { tail -5 $OUT/rank_share.err; exit 13; }
 cut -c1-900 $OUT/rank_share_s22.jsonl
-timeout -k 10 600 python -u bench.py --rank-share all --gpus-virtual 2 --scale 21 > $OUT/rank_share_s21_n2.jsonl 2> $OUT/rank_share2.err || { tail -5 $OUT/rank_share2.err; exit 3; }
+timeout -k 10 600 python -u bench.py --rank-share all --gpus-virtual 2 --scale 21 > $OUT/rank_share_s21_n2.jsonl 2> $OUT/rank_share2.err || { tail -5 $OUT/rank_share2.err; exit 13; }
 cut -c1-900 $OUT/rank_share_s21_n2.jsonl
 timeout -k 10 300 python3 tools/bench_merge.py --scale 20 --reps 3 --lib tools/var/merge_old/libcbgpu.so > $OUT/merge_old.log 2>&1 || { tail -5 $OUT/merge_old.log; exit 4; }
 tail -1 $OUT/merge_old.log | cut -c1-600

@@ -8,9 +8,9 @@ export TMPDIR=/tmp
 timeout -k 10 300 python3 tools/bench_merge.py --scale 20 --reps 3 > $OUT/merge.log 2>&1 || { tail -5 $OUT/merge.log; exit 4; }
 timeout -k 10 300 python3 tools/bench_merge.py --scale 20 --reps 3 --lib tools/var/merge_old/libcbgpu.so > $OUT/merge_old.log 2>&1 || { tail -5 $OUT/merge_old.log; exit 4; }
 tail -qn1 $OUT/merge.log $OUT/merge_old.log | cut -c1-400
-timeout -k 10 600 python -u bench.py --rank-share 0 --gpus-virtual 8 --scale 22 > $OUT/rank_share_s22.jsonl 2> $OUT/rank_share.err || { tail -5 $OUT/rank_share.err; exit 3; }
-timeout -k 10 600 python -u bench.py --rank-share all --gpus-virtual 2 --scale 21 > $OUT/rank_share_s21_n2.jsonl 2> $OUT/rank_share2.err || { tail -5 $OUT/rank_share2.err; exit 3; }
-timeout -k 10 600 python -u bench.py --rank-share 0 --gpus-virtual 4 --scale 21 > $OUT/rank_share_s21_n4.jsonl 2> $OUT/rank_share4.err || { tail -5 $OUT/rank_share4.err; exit 3; }
+timeout -k 10 600 python -u bench.py --rank-share 0 --gpus-virtual 8 --scale 22 > $OUT/rank_share_s22.jsonl 2> $OUT/rank_share.err || { tail -5 $OUT/rank_share.err; exit 13; }
+timeout -k 10 600 python -u bench.py --rank-share all --gpus-virtual 2 --scale 21 > $OUT/rank_share_s21_n2.jsonl 2> $OUT/rank_share2.err || { tail -5 $OUT/rank_share2.err; exit 13; }
+timeout -k 10 600 python -u bench.py --rank-share 0 --gpus-virtual 4 --scale 21 > $OUT/rank_share_s21_n4.jsonl 2> $OUT/rank_share4.err || { tail -5 $OUT/rank_share4.err; exit 13; }
 cut -c1-600 $OUT/rank_share_*.jsonl
 timeout -k 10 300 python3 -u bench.py --no-cpu --steps 10 --warmup 2 > $OUT/s20_main.log 2>&1 || exit 5
 timeout -k 10 300 python3 -u tools/var_bench.py sym_w8 part19 -- --no-cpu --steps 10 --warmup 2 > $OUT/s20_var.log 2>&1 || exit 5

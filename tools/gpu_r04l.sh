@@ -15,5 +15,5 @@ timeout -k 10 240 python -u bench.py --rank-share all --gpus-virtual 2 --scale 2
 rc=$?; cut -c1-260 $OUT/rank_share_s21_n2.jsonl; [ $rc -eq 0 ] || { tail -5 $OUT/rs2.err; exit $rc; }
 timeout -k 10 240 python -u bench.py --rank-share all --gpus-virtual 4 --scale 21 > $OUT/rank_share_s21_n4.jsonl 2> $OUT/rs4.err
 rc=$?; cut -c1-260 $OUT/rank_share_s21_n4.jsonl; [ $rc -eq 0 ] || { tail -5 $OUT/rs4.err; exit $rc; }
-timeout -k 10 300 python -u bench.py > $OUT/bench.log 2>&1 || { echo "bench failed"; tail -5 $OUT/bench.log | cut -c1-600; exit 3; }
+timeout -k 10 300 python -u bench.py > $OUT/bench.log 2>&1 || { echo "bench failed"; tail -5 $OUT/bench.log | cut -c1-600; exit 13; }
 tail -1 $OUT/bench.log | cut -c1-600
