@@ -114,6 +114,28 @@ def sample_columns(n, flop_col, target_mults):
     return np.arange(0, n, stride), stride
 
 
+def host_cores(n_gpus_visible=1):
+    """Host threads for the CPU baselines: the cores this process may run on (affinity), capped by a cgroup CPU quota
+    and by the pool's share of 16 cores per visible GPU (os.cpu_count() shows the whole machine there).  Returns
+    (threads, record of every figure)."""
+    import math
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    threads = aff
+    if quota:
+        threads = min(threads, max(1, math.floor(quota)))
+    share = 16 * max(1, n_gpus_visible)
+    threads = max(1, min(threads, share))
+    return threads, {"os_cpu_count": os.cpu_count(), "affinity_cpus": aff, "cgroup_quota_cpus": quota,
+                     "pool_share_cpus": share, "OMP_NUM_THREADS_env": os.environ.get("OMP_NUM_THREADS")}
+
+
 def cpu_baseline(cp, ir, val, n, flop_col, target_mults):
     """Oracle (CPU restatement, oracle/oracle.c) on a bounded sample: every s-th column of B.
     Returns (baseline JSON, the oracle's product of the sampled columns)."""
@@ -124,7 +146,8 @@ def cpu_baseline(cp, ir, val, n, flop_col, target_mults):
     idx = np.concatenate([np.arange(cp[c], cp[c + 1]) for c in cols]) if len(cols) else np.zeros(0, np.int64)
     A = Csc(n, n, cp, ir, val)
     B = Csc(n, len(cols), bcp, ir[idx], val[idx])
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    threads, _ = host_cores(_visible_gpus())
+    os.environ["OMP_NUM_THREADS"] = str(threads)   # the oracle's OpenMP pool starts on first use, in this process
     t0 = time.perf_counter()
     C, mults, rc = oracle_spgemm(A, B, "plus_times", "f64")
     dt = time.perf_counter() - t0
@@ -133,6 +156,14 @@ def cpu_baseline(cp, ir, val, n, flop_col, target_mults):
              "sample": f"oracle/oracle.c (CPU restatement of LocalSpGEMMHash, OpenMP, {threads} threads) on "
                        f"every {stride}-th column of B ({len(cols)} columns, {mults} multiplies, {dt:.2f} s)"},
             (cols, C))
+
+
+def _visible_gpus():
+    try:
+        import torch
+        return max(1, torch.cuda.device_count())
+    except Exception:
+        return 1
 
 
 def verify_sample(Cdev, cols, R):
@@ -149,6 +180,36 @@ def verify_sample(Cdev, cols, R):
 
 
 REFBENCH = os.path.join(HERE, "oracle", "_ref", "refbench")
+
+
+def _s64(u):
+    return u - (1 << 64) if u >= 1 << 63 else u
+
+
+_MIX = [_s64(0x9E3779B97F4A7C15), _s64(0xBF58476D1CE4E5B9), _s64(0x94D049BB133111EB)]
+
+
+def _lsr(x, k):
+    """Logical right shift of an int64 tensor (two's complement bits)."""
+    return (x >> k) & ((1 << (64 - k)) - 1)
+
+
+def _mix64_t(x):
+    """splitmix64 finaliser on an int64 torch tensor (wrapping arithmetic = the uint64 bits of _mix64)."""
+    x = x + _MIX[0]
+    x = (x ^ _lsr(x, 30)) * _MIX[1]
+    x = (x ^ _lsr(x, 27)) * _MIX[2]
+    return x ^ _lsr(x, 31)
+
+
+def entry_checksum_t(cols, rows, val):
+    """entry_checksum's sum over the entries (global col ids, rows, f64 values as torch tensors on any device), as an
+    int64 whose bits are the uint64 sum mod 2^64 -- summable over ranks."""
+    import torch
+    if rows.numel() == 0:
+        return 0
+    h = _mix64_t((rows.to(torch.int64) << 32) ^ cols.to(torch.int64)) ^ _mix64_t(val.contiguous().view(torch.int64))
+    return int(h.sum().item())
 
 
 def _mix64(x):
@@ -317,6 +378,7 @@ def bench_local(args):
             out["cpu_baseline"] = {
                 "value": h["multiplies"] / h["seconds"], "unit": "multiplies/s", "cores": h["omp_threads"],
                 "mpi_ranks": h["mpi_ranks"], "omp_threads": h["omp_threads"], "kind": "reference",
+                "host": host_cores(_visible_gpus())[1],
                 "sample": f"the reference's LocalSpGEMMHash<PlusTimesSRing<double,double>> (mtSpGEMM.h:465-661, "
                           f"oracle/_ref/refbench built from /root/reference sources, -O3 -fopenmp) at 1 MPI rank x "
                           f"{h['omp_threads']} OpenMP threads on every {stride}-th column of B ({h['columns']} columns, "
@@ -340,6 +402,66 @@ def bench_local(args):
 
 
 # ------------------------------------------------------------------------------------------ N > 1
+def select_block_cols(b, cols):
+    """Columns `cols` (sorted local ids, int64 tensor) of a Block, as a Block on the same device."""
+    import torch
+    from combblas_amd import dist as cbd
+    cols = cols.to(device=b.cp.device, dtype=torch.int64)
+    s, e = b.cp[cols], b.cp[cols + 1]
+    ln = e - s
+    cp = torch.zeros(cols.numel() + 1, dtype=torch.int64, device=b.cp.device)
+    torch.cumsum(ln, 0, out=cp[1:])
+    tot = int(cp[-1].item())
+    idx = torch.repeat_interleave(s - cp[:-1], ln, output_size=tot) + torch.arange(tot, device=b.cp.device)
+    return cbd.Block(b.nrow, int(cols.numel()), cp, b.ir[idx], b.val[idx])
+
+
+def piece_reference(be, args, n, r0, r1, c0, c1):
+    """What a rank's output piece C(r0:r1, c0:c1) must be made of, built on the rank's own GPU independently of the
+    grid: A(r0:r1, :) and A(:, c0:c1) from the reference's generator, and the symbolic pass (estimateFLOP + exact
+    nnz) of their product."""
+    Arow = be.rmat_block(args.scale, args.edgefactor, args.seed, r0, r1, 0, n)
+    Acol = be.rmat_block(args.scale, args.edgefactor, args.seed, 0, n, c0, c1)
+    mults, nnz = be.estimate(Arow, Acol)
+    return Arow, Acol, mults, nnz
+
+
+def verify_piece(be, SR, blk, Arow, Acol, r0, c0, nsample, seed, ref_stride=0):
+    """Check one rank's output piece: a seeded random sample of its columns bit for bit against a one-GPU product
+    A(r0:r1, :) * A(:, J_sample) (R-MAT values are multiplicities, so PlusTimes<double> sums are exact), and the
+    reference-sample checksum: entry_checksum over the piece's columns j = 0 mod ref_stride (global row ids, column
+    id j // ref_stride), summable over ranks into the checksum of oracle/_ref/refbench's product of those columns."""
+    import torch
+    ncols = blk.ncol
+    k = min(ncols, int(nsample))
+    g = torch.Generator().manual_seed(int(seed))
+    sel = torch.randperm(ncols, generator=g)[:k].sort().values
+    P = be.multiply(Arow, select_block_cols(Acol, sel), SR)
+    S = select_block_cols(blk, sel)
+    exact = bool(P.nnz == S.nnz and torch.equal(P.cp, S.cp) and torch.equal(P.ir, S.ir)
+                 and torch.equal(P.val.view(torch.int64), S.val.view(torch.int64)))
+    rec = {"sampled_columns": k, "sample_nnz": P.nnz, "bit_exact": exact}
+    del P, S
+    if ref_stride:
+        first = (-c0) % ref_stride
+        jl = torch.arange(first, ncols, ref_stride, dtype=torch.int64)
+        R = select_block_cols(blk, jl)
+        cols = torch.repeat_interleave((jl.to(R.cp.device) + c0) // ref_stride, torch.diff(R.cp), output_size=R.nnz)
+        rec["ref_sample_nnz"] = R.nnz
+        rec["ref_sample_checksum"] = entry_checksum_t(cols, R.ir.to(torch.int64) + r0, R.val)
+    return rec
+
+
+def local_roofline(st, ms_key="local_ms"):
+    """SURVEY 8(d) algorithmic bytes of a rank's local products (grid stats summed over its products): the heavy
+    kernels' share (the dominant kernel) and the whole local products."""
+    hb = (st.get("heavy_multiplies", 0) * (S_I + S_V) + st.get("heavy_nnz_b", 0) * (S_I + S_V + 2 * S_P)
+          + st.get("heavy_nnz_c", 0) * (S_I + S_V))
+    lb = balg_bytes(st.get("multiplies", 0), st.get("local_nnz_out", 0), st.get("local_nnz_b", 0),
+                    st.get("local_ncol_b", 0))
+    return hb, lb
+
+
 def bench_dist(args, world, rank, local_rank):
     import torch
     import torch.distributed as dist
@@ -379,15 +501,18 @@ def bench_dist(args, world, rank, local_rank):
     SR = cb.PlusTimesSRing("f64")
 
     phases = {}
+    keep = {}
 
-    def step():
+    def step(keep_result=False):
         st = {}
         C = cbd.Mult_AnXBn_SUMMA3D(SR, A, B, st)
         nz = C.block.nnz
+        if keep_result:   # the last timed product is kept for the checks below (no extra work timed)
+            keep["C"] = C
         del C
-        for k in ("bcast_ms", "local_ms", "merge_ms", "fiber_ms", "total_ms", "bcast_bytes", "fiber_bytes",
-                  "fiber_xfer_ms"):
-            phases[k] = phases.get(k, 0) + st.get(k, 0)
+        for k, v in st.items():
+            if isinstance(v, (int, float)):
+                phases[k] = phases.get(k, 0) + v
         return st.get("multiplies", 0), nz
 
     step()   # first product also sets up libcbgpu's grid (its RCCL communicators); a failure ends the run
@@ -403,39 +528,123 @@ def bench_dist(args, world, rank, local_rank):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     mults = nnzc = 0
-    for _ in range(args.steps):
-        m, z = step()
+    nzs = []
+    for s_ in range(args.steps):
+        m, z = step(keep_result=(s_ == args.steps - 1))
         mults += m
         nnzc += z
+        nzs.append(z)
     torch.cuda.synchronize()
     dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    t = torch.tensor([elapsed], dtype=torch.float64, device=be.comm_device)
+    cd = be.comm_device
+    t = torch.tensor([elapsed], dtype=torch.float64, device=cd)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    s = torch.tensor([mults, nnzc], dtype=torch.float64, device=be.comm_device)
+    elapsed_local = elapsed
+    s = torch.tensor([mults, nnzc], dtype=torch.float64, device=cd)
     dist.all_reduce(s)
     elapsed, mults, nnzc = float(t.item()), float(s[0].item()), float(s[1].item())
+
+    # ---- checks, outside the timed region: every rank's piece against its independent reference
+    C = keep.pop("C")
+    (r0, r1), (c0, c1) = C.local_range()
+    Arow, Acol, est_m, est_z = piece_reference(be, args, n, r0, r1, c0, c1)
+    tot = torch.tensor([est_m, est_z], dtype=torch.int64, device=cd)
+    dist.all_reduce(tot)
+    flops_global, nnz_global = int(tot[0].item()), int(tot[1].item())
+    ref_stride = max(1, int(np.ceil(flops_global / max(args.cpu_mults, 1)))) if not args.no_cpu else 0
+    nsample = max(int(np.ceil(1e4 / world)), C.block.ncol // 64)
+    v = verify_piece(be, SR, C.block, Arow, Acol, r0, c0, nsample, args.seed + 7919 * rank, ref_stride)
+    v.update({"rank": rank, "rows": [r0, r1], "cols": [c0, c1], "piece_nnz": C.block.nnz,
+              "piece_nnz_equals_estimate": C.block.nnz == est_z, "steps_same_nnz": len(set(nzs)) == 1})
+    del Arow, Acol
+    # per-rank roofline of the local products over the timed steps (grid stats), gathered with the checks
+    hb, lb = local_roofline(phases)
+    rrec = {"heavy_bytes": hb / args.steps, "heavy_ms": phases.get("heavy_ms", 0.0) / args.steps,
+            "local_bytes": lb / args.steps, "local_ms": phases.get("local_ms", 0.0) / args.steps,
+            "step_ms": 1e3 * elapsed_local / args.steps}
+    recs = [None] * world
+    dist.all_gather_object(recs, {"verify": v, "roofline": rrec, "phases": {k: w / args.steps for k, w in phases.items()}})
+    csum = torch.tensor([v.get("ref_sample_checksum", 0), v.get("ref_sample_nnz", 0)], dtype=torch.int64, device=cd)
+    dist.all_reduce(csum)   # int64 sums wrap: the uint64 checksum mod 2^64
+    ok_all = all(r["verify"]["bit_exact"] and r["verify"]["piece_nnz_equals_estimate"] and r["verify"]["steps_same_nnz"]
+                 for r in recs)
+    ok_all = ok_all and int(mults / args.steps) == flops_global and int(nnzc / args.steps) == nnz_global
+    keep.clear()
+    del C
+    torch.cuda.empty_cache()
+
     if rank == 0:
         cfg = workload(args.scale, args.edgefactor,
                        f"{L}x{q}x{q} ({'3D split SUMMA' if L > 1 else '2D SUMMA'}), "
                        f"libcbgpu grid over {ginfo['kind']}")
         cfg.update({"nnz_A": nnzb, "multiplies": int(mults / args.steps), "nnz_C": int(nnzc / args.steps)})
+        slow = max(range(world), key=lambda r: recs[r]["roofline"]["local_ms"])
+        rs = recs[slow]["roofline"]
+        ach = rs["heavy_bytes"] / (rs["heavy_ms"] / 1e3) / 1e9 if rs["heavy_ms"] > 0 else 0.0
         out = {"metric": METRIC, "value": mults / elapsed, "unit": "multiplies/s", "n_gpus": world,
                "steps": args.steps, "warmup": args.warmup, "ms_per_step": 1000.0 * elapsed / args.steps,
                "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
                "data": "synthetic", "config": cfg,
                "effective_GBps": balg_bytes(mults / args.steps, nnzc / args.steps, nnzb, n)
                / (elapsed / args.steps) / 1e9,
-               "rank0_phases_per_step": {k: round(v / args.steps, 3) for k, v in phases.items()},
+               "roofline": {"bound": "hbm", "kernel": "k_num_heavy_known + k_num_heavy on the slowest rank (its local "
+                                                      "products per step; HIP events on the library stream)",
+                            "rank": slow, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                            "frac": ach / HBM_PEAK_GBS, "traffic": None,
+                            "algorithmic_bytes_per_step": rs["heavy_bytes"], "avg_ms_per_step": rs["heavy_ms"],
+                            "step": {"local_algorithmic_bytes": rs["local_bytes"], "local_ms": rs["local_ms"],
+                                     "local_GBps": rs["local_bytes"] / (rs["local_ms"] / 1e3) / 1e9
+                                     if rs["local_ms"] > 0 else 0.0, "rank_step_ms": rs["step_ms"]},
+                            "per_rank": [{k: round(x, 3) if isinstance(x, float) else x for k, x in r["roofline"].items()}
+                                         for r in recs]},
+               "verified": {"bit_exact": all(r["verify"]["bit_exact"] for r in recs),
+                            "sampled_columns": sum(r["verify"]["sampled_columns"] for r in recs),
+                            "sampled_nnz": sum(r["verify"]["sample_nnz"] for r in recs),
+                            "against": "per rank: a seeded sample of its output columns vs a one-GPU product "
+                                       "A(rows_i, :) * A(:, J_sample) built independently of the grid (cbg_rmat_block)",
+                            "multiplies_equal_estimateFLOP": int(mults / args.steps) == flops_global,
+                            "nnz_equal_symbolic": int(nnzc / args.steps) == nnz_global,
+                            "estimateFLOP": flops_global, "nnz_symbolic": nnz_global, "ok": ok_all,
+                            "per_rank": [r["verify"] for r in recs]},
+               "rank0_phases_per_step": {k: round(w, 3) for k, w in recs[0]["phases"].items()},
                "grid_transport": ginfo["kind"],
                # members of every communicator as RCCL itself counts them (ncclCommCount)
                "rccl_ranks": ginfo["ranks"] if ginfo["kind"] == "rccl" else None,
                "input": {"generator": "SpParMat3D.from_rmat: each rank builds its own A and B pieces on its GPU "
                                       "(cbg_rmat_block, the reference's Graph500 edge stream)", "seed": args.seed,
                          "rank0_device_build_s": round(build_s, 4), "nnz": nnzb}}
+        if not args.no_cpu:
+            # the reference's own CPU SpGEMM on every ref_stride-th column of the global product (rank 0's host
+            # cores), its output checksum against the sum of the ranks' checksums of the same columns
+            Ag = ctx.generate_rmat(args.scale, args.edgefactor, seed=args.seed)
+            cp, ir, val = Ag.to_host()
+            Ag.free()
+            threads, host = host_cores(_visible_gpus())
+            ref = reference_baseline(n, cp, ir, val, ref_stride, threads)
+            del cp, ir, val
+            if ref and "LocalSpGEMMHash" in ref:
+                h = ref["LocalSpGEMMHash"]
+                out["cpu_baseline"] = {
+                    "value": h["multiplies"] / h["seconds"], "unit": "multiplies/s", "cores": h["omp_threads"],
+                    "mpi_ranks": h["mpi_ranks"], "omp_threads": h["omp_threads"], "kind": "reference", "host": host,
+                    "sample": f"the reference's LocalSpGEMMHash<PlusTimesSRing<double,double>> (mtSpGEMM.h:465-661, "
+                              f"oracle/_ref/refbench) at 1 MPI rank x {h['omp_threads']} OpenMP threads on rank 0's "
+                              f"host, every {ref_stride}-th column of B ({h['columns']} columns, {h['multiplies']} "
+                              f"multiplies, {h['seconds']:.2f} s)"}
+                got = f"{int(csum[0].item()) & ((1 << 64) - 1):016x}"
+                out["verified"]["reference_checksum_equal"] = (h["checksum"] == got
+                                                               and h["nnzC"] == int(csum[1].item()))
+                out["verified"]["reference_sample"] = {"stride": ref_stride, "nnz": h["nnzC"],
+                                                       "checksum_reference": h["checksum"], "checksum_grid": got}
+                ok_all = ok_all and out["verified"]["reference_checksum_equal"]
+                out["verified"]["ok"] = ok_all
         print(json.dumps(out), flush=True)
+    dist.barrier()
     dist.destroy_process_group()
+    if not ok_all:
+        sys.exit("bench: the distributed product failed its checks (verified.per_rank)")
 
 
 def bench_1d(args, world, rank, ctx, be, n, backend):
@@ -663,6 +872,7 @@ def bench_rank_share(args):
         BP = _vstack([be.rmat_block(args.scale, args.edgefactor, args.seed, k0, k1, b0, b1) for (k0, k1) in k_ranges])
         return AP, BP
 
+    bad = False
     for r in ranks:
         l, rem = divmod(r, q * q)
         i, j = divmod(rem, q)
@@ -697,6 +907,9 @@ def bench_rank_share(args):
                 t1 = time.perf_counter()
                 p_other = ctx.last_profile()
                 wire = fiber_wire_bytes(Po)
+                if rep == 1:   # the production encoder + decoder on the same message (cbg_fiber_codec)
+                    chunks = int(os.environ.get("CBG_FIBER_CHUNKS", "2"))
+                    codec = be.fiber_codec(Po, chunks)
                 del Po
                 t2 = time.perf_counter()
                 Pm = be.multiply(AP, _col_slice_block(BP, *halves[me]), SR, st)
@@ -713,6 +926,7 @@ def bench_rank_share(args):
                 local_ms = 1e3 * ((t1 - t0) + (t3 - t2))
                 merge_ms = 1e3 * (t5 - t4)
                 nnz_out = M.nnz
+                final = M if rep == 1 else None   # checked below, after the record's timings
                 del Pm, M, Pr
                 profs = [p_other, p_mine]
             else:
@@ -722,9 +936,27 @@ def bench_rank_share(args):
                 merge_ms, wire = 0.0, None
                 nnz_out = Pm.nnz
                 profs = [ctx.last_profile()]
+                final = Pm if rep == 1 else None
                 del Pm
             torch.cuda.synchronize()
             torch.cuda.empty_cache()
+        del AP, BP
+        torch.cuda.empty_cache()
+        # the rank's finished piece C(rows_i, columns) against its independent reference (verify_piece)
+        r0, r1 = cbd.block_range(n, q, i)
+        b0, _ = cbd.block_range(n, q, j)
+        h0, h1 = halves[me]
+        Arow, Acol, est_m, est_z = piece_reference(be, args, n, r0, r1, b0 + h0, b0 + h1)
+        nsample = max(int(np.ceil(1e4 / N)), final.ncol // 64)
+        v = verify_piece(be, SR, final, Arow, Acol, r0, b0 + h0, nsample, args.seed + 7919 * r)
+        v.update({"piece_nnz": final.nnz, "piece_nnz_equals_estimate": final.nnz == est_z,
+                  "piece_multiplies_estimate": est_m})
+        rec["verified"] = v
+        if L == 2:
+            rec["fiber_codec"] = codec
+            rec["fiber_codec_vs_estimate"] = round(codec["wire_bytes"] / max(wire["bytes"], 1), 5)
+        del final, Arow, Acol
+        torch.cuda.empty_cache()
         rec["phases_ms"] = [{k: round(float(pp[k]), 3) for k in phase_keys} for pp in profs]
         rec.update({"multiplies": st.get("multiplies", 0), "local_ms": round(local_ms, 3),
                     "merge_ms": round(merge_ms, 3), "nnz_C_piece": nnz_out,
@@ -733,11 +965,13 @@ def bench_rank_share(args):
                     "fiber": wire,
                     "peak_hbm_GB": round((total - floor[0]) / 1e9, 2), "hbm_total_GB": round(total / 1e9, 1)})
         print(json.dumps(rec), flush=True)
-        del AP, BP
-        torch.cuda.empty_cache()
+        bad = bad or not (v["bit_exact"] and v["piece_nnz_equals_estimate"]
+                          and (L == 1 or codec["roundtrip_exact"]))
     dist.destroy_process_group()
     if os.path.exists(store.name):
         os.unlink(store.name)
+    if bad:
+        sys.exit("bench: a rank's piece failed its checks (verified / fiber_codec)")
 
 
 def main():

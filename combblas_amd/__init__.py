@@ -114,7 +114,8 @@ class Context:
         _abi.check(self._lib.cbg_last_profile(self._ptr, ctypes.byref(p)), "cbg_last_profile")
         return {"flops_ms": p.flops_ms, "bin_ms": p.bin_ms, "symbolic_ms": p.symbolic_ms, "scan_ms": p.scan_ms,
                 "numeric_ms": p.numeric_ms, "total_ms": p.total_ms, "multiplies": p.multiplies,
-                "nnz_out": p.nnz_out, "bins": list(p.bins), "heavy_ms": p.heavy_ms, "known_items": p.known_items}
+                "nnz_out": p.nnz_out, "bins": list(p.bins), "heavy_ms": p.heavy_ms, "known_items": p.known_items,
+                "heavy_multiplies": p.heavy_multiplies, "heavy_nnz_b": p.heavy_nnz_b, "heavy_nnz_c": p.heavy_nnz_c}
 
     # raw ABI-level product (views in, device result out)
     def spgemm(self, A, B, sr, sort=True):
@@ -240,6 +241,14 @@ class SpDCCols:
                                                  ctypes.byref(res)), "cbg_col_select")
         return SpDCCols._from_result(self._ctx, res)
 
+    def fiber_codec(self, chunks=2):
+        """The 3D fiber exchange's wire codec on this matrix as one outgoing partial (cbg_fiber_codec): the bytes its
+        messages would put on the link and whether each chunk decodes back bit for bit."""
+        st = _abi.CodecStats()
+        _abi.check(self._ctx._lib.cbg_fiber_codec(self._ctx._ptr, ctypes.byref(self._res), int(chunks),
+                                                  ctypes.byref(st)), "cbg_fiber_codec")
+        return {k: getattr(st, k) for k, _ in _abi.CodecStats._fields_}
+
     def free(self):
         if self._res is not None and self._res._owner:
             self._ctx._lib.cbg_result_free(self._ctx._ptr, ctypes.byref(self._res))
@@ -306,6 +315,17 @@ def EstimateLocalFLOP(SR, A, B, clearA=False, clearB=False):
     _abi.check(ctx._lib.cbg_estimate(ctx._ptr, ctypes.byref(va), ctypes.byref(vb), ctypes.byref(m),
                                      ctypes.byref(z)), "cbg_estimate")
     return int(m.value)
+
+
+def EstimateLocalNNZ(A, B):
+    """(multiplies, nnz(A*B)) from the symbolic pass alone (estimateFLOP + estimateNNZ_Hash, mtSpGEMM.h:810-938,
+    1061-1139; exact on the device): no output is formed."""
+    ctx = A._ctx
+    m, z = ctypes.c_int64(0), ctypes.c_int64(0)
+    va, vb = A._view(), B._view()
+    _abi.check(ctx._lib.cbg_estimate(ctx._ptr, ctypes.byref(va), ctypes.byref(vb), ctypes.byref(m),
+                                     ctypes.byref(z)), "cbg_estimate")
+    return int(m.value), int(z.value)
 
 
 def MultiwayMerge(SR, lists, mdim=0, ndim=0, delarrs=False):

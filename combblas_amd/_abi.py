@@ -36,7 +36,8 @@ class Profile(ctypes.Structure):
     _fields_ = [("flops_ms", ctypes.c_double), ("bin_ms", ctypes.c_double), ("symbolic_ms", ctypes.c_double),
                 ("scan_ms", ctypes.c_double), ("numeric_ms", ctypes.c_double), ("total_ms", ctypes.c_double),
                 ("multiplies", ctypes.c_int64), ("nnz_out", ctypes.c_int64), ("bins", ctypes.c_int64 * 16),
-                ("heavy_ms", ctypes.c_double), ("known_items", ctypes.c_int64)]
+                ("heavy_ms", ctypes.c_double), ("known_items", ctypes.c_int64),
+                ("heavy_multiplies", ctypes.c_int64), ("heavy_nnz_b", ctypes.c_int64), ("heavy_nnz_c", ctypes.c_int64)]
 
 
 class HostCsc(ctypes.Structure):
@@ -53,7 +54,18 @@ class GridStats(ctypes.Structure):
     _fields_ = [("multiplies", ctypes.c_int64), ("bcast_bytes", ctypes.c_int64), ("fiber_bytes", ctypes.c_int64),
                 ("bcast_ms", ctypes.c_double), ("local_ms", ctypes.c_double), ("merge_ms", ctypes.c_double),
                 ("fiber_ms", ctypes.c_double), ("total_ms", ctypes.c_double), ("stages", ctypes.c_int32),
-                ("fiber_xfer_ms", ctypes.c_double)]
+                ("fiber_xfer_ms", ctypes.c_double),
+                ("heavy_ms", ctypes.c_double), ("heavy_multiplies", ctypes.c_int64), ("heavy_nnz_b", ctypes.c_int64),
+                ("heavy_nnz_c", ctypes.c_int64), ("local_nnz_out", ctypes.c_int64), ("local_nnz_b", ctypes.c_int64),
+                ("local_ncol_b", ctypes.c_int64), ("local_products", ctypes.c_int32)]
+
+
+class CodecStats(ctypes.Structure):
+    _fields_ = [("columns", ctypes.c_int64), ("entries", ctypes.c_int64), ("chunks", ctypes.c_int64),
+                ("header_bytes", ctypes.c_int64), ("row_bytes", ctypes.c_int64), ("escape_bytes", ctypes.c_int64),
+                ("value_bytes", ctypes.c_int64), ("value_header_bytes", ctypes.c_int64), ("wire_bytes", ctypes.c_int64),
+                ("row_formats", ctypes.c_int32), ("value_formats", ctypes.c_int32), ("roundtrip_exact", ctypes.c_int32),
+                ("mismatches", ctypes.c_int64), ("encode_ms", ctypes.c_double), ("decode_ms", ctypes.c_double)]
 
 
 # cbg_transport callbacks (include/cbgpu.h)
@@ -141,6 +153,8 @@ SIGNATURES = {
                                           ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]),
     "cbg_reduce_all": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(CscResult), ctypes.c_int32, ctypes.c_int,
                                       ctypes.c_int, ctypes.POINTER(CscResult), ctypes.POINTER(GridStats)]),
+    "cbg_fiber_codec": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(CscResult), ctypes.c_int32,
+                                       ctypes.POINTER(CodecStats)]),
 }
 
 _lib = None

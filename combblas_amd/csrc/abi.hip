@@ -90,12 +90,13 @@ cbg_status cbg_spgemm_local(cbg_ctx* ctx, const cbg_dcsc_view* A, const cbg_dcsc
 
 cbg_status cbg_estimate(cbg_ctx* ctx, const cbg_dcsc_view* A, const cbg_dcsc_view* B, int64_t* mults,
                         int64_t* nnzc) {
-  // symbolic == the first half of the product; run the pattern product and read its size
+  // the pattern product stopped after its symbolic pass and scan (kSymbolicOnly): exact multiplies and nnz(C),
+  // no output formed
   cbg_dcsc_view a = *A, b = *B;
   a.val = nullptr; b.val = nullptr;
   a.val_type = b.val_type = CBG_BOOL;
   cbg_csc_result C;
-  cbg_status s = cbg_spgemm_local(ctx, &a, &b, CBG_SR_PLUS_TIMES, CBG_BOOL, 0, &C, mults);
+  cbg_status s = cbg_spgemm_local(ctx, &a, &b, CBG_SR_PLUS_TIMES, CBG_BOOL, kSymbolicOnly, &C, mults);
   if (s != CBG_OK) return s;
   if (nnzc) *nnzc = C.nnz;
   cbg_result_free(ctx, &C);

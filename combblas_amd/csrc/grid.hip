@@ -347,6 +347,20 @@ __global__ void k_f32_to_f64(int64_t n, const float* __restrict__ in, double* __
     out[i] = (double)in[i];
 }
 
+// a local product's own profile (cbg_profile of the call just made) into the rank's sums
+void note_local(cbg_grid_stats* st, const cbg_ctx* ctx, const cbg_dcsc_view& vb) {
+  if (!st) return;
+  const cbg_profile& p = ctx->prof;
+  st->heavy_ms += p.heavy_ms;
+  st->heavy_multiplies += p.heavy_multiplies;
+  st->heavy_nnz_b += p.heavy_nnz_b;
+  st->heavy_nnz_c += p.heavy_nnz_c;
+  st->local_nnz_out += p.nnz_out;
+  st->local_nnz_b += vb.nnz;
+  st->local_ncol_b += vb.ncol;
+  ++st->local_products;
+}
+
 // device CSC piece (int64 colptr, int32 rows); storage owned by `own` unless borrowed
 struct Piece {
   int64_t nrow = 0, ncol = 0, nnz = 0;
@@ -857,6 +871,7 @@ cbg_status summa_layer_impl(cbg_grid* G, const cbg_dcsc_view* Av, const cbg_dcsc
       cbg_csc_result C;
       int64_t m = 0;
       CBGCHK(cbg_spgemm_local(ctx, &va, &vb, sr, dt, CBG_SORTED_COLS, &C, &m));
+      note_local(st, ctx, vb);
       if (st) { st->multiplies += m; st->local_ms += now_ms() - t0; st->stages += q; }
       Piece P = piece_of_result(C);
       parts->push_back(P);
@@ -958,6 +973,7 @@ cbg_status summa_layer_impl(cbg_grid* G, const cbg_dcsc_view* Av, const cbg_dcsc
     cbg_csc_result C;
     int64_t m = 0;
     CBGCHK(cbg_spgemm_local(ctx, &va, &vb, sr, dt, CBG_SORTED_COLS, &C, &m));
+    note_local(st, ctx, vb);
     if (async) {
       HIPCHK(hipEventRecord(G->ev_used[t & 1], cst));
       G->used_rec[t & 1] = true;
@@ -1133,6 +1149,7 @@ struct FiberMsg {
   int64_t E = 0, srow_b = 0, sesc_b = 0, sval_b = 0, svh_b = 0;
   const void* srow_p = nullptr;
   const void* sval_p = nullptr;
+  const void* svh_p = nullptr;                     // the value headers (varint values) or an empty stream
   PoolBuf cpv, shdr, sval, saux, svr, svv, sescoff, svroff, svvoff, srow, sesc;
   int64_t c0 = 0, mc = 0;                          // received: my columns [c0, c0 + mc)
   int rrfmt = 0, rvfmt = 0;
@@ -1144,6 +1161,166 @@ struct FiberMsg {
       b->pool = pl;
   }
 };
+
+// exclusive scan of n int64 counts (device) into out[0..n], the total into *total (device); `tiles` is reserved by the
+// caller once for the largest scan (growing a pool buffer would hand the old block back while kernels still use it)
+struct Scanner {
+  hipStream_t st = nullptr;
+  const PoolBuf* tiles = nullptr;
+  cbg_status operator()(int64_t n, const int64_t* in, int64_t* outp, int64_t* total) const {
+    const int64_t nt = (n + kScanTile - 1) / kScanTile;
+    if (8 * (nt + 1) > (int64_t)tiles->n) return CBG_EINVAL;
+    if (n > 0) {
+      k_scan_tiles<<<(int)nt, 256, 0, st>>>(n, in, tiles->as<int64_t>());
+      k_scan_sums<<<1, 1024, 0, st>>>(nt, tiles->as<int64_t>(), total);
+      k_scan_apply<<<(int)nt, 256, 0, st>>>(n, in, tiles->as<int64_t>(), outp);
+    } else {
+      HIPCHK(hipMemsetAsync(outp, 0, 8, st));
+      HIPCHK(hipMemsetAsync(total, 0, 8, st));
+    }
+    HIPCHK(hipGetLastError());
+    return CBG_OK;
+  }
+};
+
+struct CodecOpts {
+  bool gaps, narrow, var;
+};
+// CBG_FIBER_GAPS=0: int32 rows; CBG_FIBER_NARROW=0: native values; CBG_FIBER_VARINT=0: no varint codes
+const CodecOpts& codec_opts() {
+  static const CodecOpts o = [] {
+    auto on = [](const char* n) { const char* x = std::getenv(n); return !(x && x[0] == '0'); };
+    return CodecOpts{on("CBG_FIBER_GAPS"), on("CBG_FIBER_NARROW"), on("CBG_FIBER_VARINT")};
+  }();
+  return o;
+}
+
+// The sender's side of one fiber message (the partial m.P): one counting pass (k_code_count) gives the bytes of
+// every candidate form, the message takes the smallest lossless one for its rows and for its values, and the
+// encoders fill m's streams: column headers (count | aux << 32), rows, escapes, values, value headers.
+// dbad: 3 device counters, dtot: 3 device totals (scratch).  Synchronises the stream once (the totals).
+cbg_status fiber_encode(hipStream_t cst, const Scanner& scan, unsigned long long* dbad, int64_t* dtot, cbg_dtype dt,
+                        FiberMsg& m) {
+  const CodecOpts& opt = codec_opts();
+  const size_t vs = dt_size(dt);
+  const Piece& Po = m.P;
+  m.oc = Po.ncol;
+  m.n = Po.nnz;
+  const int64_t oc = m.oc, n = m.n;
+  const bool has_val = Po.val != nullptr;
+  const bool coded = opt.gaps && oc > 0 && n > 0;
+  const bool vcheck = opt.narrow && dt == CBG_F64 && has_val && vs == 8 && n > 0;
+  int64_t tot[3] = {0, 0, 0};
+  unsigned long long bad[3] = {0, 0, 0};
+  if (coded || vcheck) {
+    for (PoolBuf* pb : {&m.saux, &m.svr, &m.sescoff, &m.svroff}) HIPCHK(pb->reserve(8 * (oc + 1)));
+    if (vcheck) { HIPCHK(m.svv.reserve(8 * (oc + 1))); HIPCHK(m.svvoff.reserve(8 * (oc + 1))); }
+    HIPCHK(hipMemsetAsync(dbad, 0, 24, cst));
+    k_code_count<<<(int)grid_for(oc, 4, kMaxGrid * 2), 256, 0, cst>>>(
+        oc, Po.cp, Po.ir, vcheck ? (const double*)Po.val : nullptr, m.saux.as<int64_t>(), m.svr.as<int64_t>(),
+        vcheck ? m.svv.as<int64_t>() : nullptr, dbad);
+    HIPCHK(hipGetLastError());
+    CBGCHK(scan(oc, m.saux.as<int64_t>(), m.sescoff.as<int64_t>(), dtot + 0));
+    CBGCHK(scan(oc, m.svr.as<int64_t>(), m.svroff.as<int64_t>(), dtot + 1));
+    if (vcheck) CBGCHK(scan(oc, m.svv.as<int64_t>(), m.svvoff.as<int64_t>(), dtot + 2));
+    HIPCHK(hipMemcpyAsync(tot, dtot, 24, hipMemcpyDeviceToHost, cst));
+    HIPCHK(hipMemcpyAsync(bad, dbad, 24, hipMemcpyDeviceToHost, cst));
+    HIPCHK(hipStreamSynchronize(cst));
+  }
+  m.rfmt = m.vfmt = 0;
+  m.E = m.sesc_b = m.svh_b = 0;
+  m.srow_b = 4 * n;
+  if (coded && 2 * n + 4 * tot[0] < m.srow_b) { m.rfmt = 1; m.srow_b = 2 * n; m.sesc_b = 4 * tot[0]; m.E = tot[0]; }
+  if (coded && opt.var && tot[1] < m.srow_b + m.sesc_b) { m.rfmt = 2; m.srow_b = tot[1]; m.sesc_b = 0; m.E = 0; }
+  m.sval_b = has_val ? (int64_t)vs * n : 0;
+  if (vcheck && bad[0] == 0 && 4 * n < m.sval_b) { m.vfmt = 1; m.sval_b = 4 * n; }
+  if (vcheck && bad[1] == 0 && 2 * n < m.sval_b) { m.vfmt = 2; m.sval_b = 2 * n; }
+  if (vcheck && opt.var && bad[2] == 0 && tot[2] + 8 * oc < m.sval_b) { m.vfmt = 3; m.sval_b = tot[2]; m.svh_b = 8 * oc; }
+  m.srow_p = Po.ir;
+  if (m.rfmt == 1) {
+    HIPCHK(m.srow.reserve(m.srow_b + 16));
+    HIPCHK(m.sesc.reserve(m.sesc_b + 16));
+    k_gap_encode<<<(int)grid_for(oc, 4, kMaxGrid * 2), 256, 0, cst>>>(oc, Po.cp, Po.ir, m.sescoff.as<int64_t>(),
+                                                                      m.srow.as<unsigned short>(), m.sesc.as<int32_t>());
+    m.srow_p = m.srow.p;
+  } else if (m.rfmt == 2) {
+    HIPCHK(m.srow.reserve(m.srow_b + 16));
+    k_var_encode<0><<<(int)grid_for(oc, 4, kMaxGrid * 2), 256, 0, cst>>>(oc, Po.cp, Po.ir, nullptr,
+                                                                         m.svroff.as<int64_t>(), m.srow.as<uint8_t>());
+    m.srow_p = m.srow.p;
+  }
+  HIPCHK(m.sesc.reserve(16));   // a transport may be handed the escape buffers with zero bytes
+  HIPCHK(m.shdr.reserve(8 * (oc + 1)));
+  if (oc)
+    k_pack_hdr<<<(int)grid_for(oc, 256, kMaxGrid), 256, 0, cst>>>(
+        oc, Po.cp, m.rfmt == 1 ? m.saux.as<int64_t>() : m.rfmt == 2 ? m.svr.as<int64_t>() : nullptr,
+        m.shdr.as<int64_t>());
+  m.sval_p = Po.val;
+  if (m.vfmt) {
+    HIPCHK(m.sval.reserve(m.sval_b + 16));
+    if (m.vfmt == 1)
+      k_f64_to_f32<<<(int)grid_for(n, 256, kMaxGrid), 256, 0, cst>>>(n, (const double*)Po.val, m.sval.as<float>());
+    else if (m.vfmt == 2)
+      k_f64_to_u16<<<(int)grid_for(n, 256, kMaxGrid), 256, 0, cst>>>(n, (const double*)Po.val,
+                                                                    m.sval.as<unsigned short>());
+    else
+      k_var_encode<1><<<(int)grid_for(oc, 4, kMaxGrid * 2), 256, 0, cst>>>(oc, Po.cp, nullptr, (const double*)Po.val,
+                                                                           m.svvoff.as<int64_t>(), m.sval.as<uint8_t>());
+    m.sval_p = m.sval.p;
+  }
+  m.svh_p = m.vfmt == 3 ? (const void*)m.svv.p : (const void*)m.sesc.p;
+  HIPCHK(hipGetLastError());
+  return CBG_OK;
+}
+
+// The received streams of one message chunk (as the sender's fiber_encode made them).
+struct RecvStreams {
+  const void* rows;        // rrfmt 0: int32 rows, 1: u16 gaps, 2: varint gaps
+  const int32_t* esc;      // rrfmt 1: escaped absolute rows
+  const void* vals;        // rvfmt 0: native values, 1: f32, 2: u16, 3: varint integers
+  const int64_t* vhdr;     // rvfmt 3: the columns' value bytes
+};
+
+// The receiver's side of one message chunk: m.mc columns whose absolute entry offsets are ccp[0..mc] (a scan of the
+// received counts) and whose header aux (escapes / row bytes) is raux[0..mc); decodes rows into rir and values into
+// rv (native type, `vs` bytes) at entries [eoff, eoff + m.rnnz).  dtot_a / dtot_v: device scratch totals.
+cbg_status fiber_decode(hipStream_t cst, const Scanner& scan, int64_t* dtot_a, int64_t* dtot_v, size_t vs,
+                        bool has_val, FiberMsg& m, const RecvStreams& in, const int64_t* ccp, const int64_t* raux,
+                        int64_t eoff, int32_t* rir, char* rv) {
+  if (m.rrfmt) {
+    HIPCHK(m.rauxoff.reserve(8 * (m.mc + 1)));
+    CBGCHK(scan(m.mc, raux, m.rauxoff.as<int64_t>(), dtot_a));
+  }
+  if (m.rnnz) {
+    if (m.rrfmt == 0)
+      HIPCHK(hipMemcpyAsync(rir + eoff, in.rows, 4 * m.rnnz, hipMemcpyDeviceToDevice, cst));
+    else if (m.rrfmt == 1)
+      k_gap_decode<<<(int)grid_for(m.mc, 4, kMaxGrid * 2), 256, 0, cst>>>(m.mc, ccp, m.rauxoff.as<int64_t>(),
+                                                                           (const unsigned short*)in.rows, in.esc, rir,
+                                                                           eoff);
+    else
+      k_var_decode<0><<<(int)grid_for(m.mc, 4, kMaxGrid * 2), 256, 0, cst>>>(m.mc, ccp, m.rauxoff.as<int64_t>(),
+                                                                              (const uint8_t*)in.rows, rir, nullptr);
+    if (has_val) {
+      double* dv = (double*)rv;
+      if (m.rvfmt == 0)
+        HIPCHK(hipMemcpyAsync(rv + vs * eoff, in.vals, vs * m.rnnz, hipMemcpyDeviceToDevice, cst));
+      else if (m.rvfmt == 1)
+        k_f32_to_f64<<<(int)grid_for(m.rnnz, 256, kMaxGrid), 256, 0, cst>>>(m.rnnz, (const float*)in.vals, dv + eoff);
+      else if (m.rvfmt == 2)
+        k_u16_to_f64<<<(int)grid_for(m.rnnz, 256, kMaxGrid), 256, 0, cst>>>(m.rnnz, (const unsigned short*)in.vals,
+                                                                             dv + eoff);
+      else {
+        HIPCHK(m.rvoff.reserve(8 * (m.mc + 1)));
+        CBGCHK(scan(m.mc, in.vhdr, m.rvoff.as<int64_t>(), dtot_v));
+        k_var_decode<1><<<(int)grid_for(m.mc, 4, kMaxGrid * 2), 256, 0, cst>>>(m.mc, ccp, m.rvoff.as<int64_t>(),
+                                                                                (const uint8_t*)in.vals, nullptr, dv);
+      }
+    }
+  }
+  HIPCHK(hipGetLastError());
+  return CBG_OK;
+}
 
 // L = 2, plain product (reduce_all_impl's exchange-after-product, overlapped): the columns of the other layer's
 // part (block_range of the local columns, as fiber_exchange cuts them) are multiplied first, in C chunks of columns
@@ -1204,24 +1381,7 @@ cbg_status fiber_pipeline(cbg_grid* G, const cbg_dcsc_view& va, const cbg_dcsc_v
     v->val = vb.val ? (const void*)((const char*)vb.val + vs * e[0]) : nullptr;
     return CBG_OK;
   };
-  // exclusive scan of n int64 counts into out[0..n], the total into *total (device)
-  auto scan = [&](int64_t n, const int64_t* in, int64_t* outp, int64_t* total) -> cbg_status {
-    const int64_t nt = (n + kScanTile - 1) / kScanTile;
-    if (8 * (nt + 1) > (int64_t)tiles.n) return CBG_EINVAL;   // sized for the largest scan above
-    if (n > 0) {
-      k_scan_tiles<<<(int)nt, 256, 0, cst>>>(n, in, tiles.as<int64_t>());
-      k_scan_sums<<<1, 1024, 0, cst>>>(nt, tiles.as<int64_t>(), total);
-      k_scan_apply<<<(int)nt, 256, 0, cst>>>(n, in, tiles.as<int64_t>(), outp);
-    } else {
-      HIPCHK(hipMemsetAsync(outp, 0, 8, cst));
-      HIPCHK(hipMemsetAsync(total, 0, 8, cst));
-    }
-    HIPCHK(hipGetLastError());
-    return CBG_OK;
-  };
-  static const bool gaps_env = [] { const char* x = std::getenv("CBG_FIBER_GAPS"); return !(x && x[0] == '0'); }();
-  static const bool narrow_env = [] { const char* x = std::getenv("CBG_FIBER_NARROW"); return !(x && x[0] == '0'); }();
-  static const bool var_env = [] { const char* x = std::getenv("CBG_FIBER_VARINT"); return !(x && x[0] == '0'); }();
+  const Scanner scan{cst, &tiles};
   // RCCL's kernel needs 37.6 KB of LDS per workgroup (ncclDevKernel_Generic on gfx950) and cannot share a CU with the
   // persistent heavy grid (one 1024-thread workgroup holding 152.7 KB on every CU): while a transfer is in flight the
   // products leave CBG_FIBER_RESERVE_CU CUs to it (the heavy kernels take their work from a ticket, so a workgroup held
@@ -1245,6 +1405,7 @@ cbg_status fiber_pipeline(cbg_grid* G, const cbg_dcsc_view& va, const cbg_dcsc_v
     if (async && in_flight) ctx->reserve_cu = reserve_env;
     const cbg_status s = cbg_spgemm_local(ctx, &va, &vbx, sr, dt, CBG_SORTED_COLS, R, m);
     ctx->reserve_cu = 0;
+    if (s == CBG_OK) note_local(st, ctx, vbx);
     t_local += now_ms() - t0;
     return s;
   };
@@ -1262,70 +1423,9 @@ cbg_status fiber_pipeline(cbg_grid* G, const cbg_dcsc_view& va, const cbg_dcsc_v
     mults += mo;
     m.P = piece_of_result(Ro);
     const double t0 = now_ms();
-    const Piece& Po = m.P;
-    m.oc = Po.ncol;
-    m.n = Po.nnz;
+    CBGCHK(fiber_encode(cst, scan, (unsigned long long*)(dsn + 16), dtot, dt, m));
     const int64_t oc = m.oc, n = m.n;
-    const bool has_val = Po.val != nullptr;
-    const bool coded = gaps_env && oc > 0 && n > 0;
-    const bool vcheck = narrow_env && dt == CBG_F64 && has_val && vs == 8 && n > 0;
-    int64_t tot[3] = {0, 0, 0};
-    unsigned long long bad[3] = {0, 0, 0};
-    if (coded || vcheck) {
-      for (PoolBuf* pb : {&m.saux, &m.svr, &m.sescoff, &m.svroff}) HIPCHK(pb->reserve(8 * (oc + 1)));
-      if (vcheck) { HIPCHK(m.svv.reserve(8 * (oc + 1))); HIPCHK(m.svvoff.reserve(8 * (oc + 1))); }
-      HIPCHK(hipMemsetAsync(dsn + 16, 0, 24, cst));
-      k_code_count<<<(int)grid_for(oc, 4, kMaxGrid * 2), 256, 0, cst>>>(
-          oc, Po.cp, Po.ir, vcheck ? (const double*)Po.val : nullptr, m.saux.as<int64_t>(), m.svr.as<int64_t>(),
-          vcheck ? m.svv.as<int64_t>() : nullptr, (unsigned long long*)(dsn + 16));
-      HIPCHK(hipGetLastError());
-      CBGCHK(scan(oc, m.saux.as<int64_t>(), m.sescoff.as<int64_t>(), dtot + 0));
-      CBGCHK(scan(oc, m.svr.as<int64_t>(), m.svroff.as<int64_t>(), dtot + 1));
-      if (vcheck) CBGCHK(scan(oc, m.svv.as<int64_t>(), m.svvoff.as<int64_t>(), dtot + 2));
-      HIPCHK(hipMemcpyAsync(tot, dtot, 24, hipMemcpyDeviceToHost, cst));
-      HIPCHK(hipMemcpyAsync(bad, dsn + 16, 24, hipMemcpyDeviceToHost, cst));
-      HIPCHK(hipStreamSynchronize(cst));
-    }
-    m.srow_b = 4 * n;
-    if (coded && 2 * n + 4 * tot[0] < m.srow_b) { m.rfmt = 1; m.srow_b = 2 * n; m.sesc_b = 4 * tot[0]; m.E = tot[0]; }
-    if (coded && var_env && tot[1] < m.srow_b + m.sesc_b) { m.rfmt = 2; m.srow_b = tot[1]; m.sesc_b = 0; m.E = 0; }
-    m.sval_b = has_val ? (int64_t)vs * n : 0;
-    if (vcheck && bad[0] == 0 && 4 * n < m.sval_b) { m.vfmt = 1; m.sval_b = 4 * n; }
-    if (vcheck && bad[1] == 0 && 2 * n < m.sval_b) { m.vfmt = 2; m.sval_b = 2 * n; }
-    if (vcheck && var_env && bad[2] == 0 && tot[2] + 8 * oc < m.sval_b) { m.vfmt = 3; m.sval_b = tot[2]; m.svh_b = 8 * oc; }
-    m.srow_p = Po.ir;
-    if (m.rfmt == 1) {
-      HIPCHK(m.srow.reserve(m.srow_b + 16));
-      HIPCHK(m.sesc.reserve(m.sesc_b + 16));
-      k_gap_encode<<<(int)grid_for(oc, 4, kMaxGrid * 2), 256, 0, cst>>>(oc, Po.cp, Po.ir, m.sescoff.as<int64_t>(),
-                                                                        m.srow.as<unsigned short>(), m.sesc.as<int32_t>());
-      m.srow_p = m.srow.p;
-    } else if (m.rfmt == 2) {
-      HIPCHK(m.srow.reserve(m.srow_b + 16));
-      k_var_encode<0><<<(int)grid_for(oc, 4, kMaxGrid * 2), 256, 0, cst>>>(oc, Po.cp, Po.ir, nullptr,
-                                                                           m.svroff.as<int64_t>(), m.srow.as<uint8_t>());
-      m.srow_p = m.srow.p;
-    }
-    HIPCHK(m.sesc.reserve(16));   // a transport may be handed the escape buffers with zero bytes
-    HIPCHK(m.shdr.reserve(8 * (oc + 1)));
-    if (oc)
-      k_pack_hdr<<<(int)grid_for(oc, 256, kMaxGrid), 256, 0, cst>>>(
-          oc, Po.cp, m.rfmt == 1 ? m.saux.as<int64_t>() : m.rfmt == 2 ? m.svr.as<int64_t>() : nullptr,
-          m.shdr.as<int64_t>());
-    m.sval_p = Po.val;
-    if (m.vfmt) {
-      HIPCHK(m.sval.reserve(m.sval_b + 16));
-      if (m.vfmt == 1)
-        k_f64_to_f32<<<(int)grid_for(n, 256, kMaxGrid), 256, 0, cst>>>(n, (const double*)Po.val, m.sval.as<float>());
-      else if (m.vfmt == 2)
-        k_f64_to_u16<<<(int)grid_for(n, 256, kMaxGrid), 256, 0, cst>>>(n, (const double*)Po.val,
-                                                                      m.sval.as<unsigned short>());
-      else
-        k_var_encode<1><<<(int)grid_for(oc, 4, kMaxGrid * 2), 256, 0, cst>>>(oc, Po.cp, nullptr, (const double*)Po.val,
-                                                                             m.svvoff.as<int64_t>(), m.sval.as<uint8_t>());
-      m.sval_p = m.sval.p;
-    }
-    HIPCHK(hipGetLastError());
+    const bool has_val = m.P.val != nullptr;
     // the count exchange: [entries | rows format << 56 | values format << 58, escapes, row bytes, value bytes]
     int64_t sflag[8] = {0, 0, 0, 0, 0, 0, 0, 0}, rflag[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     sflag[4 * other + 0] = n | ((int64_t)m.rfmt << 56) | ((int64_t)m.vfmt << 58);
@@ -1353,7 +1453,7 @@ cbg_status fiber_pipeline(cbg_grid* G, const cbg_dcsc_view& va, const cbg_dcsc_v
     HIPCHK(m.rvbuf.reserve(m.rval_b + 16));
     HIPCHK(m.rvhdr.reserve(m.rvh_b + 16));
     if (st) st->fiber_bytes += 8 * oc + m.srow_b + m.sesc_b + (has_val ? m.sval_b + m.svh_b : 0);
-    const void* svh_p = m.vfmt == 3 ? (const void*)m.svv.p : (const void*)m.sesc.p;
+    const void* svh_p = m.svh_p;
     t_setup += now_ms() - t0;
     if (async) {
       HIPCHK(hipEventRecord(G->ev_t[0], cst));   // this chunk's headers and encoded streams are ready
@@ -1427,38 +1527,9 @@ cbg_status fiber_pipeline(cbg_grid* G, const cbg_dcsc_view& va, const cbg_dcsc_v
   for (auto& mp : msgs) {
     FiberMsg& m = *mp;
     const int64_t* ccp = co->cp.as<int64_t>() + m.c0;   // absolute entry offsets of the chunk's columns
-    if (m.rrfmt) {
-      HIPCHK(m.rauxoff.reserve(8 * (m.mc + 1)));
-      CBGCHK(scan(m.mc, raux.as<int64_t>() + m.c0, m.rauxoff.as<int64_t>(), dtot + 3));
-    }
-    if (m.rnnz) {
-      if (m.rrfmt == 0)
-        HIPCHK(hipMemcpyAsync(rir + eoff, m.rrow.p, 4 * m.rnnz, hipMemcpyDeviceToDevice, cst));
-      else if (m.rrfmt == 1)
-        k_gap_decode<<<(int)grid_for(m.mc, 4, kMaxGrid * 2), 256, 0, cst>>>(m.mc, ccp, m.rauxoff.as<int64_t>(),
-                                                                             m.rrow.as<unsigned short>(),
-                                                                             m.resc.as<int32_t>(), rir, eoff);
-      else
-        k_var_decode<0><<<(int)grid_for(m.mc, 4, kMaxGrid * 2), 256, 0, cst>>>(m.mc, ccp, m.rauxoff.as<int64_t>(),
-                                                                                m.rrow.as<uint8_t>(), rir, nullptr);
-      if (has_val) {
-        double* dv = (double*)rv;
-        if (m.rvfmt == 0)
-          HIPCHK(hipMemcpyAsync(rv + vs * eoff, m.rvbuf.p, vs * m.rnnz, hipMemcpyDeviceToDevice, cst));
-        else if (m.rvfmt == 1)
-          k_f32_to_f64<<<(int)grid_for(m.rnnz, 256, kMaxGrid), 256, 0, cst>>>(m.rnnz, m.rvbuf.as<float>(), dv + eoff);
-        else if (m.rvfmt == 2)
-          k_u16_to_f64<<<(int)grid_for(m.rnnz, 256, kMaxGrid), 256, 0, cst>>>(m.rnnz, m.rvbuf.as<unsigned short>(),
-                                                                               dv + eoff);
-        else {
-          HIPCHK(m.rvoff.reserve(8 * (m.mc + 1)));
-          CBGCHK(scan(m.mc, m.rvhdr.as<int64_t>(), m.rvoff.as<int64_t>(), dtot + 5));
-          k_var_decode<1><<<(int)grid_for(m.mc, 4, kMaxGrid * 2), 256, 0, cst>>>(m.mc, ccp, m.rvoff.as<int64_t>(),
-                                                                                  m.rvbuf.as<uint8_t>(), nullptr, dv);
-        }
-      }
-    }
-    HIPCHK(hipGetLastError());
+    const RecvStreams in{m.rrow.p, m.resc.as<int32_t>(), m.rvbuf.p, m.rvhdr.as<int64_t>()};
+    CBGCHK(fiber_decode(cst, scan, dtot + 3, dtot + 5, vs, has_val, m, in, ccp, raux.as<int64_t>() + m.c0, eoff, rir,
+                        rv));
     eoff += m.rnnz;
   }
   Piece Pr;
@@ -1487,6 +1558,17 @@ cbg_status fiber_pipeline(cbg_grid* G, const cbg_dcsc_view& va, const cbg_dcsc_v
     st->fiber_xfer_ms += xfer_ms;
   }
   return CBG_OK;
+}
+
+// entries where a and b differ (bit patterns), summed into *cnt
+template <typename T>
+__global__ void k_count_diff(int64_t n, const T* __restrict__ a, const T* __restrict__ b,
+                             unsigned long long* __restrict__ cnt) {
+  int64_t c = 0;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    c += a[i] != b[i];
+  c = wave_sum64(c);
+  if (lane_id() == 0 && c) atomicAdd(cnt, (unsigned long long)c);
 }
 
 // hand a piece out as a library result (move its storage when it owns it alone, else copy)
@@ -1742,6 +1824,103 @@ cbg_status cbg_spgemm_grid(cbg_grid* G, const cbg_dcsc_view* A, const cbg_dcsc_v
     CBGCHK(reduce_all_impl(G, ps, sr, dt, C, st));
   }
   if (st) st->total_ms = now_ms() - t0;
+  return CBG_OK;
+}
+
+// The production fiber codec on one partial, without a transport (include/cbgpu.h): the chunks the pipeline would
+// send, each encoded by fiber_encode and decoded by fiber_decode from the sender's own streams, then compared with
+// the source chunk bit for bit.
+cbg_status cbg_fiber_codec(cbg_ctx* ctx, const cbg_csc_result* P, int32_t chunks, cbg_codec_stats* out) {
+  if (!ctx || !P || !out || chunks < 1) return CBG_EINVAL;
+  if (P->nnz > 0 && (!P->colptr || !P->row)) return CBG_EINVAL;
+  memset(out, 0, sizeof(*out));
+  hipStream_t cst = ctx->stream;
+  const cbg_dtype dt = P->val_type;
+  const size_t vs = dt_size(dt);
+  const bool has_val = P->val != nullptr;
+  const int64_t ncol = P->ncol;
+  const int C = (int)std::max<int64_t>(1, std::min<int64_t>(chunks, ncol));
+  PoolBuf tiles, scal, cnt, hdr, raux, rcp, rbuf;
+  for (PoolBuf* b : {&tiles, &scal, &cnt, &hdr, &raux, &rcp, &rbuf}) b->pool = ctx->pool;
+  StreamFence fence(cst);
+  HIPCHK(tiles.reserve(8 * ((ncol + kScanTile - 1) / kScanTile + 2)));
+  HIPCHK(scal.reserve(128));
+  HIPCHK(cnt.reserve(64));
+  HIPCHK(hipMemsetAsync(cnt.p, 0, 64, cst));
+  int64_t* dtot = scal.as<int64_t>();
+  unsigned long long* dbad = (unsigned long long*)(dtot + 8);
+  unsigned long long* dmis = cnt.as<unsigned long long>();
+  const Scanner scan{cst, &tiles};
+  std::vector<int64_t> hcp(ncol + 1);
+  if (ncol >= 0) HIPCHK(hipMemcpyAsync(hcp.data(), P->colptr, 8 * (ncol + 1), hipMemcpyDeviceToHost, cst));
+  HIPCHK(hipStreamSynchronize(cst));
+  out->columns = ncol;
+  out->entries = P->nnz;
+  out->chunks = C;
+  hipEvent_t e0 = ctx->ev[0], e1 = ctx->ev[1], e2 = ctx->ev[2];
+  double enc_ms = 0, dec_ms = 0;
+  for (int c = 0; c < C; ++c) {
+    const int64_t a = (ncol / C) * c, b = c == C - 1 ? ncol : a + ncol / C, oc = b - a;
+    FiberMsg m(ctx->pool);
+    HIPCHK(m.cpv.reserve(8 * (oc + 1)));
+    k_cp_rebase<<<(int)grid_for(oc + 1, 256, kMaxGrid), 256, 0, cst>>>(oc, P->colptr + a, 0, m.cpv.as<int64_t>());
+    HIPCHK(hipGetLastError());
+    const int64_t e_0 = hcp[a], n = hcp[b] - hcp[a];
+    m.P.nrow = P->nrow; m.P.ncol = oc; m.P.nnz = n;
+    m.P.cp = m.cpv.as<int64_t>();
+    m.P.ir = P->row + e_0;
+    m.P.val = has_val ? (const void*)((const char*)P->val + vs * e_0) : nullptr;
+    HIPCHK(hipEventRecord(e0, cst));
+    CBGCHK(fiber_encode(cst, scan, dbad, dtot, dt, m));
+    HIPCHK(hipEventRecord(e1, cst));
+    out->header_bytes += 8 * oc;
+    out->row_bytes += m.srow_b;
+    out->escape_bytes += m.sesc_b;
+    if (has_val) { out->value_bytes += m.sval_b; out->value_header_bytes += m.svh_b; }
+    if (n > 0) { out->row_formats |= 1 << m.rfmt; if (has_val) out->value_formats |= 1 << m.vfmt; }
+    // the receiver's view of the same bytes: the headers split into counts + aux, the colptr a scan of the counts
+    HIPCHK(hdr.reserve(8 * (oc + 1)));
+    HIPCHK(raux.reserve(8 * (oc + 1)));
+    HIPCHK(rcp.reserve(8 * (oc + 2)));
+    const int64_t ir_bytes = (4 * n + 15) & ~15LL;
+    HIPCHK(rbuf.reserve(ir_bytes + vs * n + 16));
+    if (oc) HIPCHK(hipMemcpyAsync(hdr.p, m.shdr.p, 8 * oc, hipMemcpyDeviceToDevice, cst));
+    if (oc) k_split_hdr<<<(int)grid_for(oc, 256, kMaxGrid), 256, 0, cst>>>(oc, hdr.as<int64_t>(), raux.as<int64_t>());
+    CBGCHK(scan(oc, hdr.as<int64_t>(), rcp.as<int64_t>(), dtot + 4));
+    m.rrfmt = m.rfmt; m.rvfmt = m.vfmt; m.rnnz = n; m.rE = m.E; m.mc = oc; m.c0 = 0;
+    const RecvStreams in{m.srow_p, m.sesc.as<int32_t>(), m.sval_p, (const int64_t*)m.svh_p};
+    int32_t* rir = rbuf.as<int32_t>();
+    char* rv = rbuf.as<char>() + ir_bytes;
+    CBGCHK(fiber_decode(cst, scan, dtot + 5, dtot + 6, vs, has_val, m, in, rcp.as<int64_t>(), raux.as<int64_t>(), 0,
+                        rir, rv));
+    HIPCHK(hipEventRecord(e2, cst));
+    k_count_diff<int64_t><<<(int)grid_for(oc + 1, 256, kMaxGrid), 256, 0, cst>>>(oc + 1, rcp.as<int64_t>(),
+                                                                                m.cpv.as<int64_t>(), dmis);
+    if (n) {
+      k_count_diff<int32_t><<<(int)grid_for(n, 256, kMaxGrid), 256, 0, cst>>>(n, rir, m.P.ir, dmis);
+      if (has_val && vs == 8)
+        k_count_diff<uint64_t><<<(int)grid_for(n, 256, kMaxGrid), 256, 0, cst>>>(n, (const uint64_t*)rv,
+                                                                                (const uint64_t*)m.P.val, dmis);
+      else if (has_val && vs == 4)
+        k_count_diff<uint32_t><<<(int)grid_for(n, 256, kMaxGrid), 256, 0, cst>>>(n, (const uint32_t*)rv,
+                                                                                (const uint32_t*)m.P.val, dmis);
+      else if (has_val)
+        k_count_diff<uint8_t><<<(int)grid_for(n, 256, kMaxGrid), 256, 0, cst>>>(n, (const uint8_t*)rv,
+                                                                               (const uint8_t*)m.P.val, dmis);
+    }
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(cst));   // m's buffers go back to the pool at the end of the iteration
+    float t = 0.f;
+    (void)hipEventElapsedTime(&t, e0, e1); enc_ms += t;
+    (void)hipEventElapsedTime(&t, e1, e2); dec_ms += t;
+  }
+  unsigned long long mis = 0;
+  HIPCHK(hipMemcpy(&mis, dmis, 8, hipMemcpyDeviceToHost));
+  out->mismatches = (int64_t)mis;
+  out->roundtrip_exact = mis == 0;
+  out->wire_bytes = out->header_bytes + out->row_bytes + out->escape_bytes + out->value_bytes + out->value_header_bytes;
+  out->encode_ms = enc_ms;
+  out->decode_ms = dec_ms;
   return CBG_OK;
 }
 

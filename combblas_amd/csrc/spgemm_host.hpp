@@ -34,6 +34,17 @@ using namespace cbg;
     if (s_ != CBG_OK) return s_; \
   } while (0)
 
+// refuse a phase's launches when a workspace buffer it captured was reallocated since (Captures)
+#define CAPCHK(c)                                                                                            \
+  do {                                                                                                       \
+    const char* w_ = "?";                                                                                    \
+    if (!(c).ok(&w_)) {                                                                                      \
+      fprintf(stderr, "cbgpu: workspace '%s' reallocated after its pointer was taken (%s:%d)\n", w_, __FILE__, \
+              __LINE__);                                                                                     \
+      return CBG_EINVAL;                                                                                     \
+    }                                                                                                        \
+  } while (0)
+
 namespace cbg { namespace host {
 
 // symbolic classes: wave T = 64..1024 words, block T = 2048..32768 words, then window
@@ -43,13 +54,21 @@ constexpr int kNumWave = 4, kNumBlock = 4;
 constexpr int kBlockNT = 512;
 constexpr int kWinNT = 256;
 constexpr int kMaxGrid = 4096;
+// library-internal flag of spgemm_impl: stop after the symbolic pass and the scan (cbg_estimate): the result holds the
+// colptr only, nnz(C) and the multiplies are exact, no output is allocated or computed
+constexpr uint32_t kSymbolicOnly = 1u << 28;
 
+// Grow-only buffers.  `gen` counts reallocations: a pointer taken with as<T>() is stale once gen moves (the old block
+// is freed, or handed back to the pool while kernels queued on the stream may still use it).  Captures records the
+// generations of the buffers a phase's launches were given and check() refuses to launch after any of them moved.
 struct DevBuf {
   void* p = nullptr;
   size_t n = 0;
+  uint32_t gen = 0;
   ~DevBuf() { if (p) (void)hipFree(p); }
   hipError_t reserve(size_t bytes) {
     if (bytes <= n) return hipSuccess;
+    ++gen;
     if (p) { (void)hipFree(p); p = nullptr; n = 0; }
     hipError_t e = hipMalloc(&p, bytes ? bytes : 16);
     if (e == hipSuccess) n = bytes;
@@ -60,6 +79,7 @@ struct DevBuf {
     if (p) (void)hipFree(p);
     p = nullptr;
     n = 0;
+    ++gen;
   }
 };
 
@@ -108,13 +128,28 @@ struct PoolBuf {
   std::shared_ptr<Pool> pool;
   void* p = nullptr;
   size_t n = 0;
+  uint32_t gen = 0;
   ~PoolBuf() { if (p) pool->put(p, n); }
   hipError_t reserve(size_t bytes) {
     if (bytes <= n) return hipSuccess;
+    ++gen;
     if (p) { pool->put(p, n); p = nullptr; n = 0; }
     return pool->get(bytes ? bytes : 16, &p, &n);
   }
   template <typename T> T* as() const { return (T*)p; }
+};
+
+// Generations of the buffers whose pointers a phase captured; check() before the phase's launches.  A moved buffer
+// is a host-side bug (a reserve after the capture): refuse the launch instead of handing kernels a freed block.
+struct Captures {
+  struct Ent { const uint32_t* gen; uint32_t at; const char* what; };
+  std::vector<Ent> v;
+  template <class Buf> void add(const Buf& b, const char* what) { v.push_back(Ent{&b.gen, b.gen, what}); }
+  bool ok(const char** which = nullptr) const {
+    for (const Ent& e : v)
+      if (*e.gen != e.at) { if (which) *which = e.what; return false; }
+    return true;
+  }
 };
 
 // Synchronises the given streams when it goes out of scope.  Declared after the pool buffers that kernels or
@@ -447,7 +482,8 @@ hipError_t launch_numeric_classes(hipStream_t st, const Classes& cl, const int32
 template <class SRT, typename V>
 cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_view* Bv, uint32_t flags,
                        cbg_csc_result* C, int64_t* mult_out) {
-  (void)flags;   // output columns are always row-sorted (sorting is free in the compaction)
+  // output columns are always row-sorted (sorting is free in the compaction); kSymbolicOnly: cbg_estimate
+  const bool symbolic_only = (flags & kSymbolicOnly) != 0;
   hipStream_t st = ctx->stream;
   cbg_profile& pf = ctx->prof;
   memset(&pf, 0, sizeof(pf));
@@ -492,22 +528,26 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
   HIPCHK(ctx->cnt.reserve(sizeof(int64_t) * (N + 1)));
   HIPCHK(ctx->list.reserve(sizeof(int32_t) * (N + 1)));
   HIPCHK(ctx->hist.reserve(sizeof(unsigned long long) * 256));
-  HIPCHK(ctx->scalars.reserve(128));
+  HIPCHK(ctx->scalars.reserve(256));
   HIPCHK(ctx->ovf_list.reserve(sizeof(int32_t) * (N + 1)));
   HIPCHK(ctx->split_idx.reserve(sizeof(int32_t) * (A.ncol + 1)));
   HIPCHK(ctx->long_cols.reserve(sizeof(int32_t) * (A.ncol + 1)));
+  Captures cap;   // every workspace pointer below is taken after its buffer's last reserve; CAPCHK before launches
+  cap.add(ctx->flop, "flop"); cap.add(ctx->span, "span"); cap.add(ctx->cnt, "cnt"); cap.add(ctx->list, "list");
+  cap.add(ctx->hist, "hist"); cap.add(ctx->scalars, "scalars"); cap.add(ctx->ovf_list, "ovf_list");
+  cap.add(ctx->split_idx, "split_idx"); cap.add(ctx->long_cols, "long_cols");
   int64_t* flop = ctx->flop.as<int64_t>();
   int2* span = ctx->span.as<int2>();
   int64_t* nnz = ctx->cnt.as<int64_t>();
   int32_t* list = ctx->list.as<int32_t>();
   unsigned long long* hist = ctx->hist.as<unsigned long long>();
   // scalars: [0] multiplies, [1] nnz(C); ints from byte 16: heavy n, nlong, adderr, col ovf, unit ovf,
-  // fallback units, fallback-unit ovf
+  // fallback units, fallback-unit ovf; [16..18] heavy multiplies, B nonzeros, outputs (k_heavy_sums)
   unsigned long long* sc = ctx->scalars.as<unsigned long long>();
   int* si = (int*)(sc + 2);
   int *heavy_n = si + 0, *nlong = si + 1, *adderr = si + 2, *ovf_n = si + 3, *uovf_n = si + 4, *fb_n = si + 5,
       *fb_ovf_n = si + 6;
-  HIPCHK(hipMemsetAsync(sc, 0, 128, st));
+  HIPCHK(hipMemsetAsync(sc, 0, 256, st));
   HIPCHK(hipMemsetAsync(nnz, 0, sizeof(int64_t) * N, st));
   {
     const int64_t avg = N > 0 ? (B.nnz + N - 1) / N : 0;   // lanes per column ~ the mean B column length
@@ -537,6 +577,7 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
   const int64_t hcap = (int64_t)cs.hist[31];
   HIPCHK(ctx->heavy_cols.reserve(sizeof(int32_t) * (hcap + 1)));
   HIPCHK(ctx->sub.reserve(sizeof(int32_t) * (hcap * nsub + 1)));
+  cap.add(ctx->heavy_cols, "heavy_cols"); cap.add(ctx->sub, "sub");
   HeavyOut ho{heavy_n, ctx->heavy_cols.as<int32_t>(), ctx->sub.as<int32_t>(), nsub, slog,
               nullptr, nullptr, 0, nullptr, nullptr};
   // row handoff: scratch for the heavy columns' sorted rows, sized by the bound sum(min(flop, span))
@@ -546,7 +587,7 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
     ctx->row_handoff = (e && e[0] == '0') ? 0 : 1;
   }
   const unsigned long long hbound = hh[42];
-  if (ctx->row_handoff && hcap > 0 && hbound > 0 && !SRT::kAddIsError) {
+  if (ctx->row_handoff && hcap > 0 && hbound > 0 && !SRT::kAddIsError && !symbolic_only) {
     size_t fr = 0, tot = 0;
     HIPCHK(hipMemGetInfo(&fr, &tot));
     const size_t need = sizeof(int32_t) * (hbound + 1);
@@ -560,6 +601,7 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
       ho.cap = hbound;
       ho.poff = ctx->hpoff.as<int64_t>();
       ho.mode = ctx->hmode.as<int32_t>();
+      cap.add(ctx->hrows, "hrows"); cap.add(ctx->hmode, "hmode"); cap.add(ctx->hpoff, "hpoff");
     }
   }
   // split table (unit segments, wide-column parts): needed whenever a column can be heavy
@@ -567,11 +609,13 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
   if (hcap > 0) {
     HIPCHK(ctx->split_tab.reserve(sizeof(int32_t) * ((int64_t)NL * (nsub + 1) + 1)));
     spl.tab = ctx->split_tab.as<int32_t>();
+    cap.add(ctx->split_tab, "split_tab");
     if (NL > 0)
       k_split_fill<<<(int)grid_for(NL, 4, kMaxGrid * 2), 256, 0, st>>>(NL, ctx->long_cols.as<int32_t>(), A.cp, A.ir,
                                                                         ctx->split_tab.as<int32_t>(), nsub, slog);
   }
   HIPCHK(hipEventRecord(ctx->ev[2], st));
+  CAPCHK(cap);
   {
     auto L = [&](int c) { return list + cs.off[c]; };
     auto n = [&](int c) { return (int64_t)cs.hist[c]; };
@@ -597,6 +641,8 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
     if (nwide && e == hipSuccess) {
       HIPCHK(ctx->parts.reserve(sizeof(PartItem) * (nwide * kMaxParts + 1)));
       HIPCHK(ctx->wide_win.reserve(sizeof(int32_t) * (nwide + 1)));
+      cap.add(ctx->parts, "parts"); cap.add(ctx->wide_win, "wide_win");
+      CAPCHK(cap);
       int *nparts = si + 8, *nwin = si + 9;
       k_part_items<<<(int)grid_for(nwide, 256, kMaxGrid), 256, 0, st>>>(L(kWideClass), nwide, slog <= kPartLog ? kMaxParts : 0, span, ho,
                                                                          ctx->parts.as<PartItem>(), nparts,
@@ -607,6 +653,7 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
       if (nw_cap && e == hipSuccess) {
         HIPCHK(ctx->cur.reserve(sizeof(int64_t) * (B.nnz + 1)));
         HIPCHK(ctx->nxt.reserve(sizeof(int32_t) * (B.nnz + 1)));
+        CAPCHK(cap);
         e = launch_window<0, SRT, V, kSymWinRows>(st, ctx->wide_win.as<int32_t>(), nwin, nw_cap,
                                                   grid_for(nw_cap, 1, 1024), A, B, span, nullptr,
                                                   ctx->cur.as<int64_t>(), ctx->nxt.as<int32_t>(), nnz, ho,
@@ -621,6 +668,8 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
   // 3. scan -> colptr, nnz(C)
   const int64_t ntiles = (N + kScanTile - 1) / kScanTile;
   HIPCHK(ctx->scan_tiles.reserve(sizeof(int64_t) * (ntiles + 1)));
+  cap.add(ctx->scan_tiles, "scan_tiles");
+  CAPCHK(cap);
   k_scan_tiles<<<(int)ntiles, 256, 0, st>>>(N, nnz, ctx->scan_tiles.as<int64_t>());
   k_scan_sums<<<1, 1024, 0, st>>>(ntiles, ctx->scan_tiles.as<int64_t>(), (int64_t*)(sc + 1));
   k_scan_apply<<<(int)ntiles, 256, 0, st>>>(N, nnz, ctx->scan_tiles.as<int64_t>(), colptr);
@@ -632,6 +681,27 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
   const int64_t mults = (int64_t)hsc[0], nnzc = (int64_t)hsc[1];
   const int H = ((int*)&hsc[2])[0];
   pf.multiplies = mults; pf.nnz_out = nnzc;
+  if (symbolic_only) {
+    HIPCHK(own->ir.reserve(4));
+    HIPCHK(own->val.reserve(8));
+    float t;
+    (void)hipEventElapsedTime(&t, ctx->ev[0], ctx->ev[1]); pf.flops_ms = t;
+    (void)hipEventElapsedTime(&t, ctx->ev[1], ctx->ev[2]); pf.bin_ms = t;
+    (void)hipEventElapsedTime(&t, ctx->ev[2], ctx->ev[3]); pf.symbolic_ms = t;
+    (void)hipEventElapsedTime(&t, ctx->ev[3], ctx->ev[4]); pf.scan_ms = t;
+    (void)hipEventElapsedTime(&t, ctx->ev[0], ctx->ev[4]); pf.total_ms = t;
+    C->nnz = nnzc;
+    C->colptr = colptr;
+    C->row = own->ir.as<int32_t>();
+    C->val = own->val.p;
+    C->multiplies = mults;
+    C->_owner = own.release();
+    if (mult_out) *mult_out = mults;
+    return CBG_OK;
+  }
+  // what the heavy kernels will process (listed columns with nnz > kHeavy): sc[16..18], read back with the errors
+  if (H > 0)
+    k_heavy_sums<<<(int)grid_for(H, 256, 1024), 256, 0, st>>>(H, ctx->heavy_cols.as<int32_t>(), flop, nnz, B.cp, sc + 16);
   HIPCHK(own->ir.reserve(sizeof(int32_t) * (nnzc + 1)));
   HIPCHK(own->val.reserve(sizeof(V) * (nnzc + 1)));
 
@@ -654,6 +724,10 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
     HIPCHK(ctx->icnt.reserve(sizeof(int64_t) * (H + 1)));
     HIPCHK(ctx->itemoff.reserve(sizeof(int64_t) * (H + 1)));
     if (ho.rows) HIPCHK(ctx->urows.reserve(sizeof(UnitRows) * (nunit_cap + 1)));
+    for (DevBuf* b : {&ctx->units, &ctx->ucnt, &ctx->uspan, &ctx->ulist, &ctx->fb_units, &ctx->fb_list, &ctx->uovf_list,
+                      &ctx->nunits, &ctx->segsz, &ctx->segoff, &ctx->icnt, &ctx->itemoff, &ctx->urows})
+      cap.add(*b, "heavy units");
+    CAPCHK(cap);
     k_build_units<<<(H + 255) / 256, 256, 0, st>>>(H, ctx->heavy_cols.as<int32_t>(), ctx->sub.as<int32_t>(), nsub,
                                                    slog, heavy_unit_cap<SRT>(), heavy_span_cap<SRT>(), span,
                                                    colptr, B.cp, units, ctx->ucnt.as<int64_t>(),
@@ -693,6 +767,7 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
   if (H > 0) {
     HIPCHK(ctx->useg.reserve(sizeof(UnitSeg) * (segtot + 1)));
     spl.useg = ctx->useg.as<UnitSeg>();
+    cap.add(ctx->useg, "useg");
     k_unit_segs<SRT, CBG_KNOWN_LOGT, CBG_KNOWN_NT><<<H, 256, 0, st>>>(
         ctx->heavy_cols.as<int32_t>(), ctx->nunits.as<int32_t>(), ctx->segoff.as<int64_t>(), units, nsub, A.cp, A.ir,
         B.cp, B.ir, spl, ctx->useg.as<UnitSeg>(), ctx->uspan.as<int2>());
@@ -700,6 +775,8 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
     const int64_t ucap = nitems * kItemUnits + 1;
     HIPCHK(ctx->items.reserve(sizeof(KnownUnit) * ucap));
     HIPCHK(ctx->oitems.reserve(sizeof(HeavyItem) * ucap));
+    cap.add(ctx->items, "items"); cap.add(ctx->oitems, "oitems");
+    CAPCHK(cap);
     k_heavy_items_split<SRT, CBG_KNOWN_LOGT, CBG_KNOWN_NT><<<(H + 255) / 256, 256, 0, st>>>(
         H, ctx->heavy_cols.as<int32_t>(), ctx->nunits.as<int32_t>(), units, nsub, ctx->uspan.as<int2>(), spl.urows,
         B.cp, ctx->items.as<KnownUnit>(), ctx->oitems.as<HeavyItem>(), sc + 12);
@@ -714,6 +791,7 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
   pf.bins[12] = H;
   pf.bins[13] = nitems;
   NumOut<V> oc{own->ir.as<int32_t>(), own->val.as<V>(), adderr, ovf_n, ctx->ovf_list.as<int32_t>()};
+  CAPCHK(cap);
   {
     hipError_t e = launch_numeric_classes<SRT, V, false>(st, cn, list, nullptr, A, B, span, colptr, spl, oc);
     if (e == hipSuccess && H > 0) {
@@ -749,6 +827,7 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
           arv = ctx->aos.as<RowVal<V>>();
         }
       }
+      CAPCHK(cap);
       // tickets of the persistent kernels: sc[14], sc[15] (zeroed with the scalars)
       e = launch_num_heavy_known<CBG_KNOWN_LOGT, CBG_KNOWN_NT, SRT, V>(st, grid, ctx->items.as<KnownUnit>(), sc + 12,
                                                                      A, B, spl, ou, sc + 14, arv);
@@ -771,6 +850,7 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
     if (e == hipSuccess) {
       HIPCHK(ctx->cur.reserve(sizeof(int64_t) * (B.nnz + 1)));
       HIPCHK(ctx->nxt.reserve(sizeof(int32_t) * (B.nnz + 1)));
+      CAPCHK(cap);
       e = launch_window<1, SRT, V, kWinRows>(st, ctx->ovf_list.as<int32_t>(), ovf_n, 0, 512, A, B, span, colptr,
                                              ctx->cur.as<int64_t>(), ctx->nxt.as<int32_t>(), nnz, ho, oc);
     }
@@ -780,9 +860,12 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
   HIPCHK(hipEventRecord(ctx->ev[5], st));
   int* herr = pinned<int>(ctx, kPinErr);   // 8 ints, then the rows-known unit count
   unsigned long long& hknown = *pinned<unsigned long long>(ctx, kPinErr + 32);
+  unsigned long long* hsum = pinned<unsigned long long>(ctx, kPinErr + 40);   // 3 entries
   hknown = 0;
+  hsum[0] = hsum[1] = hsum[2] = 0;
   HIPCHK(hipMemcpyAsync(herr, si, 8 * sizeof(int), hipMemcpyDeviceToHost, st));
   if (H > 0) HIPCHK(hipMemcpyAsync(&hknown, sc + 12, sizeof(hknown), hipMemcpyDeviceToHost, st));
+  if (H > 0) HIPCHK(hipMemcpyAsync(hsum, sc + 16, 3 * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
   float t;
   (void)hipEventElapsedTime(&t, ctx->ev[0], ctx->ev[1]); pf.flops_ms = t;
@@ -793,6 +876,9 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
   (void)hipEventElapsedTime(&t, ctx->ev[0], ctx->ev[5]); pf.total_ms = t;
   if (H > 0) { (void)hipEventElapsedTime(&t, ctx->ev[6], ctx->ev[7]); pf.heavy_ms = t; }
   pf.known_items = (int64_t)hknown;
+  pf.heavy_multiplies = (int64_t)hsum[0];
+  pf.heavy_nnz_b = (int64_t)hsum[1];
+  pf.heavy_nnz_c = (int64_t)hsum[2];
   pf.bins[14] = herr[4];   // overflowed units (re-run dense per subwindow)
   pf.bins[15] = herr[3];   // overflowed columns (windowed fallback)
   C->nnz = nnzc;

@@ -1364,6 +1364,31 @@ constexpr int64_t heavy_span_cap() {
   return CBG_RANK_SPAN_CAP < cap ? CBG_RANK_SPAN_CAP : cap;
 }
 
+// what the heavy kernels process (columns with nnz > kHeavy): multiplies, B nonzeros and outputs, summed into
+// out[0..2] -- the per-unit figures of SURVEY 8(d)'s algorithmic bytes of the dominant kernels (cbg_profile)
+__global__ void __launch_bounds__(256) k_heavy_sums(int H, const int32_t* __restrict__ cols,
+                                                    const int64_t* __restrict__ flop, const int64_t* __restrict__ nnz,
+                                                    const int64_t* __restrict__ Bcp, unsigned long long* __restrict__ out) {
+  int64_t f = 0, b = 0, c = 0;
+  for (int h = blockIdx.x * blockDim.x + threadIdx.x; h < H; h += gridDim.x * blockDim.x) {
+    const int32_t j = cols[h];
+    const int64_t z = nnz[j];
+    if (z > kHeavy) {
+      f += flop[j];
+      b += Bcp[j + 1] - Bcp[j];
+      c += z;
+    }
+  }
+  f = wave_sum64(f);
+  b = wave_sum64(b);
+  c = wave_sum64(c);
+  if (lane_id() == 0 && (f | b | c)) {
+    atomicAdd(out + 0, (unsigned long long)f);
+    atomicAdd(out + 1, (unsigned long long)b);
+    atomicAdd(out + 2, (unsigned long long)c);
+  }
+}
+
 // units of a heavy column: consecutive subwindows while the running count stays <= unit_cap
 // unit_cap / span_cap come from the semiring (heavy_unit_caps): rank-mode accumulators hold up to
 // kUnitCap outputs over a bounded span; hash-only semirings (BoolCopy) keep load <= 1/2.

@@ -1063,6 +1063,11 @@ def _stats_update(stats, st):
               "fiber_xfer_ms"):
         stats[k] = stats.get(k, 0) + getattr(st, k)
     stats["stages"] = stats.get("stages", 0) + int(st.stages)
+    for k in ("heavy_ms",):
+        stats[k] = stats.get(k, 0.0) + float(getattr(st, k))
+    for k in ("heavy_multiplies", "heavy_nnz_b", "heavy_nnz_c", "local_nnz_out", "local_nnz_b", "local_ncol_b",
+              "local_products"):
+        stats[k] = stats.get(k, 0) + int(getattr(st, k))
 
 
 class GpuBackend:
@@ -1210,6 +1215,22 @@ class GpuBackend:
                                                 ctypes.byref(st)), "cbg_reduce_all")
         _stats_update(stats, st)
         return self._take(res)
+
+    def estimate(self, A, B):
+        """(multiplies, nnz(C)) of A*B from the symbolic pass alone (cbg_estimate: estimateFLOP + exact nnz)."""
+        va, vb = self._view(A), self._view(B)
+        f, z = ctypes.c_int64(0), ctypes.c_int64(0)
+        _abi.check(self.ctx._lib.cbg_estimate(self.ctx._ptr, ctypes.byref(va), ctypes.byref(vb), ctypes.byref(f),
+                                              ctypes.byref(z)), "cbg_estimate")
+        return int(f.value), int(z.value)
+
+    def fiber_codec(self, P, chunks=2):
+        """The production fiber encoder + decoder on partial P (cbg_fiber_codec): wire bytes per part and whether
+        every chunk round-trips bit for bit."""
+        st = _abi.CodecStats()
+        _abi.check(self.ctx._lib.cbg_fiber_codec(self.ctx._ptr, ctypes.byref(self._res_view(P)), int(chunks),
+                                                 ctypes.byref(st)), "cbg_fiber_codec")
+        return {k: getattr(st, k) for k, _ in _abi.CodecStats._fields_}
 
     def merge(self, parts, sr):
         arr = (_abi.CscResult * len(parts))(*[self._res_view(p) for p in parts])

@@ -51,7 +51,9 @@
 extern "C" {
 #endif
 
-#define CBG_ABI_VERSION 2   /* 2: cbg_grid_stats.fiber_xfer_ms after stages; cbg_device_count */
+#define CBG_ABI_VERSION 3   /* 2: cbg_grid_stats.fiber_xfer_ms after stages; cbg_device_count
+                               3: cbg_profile heavy_* counts; cbg_grid_stats heavy / local-product sums;
+                                  cbg_fiber_codec */
 
 typedef enum {
   CBG_OK = 0,
@@ -117,6 +119,9 @@ typedef struct {
   int64_t multiplies, nnz_out, bins[16];
   double heavy_ms;      /* k_num_heavy_known + k_num_heavy (heavy-column units), HIP events on the context stream */
   int64_t known_items;  /* heavy units whose rows came from the symbolic pass (k_num_heavy_known) */
+  /* ABI 3: what the heavy kernels processed (columns with nnz(C(:,j)) > 4096): multiplies, B nonzeros, outputs --
+   * the per-unit counts of SURVEY 8(d)'s algorithmic bytes of the dominant kernels */
+  int64_t heavy_multiplies, heavy_nnz_b, heavy_nnz_c;
 } cbg_profile;
 
 int32_t     cbg_abi_version(void);
@@ -306,6 +311,12 @@ typedef struct {
   int32_t stages;
   /* ABI 2: fields after `stages` (callers built against ABI 1 never read past it) */
   double fiber_xfer_ms;        /* two layers: the fiber transfer on the communication stream (overlaps local_ms) */
+  /* ABI 3: sums over this rank's local products (cbg_profile of each): heavy-kernel time and counts, and the
+   * products' outputs / B nonzeros / B columns (SURVEY 8(d) algorithmic bytes of the rank's local work) */
+  double heavy_ms;
+  int64_t heavy_multiplies, heavy_nnz_b, heavy_nnz_c;
+  int64_t local_nnz_out, local_nnz_b, local_ncol_b;
+  int32_t local_products;
 } cbg_grid_stats;
 
 /* RCCL unique id (128 bytes) made on one rank and handed to all (any out-of-band channel). */
@@ -341,6 +352,23 @@ cbg_status cbg_summa_estimate(cbg_grid* grid, const cbg_dcsc_view* A, const cbg_
 /* Merge the stage products, then (L > 1) the fiber exchange + merge: the rank's colsplit C piece. */
 cbg_status cbg_reduce_all(cbg_grid* grid, const cbg_csc_result* parts, int32_t nparts, cbg_semiring sr,
                           cbg_dtype out_type, cbg_csc_result* C, cbg_grid_stats* stats);
+
+/* ------------------------------------------------------------------ fiber wire codec (test / measurement)
+ * The fiber pipeline's production encoder and decoder (grid.hip fiber_pipeline, the wire format of the 3D fiber
+ * reduction that replaces ParFriends.h:3119-3153's all-to-all of SpTuples) run on one partial P without a
+ * transport: P's columns are cut into `chunks` message chunks as the pipeline cuts them, each chunk is encoded in
+ * its smallest lossless form, decoded back, and compared bit for bit with the chunk.  Reports the bytes the
+ * messages put on the link (what cbg_grid_stats.fiber_bytes counts in a real exchange). */
+typedef struct {
+  int64_t columns, entries, chunks;
+  int64_t header_bytes, row_bytes, escape_bytes, value_bytes, value_header_bytes, wire_bytes;
+  int32_t row_formats;       /* bit f set: some chunk's rows travelled as format f (0 int32, 1 u16 gaps, 2 varint) */
+  int32_t value_formats;     /* bit f set: some chunk's values as format f (0 native, 1 f32, 2 u16, 3 varint) */
+  int32_t roundtrip_exact;   /* 1: every decoded chunk equals its source (colptr, rows, value bits) */
+  int64_t mismatches;        /* entries (or columns) that differ after the round trip */
+  double encode_ms, decode_ms;
+} cbg_codec_stats;
+cbg_status cbg_fiber_codec(cbg_ctx* ctx, const cbg_csc_result* P, int32_t chunks, cbg_codec_stats* stats);
 
 #ifdef __cplusplus
 }

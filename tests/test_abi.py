@@ -46,17 +46,40 @@ def test_no_oracle_in_product_library():
 def test_abi_version_and_strerror():
     from combblas_amd import _abi
     lib = _abi.lib()
-    assert lib.cbg_abi_version() == 2
+    assert lib.cbg_abi_version() == 3
     assert b"3002" in lib.cbg_strerror(3002)
     assert b"BoolCopy" in lib.cbg_strerror(13)
 
 
-def test_struct_layouts_match_header():
+def test_struct_layouts_match_header(tmp_path):
+    """Every ctypes mirror has the C compiler's size and field offsets of include/cbgpu.h's struct."""
+    import shutil
+    import subprocess
     from combblas_amd import _abi
-    # cbg_dcsc_view: 4 int64, 3 pointers, 2 int32, pointer, enum, int32 -> 80 bytes on LP64
-    assert ctypes.sizeof(_abi.DcscView) == 80
-    assert ctypes.sizeof(_abi.CscResult) == 72
-    assert ctypes.sizeof(_abi.Profile) == 6 * 8 + 2 * 8 + 16 * 8 + 8 + 8   # + heavy_ms, known_items
+    structs = {"cbg_dcsc_view": _abi.DcscView, "cbg_csc_result": _abi.CscResult, "cbg_profile": _abi.Profile,
+               "cbg_mcl_stats": _abi.MclStats, "cbg_grid_stats": _abi.GridStats, "cbg_codec_stats": _abi.CodecStats,
+               "cbg_grid_info": _abi.GridInfo, "cbg_transport": _abi.Transport, "cbg_host_csc": _abi.HostCsc}
+    assert ctypes.sizeof(_abi.DcscView) == 80 and ctypes.sizeof(_abi.CscResult) == 72
+    if shutil.which("gcc") is None:
+        pytest.skip("no C compiler")
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "cbgpu.h"', "int main(void) {"]
+    for cname, py in structs.items():
+        lines.append(f'  printf("{cname} size %zu\\n", sizeof({cname}));')
+        for f in py._fields_:
+            lines.append(f'  printf("{cname} {f[0]} %zu\\n", offsetof({cname}, {f[0]}));')
+    lines.append("  return 0;\n}")
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-I", os.path.join(REPO, "include"), str(src), "-o", str(exe)], check=True)
+    got = {}
+    for line in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.splitlines():
+        c, f, v = line.split()
+        got[(c, f)] = int(v)
+    for cname, py in structs.items():
+        assert got[(cname, "size")] == ctypes.sizeof(py), cname
+        for f in py._fields_:
+            assert got[(cname, f[0])] == getattr(py, f[0]).offset, (cname, f[0])
 
 
 def test_init_without_gpu_fails_loudly():

@@ -93,3 +93,36 @@ def test_predict_scaling_model():
     p4 = ps.predict([r4, dict(r4, rank=1)], link_gbps=60.0)
     assert p4["parts_ms"]["merge"] == 0.0 and abs(p4["parts_ms"]["bcast"] - 2.0) < 1e-6   # 120 MB at 60 GB/s
     assert p4["multiplies"] == 1e10
+
+
+def test_select_block_cols_and_torch_checksum():
+    """bench.py's distributed checks: a column sample of a Block, and the checksum of a piece's reference-sample
+    columns summed over pieces equal to the checksum of the whole sample (what refbench prints)."""
+    rng = np.random.default_rng(3)
+    M = sp.random(40, 30, density=0.2, random_state=rng, format="csc")
+    M.data = np.round(M.data * 100)
+    b = _block(M)
+    cols = torch.tensor([0, 3, 4, 17, 29])
+    S = bench.select_block_cols(b, cols)
+    assert np.array_equal(_dense(S), M.toarray()[:, cols.numpy()])
+    stride = 3
+    whole = M[:, ::stride].tocsc()
+    whole.sort_indices()
+    ref = bench.entry_checksum(whole.indptr.astype(np.int64), whole.indices.astype(np.int32), whole.data)
+    total = 0
+    for (r0, r1) in ((0, 25), (25, 40)):
+        for (c0, c1) in ((0, 11), (11, 30)):
+            P = sp.csc_matrix(M[r0:r1, c0:c1])
+            P.sort_indices()
+            first = (-c0) % stride
+            jl = torch.arange(first, c1 - c0, stride)
+            R = bench.select_block_cols(_block(P), jl)
+            cc = torch.repeat_interleave((jl + c0) // stride, torch.diff(R.cp))
+            total += bench.entry_checksum_t(cc, R.ir.to(torch.int64) + r0, R.val)
+    assert f"{total & ((1 << 64) - 1):016x}" == ref
+
+
+def test_host_cores_record():
+    threads, rec = bench.host_cores(1)
+    assert 1 <= threads <= 16 and threads <= rec["affinity_cpus"]
+    assert rec["os_cpu_count"] == os.cpu_count() and rec["pool_share_cpus"] == 16

@@ -1,0 +1,71 @@
+#!/bin/bash
+# One gpurun call as a list of steps (run from the repo root); every GPU step has its own time limit and the
+# script stops at the first step that fails (exit 10 + step index: never 2 or 3, which gpurun reserves).
+#   tools/gpu_steps.sh <tag> <step> [<step> ...]
+# steps:
+#   tests              the whole -m gpu suite            tests:<expr>   pytest -m gpu -k <expr>
+#   bench              N = 1 bench line (configs[1])     bench:<args>   bench.py with extra args (',' = ' ')
+#   dist:<N>:<scale>   N ranks on this one GPU over libcbgpu's RCCL grid (RCCL sockets), verified bench line
+#   share:<N>:<scale>  every rank's share of the N-GPU layout at full size, verified (bench.py --rank-share)
+#   prof               rocprofv3 kernel stats of the bench (5 timed products)
+#   pmc                heavy-kernel and whole-product HBM bytes (tools/pmc_heavy.py, one counter per pass)
+#   sq                 SQ limiter counters (two groups) over one product
+set -u
+TAG=$1; shift
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+i=0
+fail() { echo "step $i ($1) failed rc=$2"; exit $((10 + i)); }
+for step in "$@"; do
+  i=$((i + 1))
+  IFS=: read -r kind a b <<< "$step"
+  echo "== step $i: $step ($(date +%T))"
+  case $kind in
+    tests)
+      if [ -n "${a:-}" ]; then K=(-k "$a"); else K=(); fi
+      timeout -k 10 1000 python -u -m pytest tests -m gpu -v "${K[@]}" --timeout 300 --timeout-method thread \
+        > "$OUT/gpu_tests${a:+_$a}.log" 2>&1
+      rc=$?; tail -2 "$OUT/gpu_tests${a:+_$a}.log"
+      [ $rc -eq 0 ] || { grep -E "^(FAILED|ERROR)|Error" "$OUT/gpu_tests${a:+_$a}.log" | head -20; fail "$step" $rc; } ;;
+    bench)
+      extra=${a//,/ }
+      timeout -k 10 600 python -u bench.py $extra > "$OUT/bench${a:+_${a//[ ,=-]/}}.log" 2>&1 || \
+        { tail -5 "$OUT/bench${a:+_${a//[ ,=-]/}}.log" | cut -c1-800; fail "$step" 1; }
+      tail -1 "$OUT/bench${a:+_${a//[ ,=-]/}}.log" | cut -c1-1200 ;;
+    dist)
+      CBG_DIST_BACKEND=${BACKEND:-rccl-net} timeout -k 10 600 python -m torch.distributed.run --nnodes=1 \
+        --nproc-per-node "$a" --master-addr 127.0.0.1 --master-port $((29600 + i)) bench.py --gpus "$a" \
+        --steps ${STEPS:-3} --warmup 1 --scale "$b" > "$OUT/dist_n${a}_s${b}.log" 2>&1
+      rc=$?; grep '^{' "$OUT/dist_n${a}_s${b}.log" | tail -1 | cut -c1-1500
+      [ $rc -eq 0 ] || { grep -v '^{' "$OUT/dist_n${a}_s${b}.log" | tail -8 | cut -c1-400; fail "$step" $rc; } ;;
+    share)
+      timeout -k 10 900 python -u bench.py --rank-share all --gpus-virtual "$a" --scale "$b" \
+        > "$OUT/rank_share_s${b}_n${a}.jsonl" 2> "$OUT/rank_share_s${b}_n${a}.err"
+      rc=$?; cut -c1-400 "$OUT/rank_share_s${b}_n${a}.jsonl"
+      [ $rc -eq 0 ] || { tail -8 "$OUT/rank_share_s${b}_n${a}.err"; fail "$step" $rc; } ;;
+    prof)
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
+        python3 bench.py --steps 5 --warmup 2 --no-cpu > "$OUT/prof.log" 2>&1 || { tail -20 "$OUT/prof.log"; fail prof 1; }
+      tail -1 "$OUT/prof.log" | cut -c1-400 ;;
+    pmc)
+      timeout -k 10 600 python3 -u tools/pmc_heavy.py run "$TAG" 20 > "$OUT/pmc_heavy.log" 2>&1 || \
+        { tail -5 "$OUT/pmc_heavy.log"; fail pmc 1; }
+      tail -1 "$OUT/pmc_heavy.log" | cut -c1-600
+      timeout -k 10 600 python3 -u tools/pmc_heavy.py product "$TAG" 20 > "$OUT/pmc_product.log" 2>&1 || \
+        { tail -5 "$OUT/pmc_product.log"; fail pmc 2; }
+      tail -1 "$OUT/pmc_product.log" | cut -c1-600 ;;
+    sq)
+      j=0
+      for grp in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VALU" \
+                 "SQ_WAVES SQ_BUSY_CYCLES SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE"; do
+        j=$((j + 1))
+        timeout -s KILL 180 rocprofv3 --pmc $grp --output-format csv -d "$OUT/sq$j" -o run -- \
+          python3 bench.py --steps 1 --warmup 0 --no-cpu > "$OUT/sq$j.log" 2>&1 || fail "sq $j" 1
+      done
+      python3 tools/pmc_summary.py "$OUT/${TAG}_sq.json" "$OUT"/sq1 "$OUT"/sq2 > "$OUT/sq_summary.txt" 2>&1 || true
+      head -4 "$OUT/sq_summary.txt" | cut -c1-900 ;;
+    *) echo "unknown step $step"; exit 9 ;;
+  esac
+done
+echo "== all steps ok ($(date +%T))"
