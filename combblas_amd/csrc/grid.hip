@@ -153,31 +153,66 @@ __device__ __forceinline__ bool as_u32(double x, uint32_t* u) {   // an integer 
   return in && __double_as_longlong((double)*u) == __double_as_longlong(x);
 }
 
+// The codec kernels take one column per wave and kCodeEpl consecutive entries per lane per step (a step = 256
+// entries or 256 bytes): one wave scan per step instead of one per 64 entries, four loads in flight per lane.
+constexpr int kCodeEpl = 4;
+constexpr int kCodeStep = kCodeEpl * kWave;
+
 // one wave per column: escapes of the u16 gaps, varint bytes of the row gaps, varint bytes of the values; over
 // the message: bad[0] values that do not survive f32, bad[1] not u16, bad[2] not u32 integers
-__global__ void k_code_count(int64_t ncol, const int64_t* __restrict__ cp, const int32_t* __restrict__ ir,
-                             const double* __restrict__ val, int64_t* __restrict__ esc, int64_t* __restrict__ rbytes,
-                             int64_t* __restrict__ vbytes, unsigned long long* __restrict__ bad) {
+__global__ void __launch_bounds__(256) k_code_count(int64_t ncol, const int64_t* __restrict__ cp,
+                                                    const int32_t* __restrict__ ir, const double* __restrict__ val,
+                                                    int64_t* __restrict__ esc, int64_t* __restrict__ rbytes,
+                                                    int64_t* __restrict__ vbytes, unsigned long long* __restrict__ bad) {
   const int l = lane_id();
   int64_t b32 = 0, b16 = 0, bvar = 0;
   for (int64_t c = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / kWave; c < ncol;
        c += ((int64_t)gridDim.x * blockDim.x) / kWave) {
     const int64_t s = cp[c], e = cp[c + 1];
     int64_t ne = 0, nr = 0, nv = 0;
-    for (int64_t i = s + l; i < e; i += kWave) {
-      const int64_t d = (int64_t)ir[i] - (i == s ? 0 : ir[i - 1]);
-      ne += d > (int64_t)kGapMax;
-      nr += vlen32((uint32_t)d);
-      if (val) {
-        const double x = val[i];
-        b32 += __double_as_longlong((double)(float)x) != __double_as_longlong(x);
-        const bool in16 = x >= 0.0 && x <= 65535.0;
-        b16 += !(in16 && __double_as_longlong((double)(unsigned short)x) == __double_as_longlong(x));
-        uint32_t u;
-        const bool ok = as_u32(x, &u);
-        bvar += !ok;
-        nv += ok ? vlen32(u) : 5;
+    int32_t prev = 0;   // the row before the step (0 before the column's first entry)
+    // the next step's rows and values are loaded while this step is counted (a long column is one wave's serial
+    // walk: without the prefetch every step waits a full memory latency)
+    int32_t rn[kCodeEpl];
+    double xn[kCodeEpl];
+    // unconditional loads from clamped addresses (a conditional load becomes a branch + an immediate wait: the
+    // four loads of a step would go out one at a time)
+    auto load = [&](int64_t b) {
+#pragma unroll
+      for (int k = 0; k < kCodeEpl; ++k) {
+        const int64_t i = min(b + k, e - 1);
+        rn[k] = ir[i];
+        if (val) xn[k] = val[i];
       }
+    };
+    if (s < e) load(s + kCodeEpl * l);   // (an empty column has no address to clamp to)
+    for (int64_t i0 = s; i0 < e; i0 += kCodeStep) {
+      const int64_t base = i0 + kCodeEpl * l;
+      int32_t r[kCodeEpl];
+      double x[kCodeEpl];
+#pragma unroll
+      for (int k = 0; k < kCodeEpl; ++k) { r[k] = rn[k]; x[k] = val ? xn[k] : 0.0; }
+      if (i0 + kCodeStep < e) load(base + kCodeStep);
+      const int32_t up = (int32_t)dpp_prev_lane((uint32_t)r[kCodeEpl - 1]);
+      const int32_t before = l == 0 ? prev : up;
+#pragma unroll
+      for (int k = 0; k < kCodeEpl; ++k) {
+        if (base + k >= e) break;
+        const int64_t d = (int64_t)r[k] - (k ? r[k - 1] : before);
+        ne += d > (int64_t)kGapMax;
+        nr += vlen32((uint32_t)d);
+        if (val) {
+          const double v = x[k];
+          b32 += __double_as_longlong((double)(float)v) != __double_as_longlong(v);
+          const bool in16 = v >= 0.0 && v <= 65535.0;
+          b16 += !(in16 && __double_as_longlong((double)(unsigned short)v) == __double_as_longlong(v));
+          uint32_t u;
+          const bool ok = as_u32(v, &u);
+          bvar += !ok;
+          nv += ok ? vlen32(u) : 5;
+        }
+      }
+      prev = (int32_t)last_lane((uint32_t)r[kCodeEpl - 1]);
     }
     ne = wave_sum64(ne);
     nr = wave_sum64(nr);
@@ -196,87 +231,175 @@ __global__ void k_code_count(int64_t ncol, const int64_t* __restrict__ cp, const
   if (l == 0 && bvar) atomicAdd(bad + 2, (unsigned long long)bvar);
 }
 
-// MODE 0: row gaps of ir, MODE 1: values (u32 integers) of val -> varint bytes at off[c] of column c
+// MODE 0: row gaps of ir, MODE 1: values (u32 integers) of val -> varint bytes at off[c] of column c.  A step's codes
+// are assembled in the wave's LDS slice (one wave scan places them), then copied out with coalesced byte stores.
 template <int MODE>
-__global__ void k_var_encode(int64_t ncol, const int64_t* __restrict__ cp, const int32_t* __restrict__ ir,
-                             const double* __restrict__ val, const int64_t* __restrict__ off,
-                             uint8_t* __restrict__ out) {
+__global__ void __launch_bounds__(256) k_var_encode(int64_t ncol, const int64_t* __restrict__ cp,
+                                                    const int32_t* __restrict__ ir, const double* __restrict__ val,
+                                                    const int64_t* __restrict__ off, uint8_t* __restrict__ out) {
+  __shared__ uint8_t stage[256 / kWave][kCodeStep * 5];
   const int l = lane_id();
+  uint8_t* sb = stage[threadIdx.x / kWave];
   for (int64_t c = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / kWave; c < ncol;
        c += ((int64_t)gridDim.x * blockDim.x) / kWave) {
     const int64_t s = cp[c], e = cp[c + 1];
     int64_t o = off[c];
-    for (int64_t i0 = s; i0 < e; i0 += kWave) {
-      const int64_t i = i0 + l;
-      uint32_t x = 0;
-      int len = 0;
-      if (i < e) {
-        if (MODE == 0) x = (uint32_t)(ir[i] - (i == s ? 0 : ir[i - 1]));
-        else (void)as_u32(val[i], &x);
-        len = vlen32(x);
+    int32_t prev = 0;
+    int32_t rn[kCodeEpl];   // the next step's rows (MODE 0) or values (MODE 1), loaded one step ahead
+    double vn[kCodeEpl];
+    auto load = [&](int64_t b) {   // clamped, unconditional (see k_code_count)
+#pragma unroll
+      for (int k = 0; k < kCodeEpl; ++k) {
+        const int64_t i = min(b + k, e - 1);
+        if (MODE == 0) rn[k] = ir[i];
+        else vn[k] = val[i];
       }
-      const int incl = wave_incl_scan(len);
-      uint8_t* dst = out + o + (incl - len);
-      for (int k = 0; k < len; ++k) dst[k] = (uint8_t)(((x >> (7 * k)) & 0x7Fu) | (k + 1 < len ? 0x80u : 0u));
-      o += __shfl(incl, kWave - 1, kWave);
+    };
+    if (s < e) load(s + kCodeEpl * l);   // (an empty column has no address to clamp to)
+    for (int64_t i0 = s; i0 < e; i0 += kCodeStep) {
+      const int64_t base = i0 + kCodeEpl * l;
+      uint32_t x[kCodeEpl];
+      int len[kCodeEpl];
+      int tot = 0;
+      int32_t r[kCodeEpl];
+      double vv[kCodeEpl];
+#pragma unroll
+      for (int k = 0; k < kCodeEpl; ++k) {
+        if (MODE == 0) r[k] = rn[k];
+        else vv[k] = vn[k];
+      }
+      if (i0 + kCodeStep < e) load(base + kCodeStep);
+      if (MODE == 0) {
+        const int32_t up = (int32_t)dpp_prev_lane((uint32_t)r[kCodeEpl - 1]);
+        const int32_t before = l == 0 ? prev : up;
+#pragma unroll
+        for (int k = 0; k < kCodeEpl; ++k) x[k] = (uint32_t)(r[k] - (k ? r[k - 1] : before));
+        prev = (int32_t)last_lane((uint32_t)r[kCodeEpl - 1]);
+      } else {
+#pragma unroll
+        for (int k = 0; k < kCodeEpl; ++k) {
+          x[k] = 0;
+          if (base + k < e) (void)as_u32(vv[k], &x[k]);
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < kCodeEpl; ++k) {
+        len[k] = base + k < e ? vlen32(x[k]) : 0;
+        tot += len[k];
+      }
+      const int incl = dpp_incl_scan(tot);
+      const int T = (int)last_lane((uint32_t)incl);
+      int p = incl - tot;
+#pragma unroll
+      for (int k = 0; k < kCodeEpl; ++k)
+        for (int b = 0; b < len[k]; ++b)
+          sb[p++] = (uint8_t)(((x[k] >> (7 * b)) & 0x7Fu) | (b + 1 < len[k] ? 0x80u : 0u));
+      wave_sync();
+      for (int q = l; q < T; q += kWave) out[o + q] = sb[q];
+      wave_sync();   // the slice is written again by the next step
+      o += T;
     }
   }
 }
 
-// one wave per column: bytes [off[c], off[c+1]) -> entries [cp[c], cp[c+1]).  A chunk is 64 bytes, one per lane; a
-// byte without the high bit ends an entry (ballot); the entry's value is gathered from the (at most 5) bytes back to
-// the previous end, an entry begun in the previous chunk continues from its pending bits.  MODE 0: the values are
-// row gaps (inclusive scan + the column's running row -> int32 rows), MODE 1: u32 integers -> f64 values.
+// one wave per column: bytes [off[c], off[c+1]) -> entries [cp[c], cp[c+1]).  A step is 512 bytes, 8 per lane (the
+// bytes in flight per wave are what bounds this kernel); a byte without the high bit ends an entry.  A code is at most 5
+// bytes, so an entry ending in lane l's bytes starts in them or in the last 4 bytes of lane l-1's (lane 0: the previous
+// step's lane 63, carried; at the column start the four bytes before it count as terminators).  MODE 0: the values are
+// row gaps (scan + the column's running row -> int32 rows), MODE 1: u32 integers -> f64 values.  The next column's
+// header is loaded while the current one is decoded.
+constexpr int kDecEpl = 8;
+constexpr int kDecStep = kDecEpl * kWave;
 template <int MODE>
-__global__ void k_var_decode(int64_t ncol, const int64_t* __restrict__ cp, const int64_t* __restrict__ off,
-                             const uint8_t* __restrict__ in, int32_t* __restrict__ ir, double* __restrict__ val) {
+__global__ void __launch_bounds__(256) k_var_decode(int64_t ncol, const int64_t* __restrict__ cp,
+                                                    const int64_t* __restrict__ off, const uint8_t* __restrict__ in,
+                                                    int32_t* __restrict__ ir, double* __restrict__ val) {
+  // a step's decoded entries (<= 512) go through the wave's LDS slice and out with coalesced stores
+  __shared__ uint64_t stage[256 / kWave][kDecStep];
   const int l = lane_id();
-  for (int64_t c = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / kWave; c < ncol;
-       c += ((int64_t)gridDim.x * blockDim.x) / kWave) {
-    const int64_t be = off[c + 1];
-    int64_t idx = cp[c];
-    int64_t run = 0;        // MODE 0: the last row decoded in this column
-    uint32_t pend = 0;      // bits of an entry begun in the previous chunk
-    int pbits = 0;
-    for (int64_t p0 = off[c]; p0 < be; p0 += kWave) {
-      const int64_t p = p0 + l;
-      const bool valid = p < be;
-      const uint32_t b = valid ? in[p] : 0u;
-      const bool term = valid && !(b & 0x80u);
-      const uint64_t T = __ballot(term);
-      const uint32_t dig = b & 0x7Fu;
-      const uint64_t below = T & ((1ull << l) - 1ull);
-      const int st = below ? 64 - __clzll(below) : 0;   // first byte lane of this lane's entry in the chunk
-      uint32_t v = st == 0 ? pend : 0u;
-      const int base = st == 0 ? pbits : 0;
+  uint64_t* sb = stage[threadIdx.x / kWave];
+  const int64_t stride = ((int64_t)gridDim.x * blockDim.x) / kWave;
+  int64_t c = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / kWave;
+  int64_t h_b = 0, h_e = 0, h_i = 0;   // the header of column c
+  if (c < ncol) { h_b = off[c]; h_e = off[c + 1]; h_i = cp[c]; }
+  for (; c < ncol; c += stride) {
+    const int64_t b0 = h_b, be = h_e;
+    int64_t idx = h_i;
+    if (c + stride < ncol) { h_b = off[c + stride]; h_e = off[c + stride + 1]; h_i = cp[c + stride]; }
+    int64_t run = 0;           // MODE 0: the last row decoded in this column
+    uint32_t cw = 0, ctm = 0xFu;
+    uint32_t bn[kDecEpl];   // the next step's bytes, loaded one step ahead
+    auto load = [&](int64_t b) {   // clamped, unconditional (see k_code_count); masked where consumed
 #pragma unroll
-      for (int k = 0; k < 5; ++k) {
-        const int j = l - k;
-        const uint32_t dj = __shfl(dig, j < 0 ? 0 : j, kWave);
-        if (j >= st && j >= 0) v |= dj << (base + 7 * (j - st));
+      for (int k = 0; k < kDecEpl; ++k) bn[k] = in[min(b + k, be - 1)];
+    };
+    if (b0 < be) load(b0 + kDecEpl * l);
+    for (int64_t p0 = b0; p0 < be; p0 += kDecStep) {
+      const int64_t pb = p0 + kDecEpl * l;
+      uint64_t wd = 0;
+      uint32_t tm = 0;
+#pragma unroll
+      for (int k = 0; k < kDecEpl; ++k) {
+        const bool in_col = pb + k < be;
+        const uint32_t b = in_col ? bn[k] : 0u;
+        wd |= (uint64_t)b << (8 * k);
+        tm |= (in_col && !(b & 0x80u) ? 1u : 0u) << k;
       }
-      const int64_t at = idx + __popcll(below);
+      if (p0 + kDecStep < be) load(pb + kDecStep);
+      const uint32_t hi = (uint32_t)(wd >> 32), thi = tm >> 4;
+      uint32_t w1 = dpp_prev_lane(hi), t1 = dpp_prev_lane(thi);
+      if (l == 0) { w1 = cw; t1 = ctm; }
+      // window: positions 0..3 = lane l-1's last 4 bytes, 4..11 = this lane's 8 bytes
+      const uint64_t W0 = (uint64_t)w1 | (wd << 32);
+      const uint32_t W1 = hi;
+      const uint32_t TM = t1 | (tm << 4);
+      auto byte_at = [&](int p) -> uint32_t {
+        return p < 8 ? (uint32_t)(W0 >> (8 * p)) & 0xFFu : (W1 >> (8 * (p - 8))) & 0xFFu;
+      };
+      uint32_t v[kDecEpl];
+      int64_t g = 0;
+#pragma unroll
+      for (int k = 0; k < kDecEpl; ++k) {
+        v[k] = 0;
+        if ((tm >> k) & 1u) {
+          const int q = 4 + k;
+          const uint32_t below = TM & ((1u << q) - 1u);
+          const int st = below ? 32 - __clz(below) : 0;   // one past the previous terminator
+#pragma unroll
+          for (int j = 0; j < 5; ++j)
+            if (st + j <= q) v[k] |= (byte_at(st + j) & 0x7Fu) << (7 * j);
+          g += v[k];
+        }
+      }
+      const int cnt = __popc(tm);
+      const int ci = dpp_incl_scan(cnt);
+      const int T = (int)last_lane((uint32_t)ci);
+      int at = ci - cnt;
       if (MODE == 0) {
-        const int64_t inc = wave_incl_scan64(term ? (int64_t)v : 0);
-        if (term) ir[at] = (int32_t)(run + inc);
-        run += __shfl(inc, kWave - 1, kWave);
-      } else if (term) {
-        val[at] = (double)v;
-      }
-      idx += __popcll(T);
-      // an entry left open at the chunk's end (the <= 4 bytes after its last terminator; a 64-byte chunk always
-      // holds a terminator, codes being <= 5 bytes): its bits carry over
-      const int ps = T ? 64 - __clzll(T) : 0;
-      const int nb = p0 + kWave <= be ? kWave - ps : 0;   // no carry past the column's last byte
-      uint32_t np = 0;
+        const int64_t gi = dpp_incl_scan64(g);
+        int64_t row = run + (gi - g);
+        uint32_t* s32 = (uint32_t*)sb;
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int j = kWave - 1 - k;
-        const uint32_t dj = __shfl(dig, j, kWave);
-        if (j >= ps && nb > 0) np |= dj << (7 * (j - ps));
+        for (int k = 0; k < kDecEpl; ++k)
+          if ((tm >> k) & 1u) {
+            row += v[k];
+            s32[at++] = (uint32_t)row;
+          }
+        run += last_lane64(gi);
+        wave_sync();
+        for (int q = l; q < T; q += kWave) ir[idx + q] = (int32_t)s32[q];
+      } else {
+        double* sd = (double*)sb;
+#pragma unroll
+        for (int k = 0; k < kDecEpl; ++k)
+          if ((tm >> k) & 1u) sd[at++] = (double)v[k];
+        wave_sync();
+        for (int q = l; q < T; q += kWave) val[idx + q] = sd[q];
       }
-      pend = np;
-      pbits = 7 * nb;
+      wave_sync();   // the slice is written again by the next step
+      idx += T;
+      cw = last_lane(hi);
+      ctm = last_lane(thi);
     }
   }
 }

@@ -200,6 +200,47 @@ __device__ __forceinline__ int wave_incl_scan(int v) {
   }
   return v;
 }
+// DPP forms (GFX9 data-parallel primitives, no LDS crossbar): row_shr within 16-lane rows, then row_bcast:15 /
+// row_bcast:31 carry the row totals across the wave.  Lanes whose source is out of range read `old` = 0.
+__device__ __forceinline__ int dpp_incl_scan(int v) {
+  v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);   // row_shr:1
+  v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);   // row_shr:2
+  v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false);   // row_shr:4
+  v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false);   // row_shr:8
+  v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);   // row_bcast:15 into rows 1, 3
+  v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);   // row_bcast:31 into rows 2, 3
+  return v;
+}
+__device__ __forceinline__ int64_t dpp_shift64(int64_t v, int ctrl_sel) {
+  const uint32_t lo = (uint32_t)v, hi = (uint32_t)((uint64_t)v >> 32);
+  uint32_t a, b;
+  switch (ctrl_sel) {
+    case 0: a = __builtin_amdgcn_update_dpp(0u, lo, 0x111, 0xf, 0xf, false); b = __builtin_amdgcn_update_dpp(0u, hi, 0x111, 0xf, 0xf, false); break;
+    case 1: a = __builtin_amdgcn_update_dpp(0u, lo, 0x112, 0xf, 0xf, false); b = __builtin_amdgcn_update_dpp(0u, hi, 0x112, 0xf, 0xf, false); break;
+    case 2: a = __builtin_amdgcn_update_dpp(0u, lo, 0x114, 0xf, 0xf, false); b = __builtin_amdgcn_update_dpp(0u, hi, 0x114, 0xf, 0xf, false); break;
+    case 3: a = __builtin_amdgcn_update_dpp(0u, lo, 0x118, 0xf, 0xf, false); b = __builtin_amdgcn_update_dpp(0u, hi, 0x118, 0xf, 0xf, false); break;
+    case 4: a = __builtin_amdgcn_update_dpp(0u, lo, 0x142, 0xa, 0xf, false); b = __builtin_amdgcn_update_dpp(0u, hi, 0x142, 0xa, 0xf, false); break;
+    default: a = __builtin_amdgcn_update_dpp(0u, lo, 0x143, 0xc, 0xf, false); b = __builtin_amdgcn_update_dpp(0u, hi, 0x143, 0xc, 0xf, false); break;
+  }
+  return (int64_t)(((uint64_t)b << 32) | a);
+}
+__device__ __forceinline__ int64_t dpp_incl_scan64(int64_t v) {
+#pragma unroll
+  for (int k = 0; k < 6; ++k) v += dpp_shift64(v, k);
+  return v;
+}
+// the value of lane l-1 (lane 0: 0): wave_shr:1
+__device__ __forceinline__ uint32_t dpp_prev_lane(uint32_t v) {
+  return __builtin_amdgcn_update_dpp(0u, v, 0x138, 0xf, 0xf, false);
+}
+// lane 63's value, uniform (scalar read)
+__device__ __forceinline__ uint32_t last_lane(uint32_t v) { return __builtin_amdgcn_readlane(v, 63); }
+__device__ __forceinline__ int64_t last_lane64(int64_t v) {
+  const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, 63);
+  const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)((uint64_t)v >> 32), 63);
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
 __device__ __forceinline__ int64_t wave_sum64(int64_t v) {
 #pragma unroll
   for (int d = kWave / 2; d > 0; d >>= 1) v += __shfl_xor(v, d, kWave);

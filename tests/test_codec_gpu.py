@@ -68,7 +68,7 @@ def test_codec_forms_and_edges(gpu_ctx):
     cols[0][1][0] = -0.0
     _check(_mat(gpu_ctx, 3000, 5, cols).fiber_codec(2), vals=1 << 1)
     # integers above 2^32 -> not varint, not f32/u16: native
-    cols = [([1, 2, 3], [2.0 ** 40, 3.0, 1.0])]
+    cols = [([1, 2, 3], [2.0 ** 40 + 1.0, 3.0, 1.0])]
     _check(_mat(gpu_ctx, 10, 1, cols).fiber_codec(1), vals=1 << 0)
     # an f32 product and a pattern (bool) product: native values, coded rows
     cols = [(np.arange(0, 9000, 7), np.ones(1286)) for _ in range(3)]

@@ -7,6 +7,7 @@
 #   bench              N = 1 bench line (configs[1])     bench:<args>   bench.py with extra args (',' = ' ')
 #   dist:<N>:<scale>   N ranks on this one GPU over libcbgpu's RCCL grid (RCCL sockets), verified bench line
 #   share:<N>:<scale>  every rank's share of the N-GPU layout at full size, verified (bench.py --rank-share)
+#   codec:<scale>      the fiber wire codec on the 1x1x2 message (tools/bench_codec.py) + its rocprofv3 kernel stats
 #   prof               rocprofv3 kernel stats of the bench (5 timed products)
 #   pmc                heavy-kernel and whole-product HBM bytes (tools/pmc_heavy.py, one counter per pass)
 #   sq                 SQ limiter counters (two groups) over one product
@@ -44,6 +45,12 @@ for step in "$@"; do
         > "$OUT/rank_share_s${b}_n${a}.jsonl" 2> "$OUT/rank_share_s${b}_n${a}.err"
       rc=$?; cut -c1-400 "$OUT/rank_share_s${b}_n${a}.jsonl"
       [ $rc -eq 0 ] || { tail -8 "$OUT/rank_share_s${b}_n${a}.err"; fail "$step" $rc; } ;;
+    codec)
+      timeout -k 10 300 python -u tools/bench_codec.py --scale "${a:-21}" > "$OUT/codec_s${a:-21}.json" 2>&1 || \
+        { tail -5 "$OUT/codec_s${a:-21}.json"; fail "$step" 1; }
+      cut -c1-600 "$OUT/codec_s${a:-21}.json"
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/codec_prof" -o run -- \
+        python3 tools/bench_codec.py --scale "${a:-21}" --reps 1 > "$OUT/codec_prof.log" 2>&1 || { tail -5 "$OUT/codec_prof.log"; fail "$step" 2; } ;;
     prof)
       timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
         python3 bench.py --steps 5 --warmup 2 --no-cpu > "$OUT/prof.log" 2>&1 || { tail -20 "$OUT/prof.log"; fail prof 1; }
