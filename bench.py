@@ -958,6 +958,13 @@ def bench_rank_share(args):
         del final, Arow, Acol
         torch.cuda.empty_cache()
         rec["phases_ms"] = [{k: round(float(pp[k]), 3) for k in phase_keys} for pp in profs]
+        # what the heavy kernels processed per product (cbg_profile): the rank's heavy roofline
+        rec["heavy_counts"] = [{k: int(pp.get(k, 0)) for k in ("heavy_multiplies", "heavy_nnz_b", "heavy_nnz_c")}
+                               for pp in profs]
+        hb = sum(c["heavy_multiplies"] * (S_I + S_V) + c["heavy_nnz_b"] * (S_I + S_V + 2 * S_P)
+                 + c["heavy_nnz_c"] * (S_I + S_V) for c in rec["heavy_counts"])
+        hms = sum(float(pp["heavy_ms"]) for pp in profs)
+        rec["heavy_GBps"] = round(hb / (hms / 1e3) / 1e9, 1) if hms > 0 else None
         rec.update({"multiplies": st.get("multiplies", 0), "local_ms": round(local_ms, 3),
                     "merge_ms": round(merge_ms, 3), "nnz_C_piece": nnz_out,
                     "heavy_ms": round(sum(p["heavy_ms"] for p in profs), 3),

@@ -335,6 +335,22 @@ void MCLPruneRecoverySelect(SpParMat<IT, NT, DER>& A, NT hardThreshold, IT selec
       std::vector<int64_t> nrows(q), roff(q + 1, 0);
       MPI_Allgather(&nrl, 1, MPI_INT64_T, nrows.data(), 1, MPI_INT64_T, colw);
       for (int i = 0; i < q; ++i) roff[i + 1] = roff[i] + nrows[i];
+      // the gather below uses MPI int counts and int32 global rows: every rank checks its own sizes and the whole
+      // grid agrees (a different choice in two processor columns would mismatch the reference's row-world
+      // collectives); too large anywhere -> every rank takes the reference's own prune
+      {
+        int64_t rtot_bound = 0;   // received entries <= the processor column's entries of my column groups
+        MPI_Allreduce(&cp[ncl], &rtot_bound, 1, MPI_INT64_T, MPI_SUM, colw);
+        const int64_t lim = INT32_MAX;
+        int fits = roff[q] < lim && 8 * (ncl + 1) <= lim && 8 * (int64_t)q * (ncl / q + ncl % q + 1) <= lim &&
+                   (int64_t)std::max(sizeof(NT), (size_t)4) * rtot_bound <= lim;
+        int all = 0;
+        MPI_Allreduce(&fits, &all, 1, MPI_INT, MPI_MIN, A.getcommgrid()->GetWorld());
+        if (!all) {
+          combblas::MCLPruneRecoverySelect(A, hardThreshold, selectNum, recoverNum, recoverPct, kselectVersion);
+          return;
+        }
+      }
       auto grp = [&](int m, int64_t n, int64_t* g0, int64_t* g1) {
         *g0 = (n / q) * m;
         *g1 = m == q - 1 ? n : *g0 + n / q;
@@ -494,22 +510,29 @@ inline cbg_grid* make_grid(GridHandle& h, MPI_Comm world, MPI_Comm row, MPI_Comm
   MPI_Comm_rank(world, &wrank);
   const int grank = grid_rank >= 0 ? grid_rank : wrank;
   if (!grid_over_mpi()) {
-    // every rank learns whether rank 0 got an id, then every rank whether all communicators came up: a
-    // failure throws on all ranks together instead of leaving some blocked in a collective
+    // every rank learns whether rank 0 got an id, then every rank whether all communicators came up: a failure
+    // takes every rank to the MPI transport together instead of leaving some blocked in a collective (e.g. ranks
+    // sharing one GPU, which RCCL refuses without NCCL_HOSTID)
     char id[128] = {0};
     int ok = wrank == 0 ? (cbg_rccl_unique_id(id) == CBG_OK) : 1;
     MPI_Bcast(&ok, 1, MPI_INT, 0, world);
-    if (!ok) throw std::runtime_error("cbg_rccl_unique_id failed on rank 0");
-    MPI_Bcast(id, 128, MPI_BYTE, 0, world);
-    const cbg_status s = cbg_grid_create_rccl(context(), id, wsize, grank, layers, rows, cols, &h.grid);
-    int mine = s == CBG_OK, all = 0;
-    MPI_Allreduce(&mine, &all, 1, MPI_INT, MPI_MIN, world);
-    if (!all) {
-      if (h.grid) { cbg_grid_destroy(h.grid); h.grid = nullptr; }
-      throw std::runtime_error(std::string("cbg_grid_create_rccl: ") + cbg_strerror(s == CBG_OK ? CBG_ECOMM : s));
+    cbg_status s = CBG_ECOMM;
+    if (ok) {
+      MPI_Bcast(id, 128, MPI_BYTE, 0, world);
+      s = cbg_grid_create_rccl(context(), id, wsize, grank, layers, rows, cols, &h.grid);
     }
-    check(cbg_grid_query(h.grid, &last_grid_info()), "cbg_grid_query");
-    return h.grid;
+    int mine = ok && s == CBG_OK, all = 0;
+    MPI_Allreduce(&mine, &all, 1, MPI_INT, MPI_MIN, world);
+    if (all) {
+      check(cbg_grid_query(h.grid, &last_grid_info()), "cbg_grid_query");
+      return h.grid;
+    }
+    if (h.grid) { cbg_grid_destroy(h.grid); h.grid = nullptr; }
+    static bool warned = false;
+    if (!warned && wrank == 0)
+      fprintf(stderr, "combblas_gpu: RCCL grid setup failed (%s); using the MPI transport\n",
+              cbg_strerror(s == CBG_OK ? CBG_ECOMM : s));
+    warned = true;
   }
   h.mt.comm[CBG_GROUP_ROW] = row; h.mt.comm[CBG_GROUP_COL] = col;
   h.mt.comm[CBG_GROUP_FIBER] = fiber; h.mt.comm[CBG_GROUP_WORLD] = world;
@@ -519,6 +542,56 @@ inline cbg_grid* make_grid(GridHandle& h, MPI_Comm world, MPI_Comm row, MPI_Comm
   check(cbg_grid_create(context(), &t, wsize, grank, layers, rows, cols, &h.grid), "cbg_grid_create");
   check(cbg_grid_query(h.grid, &last_grid_info()), "cbg_grid_query");
   return h.grid;
+}
+
+// Grids are cached on the grid's row communicator (an MPI attribute; its delete callback destroys the grids when
+// the CommGrid / CCGrid that owns the communicator frees it), keyed by the other communicators, the shape and the
+// transport: a driver called once per iteration (HipMCL's MemEfficientSpGEMM loop, MCL.cpp:573-587) sets up its
+// RCCL communicators once.  grid_creations() counts the setups of this process.
+struct GridCacheEntry {
+  MPI_Comm world, col, fiber;
+  int layers, rows, cols, grank;
+  bool mpi;
+  std::unique_ptr<GridHandle> h;
+};
+struct GridCache {
+  std::vector<GridCacheEntry> v;
+};
+inline int grid_cache_delete(MPI_Comm, int, void* attr, void*) {
+  delete (GridCache*)attr;
+  return MPI_SUCCESS;
+}
+inline int grid_cache_keyval() {
+  static int kv = MPI_KEYVAL_INVALID;
+  if (kv == MPI_KEYVAL_INVALID) MPI_Comm_create_keyval(MPI_COMM_NULL_COPY_FN, &grid_cache_delete, &kv, nullptr);
+  return kv;
+}
+inline int& grid_creations() {
+  static int n = 0;
+  return n;
+}
+inline cbg_grid* cached_grid(MPI_Comm world, MPI_Comm row, MPI_Comm col, MPI_Comm fiber, int layers, int rows, int cols,
+                             int grid_rank = -1) {
+  const int kv = grid_cache_keyval();
+  GridCache* gc = nullptr;
+  int flag = 0;
+  MPI_Comm_get_attr(row, kv, &gc, &flag);
+  if (!flag || !gc) {
+    gc = new GridCache;
+    MPI_Comm_set_attr(row, kv, gc);
+  }
+  const bool mpi = grid_over_mpi();
+  for (GridCacheEntry& e : gc->v)
+    if (e.world == world && e.col == col && e.fiber == fiber && e.layers == layers && e.rows == rows &&
+        e.cols == cols && e.grank == grid_rank && e.mpi == mpi) {
+      check(cbg_grid_query(e.h->grid, &last_grid_info()), "cbg_grid_query");
+      return e.h->grid;
+    }
+  std::unique_ptr<GridHandle> h(new GridHandle);
+  make_grid(*h, world, row, col, fiber, layers, rows, cols, grid_rank);
+  ++grid_creations();
+  gc->v.push_back(GridCacheEntry{world, col, fiber, layers, rows, cols, grid_rank, mpi, std::move(h)});
+  return gc->v.back().h->grid;
 }
 
 
@@ -537,13 +610,12 @@ SpParMat<IU, NUO, UDERO> summa2d(SpParMat<IU, NU1, UDERA>& A, SpParMat<IU, NU2, 
                                  uint32_t flags) {
   std::shared_ptr<CommGrid> GA = A.getcommgrid(), GB = B.getcommgrid();
   if (A.getncol() != B.getnrow() || !(*GA == *GB)) throw std::runtime_error("Mult_AnXBn: DIMMISMATCH (3002)");
-  GridHandle h;
-  make_grid(h, GA->GetWorld(), GA->GetRowWorld(), GA->GetColWorld(), MPI_COMM_SELF, 1, GA->GetGridRows(),
-            GA->GetGridCols());
+  cbg_grid* grid = cached_grid(GA->GetWorld(), GA->GetRowWorld(), GA->GetColWorld(), MPI_COMM_SELF, 1,
+                               GA->GetGridRows(), GA->GetGridCols());
   cbg_dcsc_view va = view_of(*A.seqptr()), vb = view_of(*B.seqptr());
   cbg_csc_result C{};
   cbg_grid_stats st{};
-  check(cbg_spgemm_grid(h.grid, &va, &vb, DeviceSemiring<SR>::code, DeviceType<NUO>::code,
+  check(cbg_spgemm_grid(grid, &va, &vb, DeviceSemiring<SR>::code, DeviceType<NUO>::code,
                         CBG_SORTED_COLS | flags, &C, &st), "cbg_spgemm_grid");
   UDERO* D = to_local<IU, NUO, UDERO>(C);
   if (clearA) A.FreeMemory();
@@ -604,13 +676,12 @@ SpParMat3D<IU, NUO, UDERO> Mult_AnXBn_SUMMA3D(SpParMat3D<IU, NU1, UDER1>& A, SpP
     if (A.getncol() != B.getnrow() || !A.isColSplit() || B.isColSplit() || A.isSpecial() || B.isSpecial())
       throw std::runtime_error("Mult_AnXBn_SUMMA3D: needs colsplit A, rowsplit B, non-special layout (3002)");
     std::shared_ptr<CommGrid> layer = G->GetCommGridLayer();
-    GridHandle h;
-    make_grid(h, G->GetWorld(), layer->GetRowWorld(), layer->GetColWorld(), G->GetFiberWorld(), G->GetGridLayers(),
-              G->GetGridRows(), G->GetGridCols());
+    cbg_grid* grid = cached_grid(G->GetWorld(), layer->GetRowWorld(), layer->GetColWorld(), G->GetFiberWorld(),
+                                 G->GetGridLayers(), G->GetGridRows(), G->GetGridCols());
     cbg_dcsc_view va = view_of(*A.seqptr()), vb = view_of(*B.seqptr());
     cbg_csc_result C{};
     cbg_grid_stats st{};
-    check(cbg_spgemm_grid(h.grid, &va, &vb, DeviceSemiring<SR>::code, DeviceType<NUO>::code, CBG_SORTED_COLS, &C, &st),
+    check(cbg_spgemm_grid(grid, &va, &vb, DeviceSemiring<SR>::code, DeviceType<NUO>::code, CBG_SORTED_COLS, &C, &st),
           "cbg_spgemm_grid");
     UDERO* D = to_local<IU, NUO, UDERO>(C);
     return SpParMat3D<IU, NUO, UDERO>(D, G, true, false);
@@ -628,10 +699,10 @@ inline int ccgrid_rank(const CCGrid& CMG) {
   return CMG.layer_grid * CMG.GridRows * CMG.GridCols + CMG.RankInCol * CMG.GridCols + CMG.RankInRow;
 }
 
-inline void ccgrid_handle(GridHandle& h, CCGrid& CMG) {
+inline cbg_grid* ccgrid_grid(CCGrid& CMG) {
   if (CMG.GridRows != CMG.GridCols) throw std::runtime_error("3DSpGEMM: square layer grid required (3002)");
-  make_grid(h, MPI_COMM_WORLD, CMG.rowWorld, CMG.colWorld, CMG.fiberWorld, CMG.GridLayers, CMG.GridRows, CMG.GridCols,
-            ccgrid_rank(CMG));
+  return cached_grid(MPI_COMM_WORLD, CMG.rowWorld, CMG.colWorld, CMG.fiberWorld, CMG.GridLayers, CMG.GridRows,
+                     CMG.GridCols, ccgrid_rank(CMG));
 }
 
 // isBT: splitB holds B's piece locally transposed ("outer" mode of test_mpipspgemm.cpp:101-117)
@@ -649,14 +720,13 @@ void SUMMALayer(SpDCCols<IT, NT>& SplitA, SpDCCols<IT, NT>& SplitB, std::vector<
                 bool isBT, bool threaded) {
   static_assert(DeviceType<NT>::ok, "3DSpGEMM on the device: NT must be a device value type");
   (void)threaded;   // LocalSpGEMM vs MultiplyReturnTuples is a CPU choice: one device product
-  GridHandle h;
-  ccgrid_handle(h, CMG);
+  cbg_grid* grid = ccgrid_grid(CMG);
   std::unique_ptr<SpDCCols<IT, NT>> bt;
   cbg_dcsc_view va = view_of(SplitA), vb = b_view(SplitB, isBT, bt);
   std::vector<cbg_csc_result> parts(2 * CMG.GridCols + 2);
   int32_t n = 0;
   cbg_grid_stats st{};
-  check(cbg_summa_layer(h.grid, &va, &vb, CBG_SR_PLUS_TIMES, DeviceType<NT>::code, CBG_SORTED_COLS, parts.data(), &n,
+  check(cbg_summa_layer(grid, &va, &vb, CBG_SR_PLUS_TIMES, DeviceType<NT>::code, CBG_SORTED_COLS, parts.data(), &n,
                         &st), "cbg_summa_layer");
   for (int32_t k = 0; k < n; ++k) C.push_back(to_tuples<IT, NT>(context(), parts[k]));
 }
@@ -666,13 +736,12 @@ template <typename IT, typename NT>
 SpDCCols<IT, NT>* multiply(SpDCCols<IT, NT>& splitA, SpDCCols<IT, NT>& splitB, CCGrid& CMG, bool isBT, bool threaded) {
   static_assert(DeviceType<NT>::ok, "3DSpGEMM on the device: NT must be a device value type");
   (void)threaded;
-  GridHandle h;
-  ccgrid_handle(h, CMG);
+  cbg_grid* grid = ccgrid_grid(CMG);
   std::unique_ptr<SpDCCols<IT, NT>> bt;
   cbg_dcsc_view va = view_of(splitA), vb = b_view(splitB, isBT, bt);
   cbg_csc_result C{};
   cbg_grid_stats st{};
-  check(cbg_spgemm_grid(h.grid, &va, &vb, CBG_SR_PLUS_TIMES, DeviceType<NT>::code, CBG_SORTED_COLS, &C, &st),
+  check(cbg_spgemm_grid(grid, &va, &vb, CBG_SR_PLUS_TIMES, DeviceType<NT>::code, CBG_SORTED_COLS, &C, &st),
         "cbg_spgemm_grid");
   SpTuples<IT, NT>* t = to_tuples<IT, NT>(context(), C);
   SpDCCols<IT, NT>* D = new SpDCCols<IT, NT>(*t, false);

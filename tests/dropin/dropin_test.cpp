@@ -428,6 +428,23 @@ int main(int argc, char** argv) {
         delete dt; delete rc2;
       }
       delete rt;
+      // the grid is set up once per CommGrid and reused (HipMCL calls the driver every iteration): ten back-to-back
+      // Mult_AnXBn_Synch calls, per-call wall time, and the process's grid setups before / after them
+      {
+        const int before = gpu::grid_creations();
+        double tmin = 1e30, tmax = 0, tsum = 0;
+        for (int it = 0; it < 10; ++it) {
+          MPI_Barrier(MPI_COMM_WORLD);
+          const double t0 = MPI_Wtime();
+          PMI D = gpu::Mult_AnXBn_Synch<PTI, int64_t, DI>(A, B);
+          MPI_Barrier(MPI_COMM_WORLD);
+          const double t = MPI_Wtime() - t0;
+          tmin = std::min(tmin, t); tmax = std::max(tmax, t); tsum += t;
+        }
+        printf("REPEAT calls=10 setups_before=%d setups_after=%d ms_min=%.3f ms_mean=%.3f ms_max=%.3f\n", before,
+               gpu::grid_creations(), 1e3 * tmin, 1e2 * tsum, 1e3 * tmax);
+        if (gpu::grid_creations() != before) rc = 1;
+      }
       const cbg_grid_info& gi = gpu::last_grid_info();   // the grid the drivers ran over
       printf("GRID rccl=%d world=%d row=%d col=%d fiber=%d\n", gi.rccl, gi.ranks[CBG_GROUP_WORLD],
              gi.ranks[CBG_GROUP_ROW], gi.ranks[CBG_GROUP_COL], gi.ranks[CBG_GROUP_FIBER]);

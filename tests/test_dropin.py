@@ -78,6 +78,12 @@ def test_dropin_distributed_drivers_4_ranks_on_gpu(transport):
         pytest.skip("dropin_test or MPICH's mpirun not available")
     r = subprocess.run(mpi_cmd(4, [], transport), capture_output=True, text=True, timeout=150)
     assert r.returncode == 0 and r.stdout.count("DROPIN OK") == 4, r.stdout + r.stderr
+    # ten more Mult_AnXBn_Synch calls on the same CommGrid set up no communicator (the grid is cached)
+    reps = [line for line in r.stdout.splitlines() if line.startswith("REPEAT")]
+    import re
+    setups = [re.search(r"setups_before=(\d+) setups_after=(\d+)", x).groups() for x in reps]
+    assert len(reps) == 4 and all(b == a for b, a in setups), reps
+    print("\n".join(reps))
     assert_grid(r.stdout, 4, 2, 1, transport)
 
 

@@ -8,6 +8,8 @@
 #   dist:<N>:<scale>   N ranks on this one GPU over libcbgpu's RCCL grid (RCCL sockets), verified bench line
 #   share:<N>:<scale>  every rank's share of the N-GPU layout at full size, verified (bench.py --rank-share)
 #   codec:<scale>      the fiber wire codec on the 1x1x2 message (tools/bench_codec.py) + its rocprofv3 kernel stats
+#   shareprof:<N>:<s>  rocprofv3 kernel stats of rank 0's share of the N-GPU layout at scale s
+#   var:<a,b,..>:<s>   tuning variants tools/var/<name>/libcbgpu.so on the N = 1 bench at scale s (var_bench.py)
 #   prof               rocprofv3 kernel stats of the bench (5 timed products)
 #   pmc                heavy-kernel and whole-product HBM bytes (tools/pmc_heavy.py, one counter per pass)
 #   sq                 SQ limiter counters (two groups) over one product
@@ -25,7 +27,7 @@ for step in "$@"; do
   case $kind in
     tests)
       if [ -n "${a:-}" ]; then K=(-k "$a"); else K=(); fi
-      timeout -k 10 1000 python -u -m pytest tests -m gpu -v "${K[@]}" --timeout 300 --timeout-method thread \
+      timeout -k 10 1000 python -u -m pytest tests -m gpu -v -rA "${K[@]}" --timeout 300 --timeout-method thread \
         > "$OUT/gpu_tests${a:+_$a}.log" 2>&1
       rc=$?; tail -2 "$OUT/gpu_tests${a:+_$a}.log"
       [ $rc -eq 0 ] || { grep -E "^(FAILED|ERROR)|Error" "$OUT/gpu_tests${a:+_$a}.log" | head -20; fail "$step" $rc; } ;;
@@ -51,6 +53,15 @@ for step in "$@"; do
       cut -c1-600 "$OUT/codec_s${a:-21}.json"
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/codec_prof" -o run -- \
         python3 tools/bench_codec.py --scale "${a:-21}" --reps 1 > "$OUT/codec_prof.log" 2>&1 || { tail -5 "$OUT/codec_prof.log"; fail "$step" 2; } ;;
+    shareprof)
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/shareprof_s${b}_n${a}" -o run -- \
+        python3 bench.py --rank-share 0 --gpus-virtual "$a" --scale "$b" > "$OUT/shareprof_s${b}_n${a}.log" 2>&1 || \
+        { tail -8 "$OUT/shareprof_s${b}_n${a}.log"; fail "$step" 1; }
+      grep '^{' "$OUT/shareprof_s${b}_n${a}.log" | cut -c1-300 ;;
+    var)
+      timeout -k 10 600 python3 -u tools/var_bench.py ${a//,/ } -- --no-cpu --steps 3 --scale "${b:-20}" \
+        > "$OUT/var_s${b:-20}.log" 2>&1 || { tail -5 "$OUT/var_s${b:-20}.log"; fail "$step" 1; }
+      cut -c1-400 "$OUT/var_s${b:-20}.log" ;;
     prof)
       timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
         python3 bench.py --steps 5 --warmup 2 --no-cpu > "$OUT/prof.log" 2>&1 || { tail -20 "$OUT/prof.log"; fail prof 1; }
