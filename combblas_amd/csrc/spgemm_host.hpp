@@ -187,6 +187,7 @@ struct cbg_ctx {
   DevBuf nunits, segsz, segoff, useg, icnt, itemoff, items, parts, wide_win;
   DevBuf hrows, hmode, hpoff, urows;   // symbolic -> numeric row handoff of heavy columns
   DevBuf oitems;                       // heavy items the rows-known kernel does not take
+  DevBuf ptab;                         // A's part table for k_sym_part (k_part_table)
   DevBuf aos;                          // A's rows and values interleaved (k_num_heavy_known gathers)
   DevBuf gal[9];                       // fused Galerkin product scratch (galerkin.hip)
   void* pin = nullptr;                 // 16 KB of pinned host memory: small read-backs (bin counts, scalars)
@@ -205,7 +206,7 @@ inline void release_workspace(cbg_ctx* c) {
                     &c->ovf_list, &c->split_idx, &c->long_cols, &c->split_tab, &c->heavy_cols, &c->sub, &c->units,
                     &c->ucnt, &c->uspan, &c->ulist, &c->fb_units, &c->fb_list, &c->uovf_list, &c->nunits, &c->segsz,
                     &c->segoff, &c->useg, &c->icnt, &c->itemoff, &c->items, &c->parts, &c->wide_win, &c->hrows,
-                    &c->hmode, &c->hpoff, &c->urows, &c->oitems, &c->aos})
+                    &c->hmode, &c->hpoff, &c->urows, &c->oitems, &c->aos, &c->ptab})
     b->release();
   for (DevBuf& b : c->stageA) b.release();
   for (DevBuf& b : c->stageB) b.release();
@@ -605,7 +606,7 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
     }
   }
   // split table (unit segments, wide-column parts): needed whenever a column can be heavy
-  Split spl{ctx->split_idx.as<int32_t>(), nullptr, nsub, slog, nullptr, nullptr, nullptr};
+  Split spl{ctx->split_idx.as<int32_t>(), nullptr, nsub, slog, nullptr, nullptr, nullptr, nullptr, 0};
   if (hcap > 0) {
     HIPCHK(ctx->split_tab.reserve(sizeof(int32_t) * ((int64_t)NL * (nsub + 1) + 1)));
     spl.tab = ctx->split_tab.as<int32_t>();
@@ -642,6 +643,20 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
       HIPCHK(ctx->parts.reserve(sizeof(PartItem) * (nwide * kMaxParts + 1)));
       HIPCHK(ctx->wide_win.reserve(sizeof(int32_t) * (nwide + 1)));
       cap.add(ctx->parts, "parts"); cap.add(ctx->wide_win, "wide_win");
+      // the part table of A (k_part_table), unless it would not fit comfortably (CBG_PART_TABLE=0: off)
+      static const bool ptab_env = [] { const char* x = std::getenv("CBG_PART_TABLE"); return !(x && x[0] == '0'); }();
+      const int32_t P = (int32_t)(((M - 1) >> kPartLog) + 1);
+      const size_t pbytes = sizeof(int32_t) * ((size_t)A.ncol * (P + 1) + 1);
+      size_t pfree = 0, ptot = 0;
+      if (ptab_env && P > 1 && A.ncol > 0 &&
+          (pbytes <= ctx->ptab.n || (hipMemGetInfo(&pfree, &ptot) == hipSuccess && pbytes < pfree / 8))) {
+        HIPCHK(ctx->ptab.reserve(pbytes));
+        cap.add(ctx->ptab, "ptab");
+        k_part_table<<<(int)grid_for(A.ncol, 256, kMaxGrid * 4), 256, 0, st>>>(A.ncol, A.cp, A.ir, P,
+                                                                                 ctx->ptab.as<int32_t>());
+        spl.ptab = ctx->ptab.as<int32_t>();
+        spl.pstride = P + 1;
+      }
       CAPCHK(cap);
       int *nparts = si + 8, *nwin = si + 9;
       k_part_items<<<(int)grid_for(nwide, 256, kMaxGrid), 256, 0, st>>>(L(kWideClass), nwide, slog <= kPartLog ? kMaxParts : 0, span, ho,

@@ -128,6 +128,8 @@ struct Split {
   const UnitSeg* useg;  // precomputed unit segments (k_unit_segs)
   const int32_t* hrows; // sorted output rows of heavy columns written by the symbolic pass (or null)
   const UnitRows* urows;// per unit: where its rows lie in hrows (k_build_units)
+  const int32_t* ptab;  // part table (k_part_table): ptab[k*pstride + p] = (first entry with row >= p*2^kPartLog) - cp[k]
+  int32_t pstride;      // parts of the row space + 1 (0: no table)
 };
 
 struct Unit {
@@ -1176,7 +1178,11 @@ k_sym_part(const PartItem* __restrict__ items, const int* __restrict__ count_dev
     auto seg = [&](int64_t b, int64_t& a0, int64_t& a1, uint8_t&) {
       const int32_t k = Bir[b];
       const int64_t c0 = Acp[k], c1 = Acp[k + 1];
-      if (c1 - c0 >= kSplitMin) {
+      if (spl.ptab) {   // every A column narrowed to the part's rows: no gathers of rows outside it
+        const int32_t* t = spl.ptab + (int64_t)k * spl.pstride + ((sp.x >> kPartLog) + it.p);
+        a0 = c0 + t[0];
+        a1 = c0 + t[1];
+      } else if (c1 - c0 >= kSplitMin) {
         const int32_t* t = spl.tab + (int64_t)spl.idx[k] * (spl.nsub + 1);
         a0 = c0 + t[s0];
         a1 = c0 + t[s1];
@@ -1274,6 +1280,34 @@ k_sym_part(const PartItem* __restrict__ items, const int* __restrict__ count_dev
     __syncthreads();
     STAMP(29);
     STAMP_COUNT(30, 1);
+  }
+}
+
+// Part table of A for k_sym_part: for every A column the entry offsets of the 2^kPartLog-row part boundaries (P + 1 per
+// column), so a part's item gathers only the rows inside the part -- without it a short column (no split-table row) is
+// read whole by every part of every wide column it feeds (8 parts at 2^21 rows).  One thread per column: a linear walk
+// over a short column's sorted rows, binary searches in a long one.
+__global__ void __launch_bounds__(256) k_part_table(int64_t ncol, const int64_t* __restrict__ Acp,
+                                                    const int32_t* __restrict__ Air, int32_t P, int32_t* __restrict__ ptab) {
+  for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < ncol; k += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t c0 = Acp[k], c1 = Acp[k + 1];
+    int32_t* t = ptab + k * (P + 1);
+    t[0] = 0;
+    if (c1 - c0 <= 64) {
+      int64_t i = c0;
+      for (int p = 1; p < P; ++p) {
+        const int64_t lim = (int64_t)p << kPartLog;
+        while (i < c1 && Air[i] < lim) ++i;
+        t[p] = (int32_t)(i - c0);
+      }
+    } else {
+      int64_t i = c0;
+      for (int p = 1; p < P; ++p) {
+        i = lower_bound_rows(Air, i, c1, (int64_t)p << kPartLog);
+        t[p] = (int32_t)(i - c0);
+      }
+    }
+    t[P] = (int32_t)(c1 - c0);
   }
 }
 
@@ -2458,12 +2492,14 @@ __global__ void __launch_bounds__(NT) k_num_heavy_known(const KnownUnit* __restr
   const SegBuf<V> sb{qb, off, bvs, scr, lens};
   const int tid = threadIdx.x;
   const int64_t n = (int64_t)*nku;
-  // units k (current), k1 (next: header and rows in flight), k2 (claimed during unit k, header prefetched)
+  // units k (current), k1 (next: header and rows in flight), k2 (claimed one unit earlier, header loaded during unit
+  // k); with the ticket, unit k3 is claimed at the top of unit k and its number published at the end of it, so the
+  // atomic's round trip is never waited on
 #if CBG_HEAVY_DYNAMIC
   __shared__ unsigned long long s_claim;
-  if (tid == 0) s_claim = atomicAdd(ticket, 2ull);
+  if (tid == 0) s_claim = atomicAdd(ticket, 3ull);
   __syncthreads();
-  int64_t k = (int64_t)s_claim, k1 = k + 1;
+  int64_t k = (int64_t)s_claim, k1 = k + 1, k2 = k + 2;
 #else
   const int64_t G = gridDim.x;
   int64_t k = blockIdx.x, k1 = k + G;
@@ -2538,7 +2574,8 @@ __global__ void __launch_bounds__(NT) k_num_heavy_known(const KnownUnit* __restr
     const KnownUnit H = hdr[slot];
     const bool has1 = k1 < n;
 #if CBG_HEAVY_DYNAMIC
-    if (tid == 0) s_claim = atomicAdd(ticket, 1ull);   // read after the barrier closing step a
+    unsigned long long k3 = 0;
+    if (tid == 0) k3 = atomicAdd(ticket, 1ull);   // published at the end of this unit
 #endif
     const int32_t lo = __builtin_amdgcn_readfirstlane(H.lo), hi = __builtin_amdgcn_readfirstlane(H.hi);
     const int32_t cnt = __builtin_amdgcn_readfirstlane(H.cnt);
@@ -2562,10 +2599,10 @@ __global__ void __launch_bounds__(NT) k_num_heavy_known(const KnownUnit* __restr
         }
       }
     }
+    STAMP(6);
     __syncthreads();
-#if CBG_HEAVY_DYNAMIC
-    const int64_t k2 = (int64_t)s_claim;
-#else
+    STAMP(7);
+#if !CBG_HEAVY_DYNAMIC
     const int64_t k2 = k + 2 * G;
 #endif
     const bool has2 = k2 < n;
@@ -2580,7 +2617,9 @@ __global__ void __launch_bounds__(NT) k_num_heavy_known(const KnownUnit* __restr
         atomicOr(&bm[o >> 5], 1u << (o & 31));
       }
     }
+    STAMP(8);
     if (has1) load_rows(hdr[slot ^ 1]);   // next unit's rows: in flight during the sweep
+    STAMP(9);
     __syncthreads();
     STAMP(2);
     // c. one sweep over the unit's multiplies
@@ -2638,12 +2677,19 @@ __global__ void __launch_bounds__(NT) k_num_heavy_known(const KnownUnit* __restr
     }
     // d. values out, row order
     for (int i = tid; i < cnt; i += NT) out.val[H.outoff + i] = SRT::out(vals[i], A.val, B.val);
+    STAMP(10);
     if (tid < kKnownWords && has2) hw[slot * kKnownWords + tid] = nh;
     if (has1) put_bnd();
+#if CBG_HEAVY_DYNAMIC
+    if (tid == 0) s_claim = k3;
+#endif
     __syncthreads();
     STAMP(5);
     k = k1;
     k1 = k2;
+#if CBG_HEAVY_DYNAMIC
+    k2 = (int64_t)s_claim;   // k3: published before the barrier above; rewritten only after the next one
+#endif
   }
 }
 

@@ -5,7 +5,10 @@ Per rank: the panel broadcasts (its A and B panels less the pieces it owns, over
 the fiber pipeline -- the other layer's column half multiplied in C chunks, each chunk's message sent as soon as it
 is made while the next chunk and then the own half multiply (one link per direction, the partner's message arriving
 on the same schedule) -- then the decode of the received message and the merge; one-layer grids multiply once.
-The step is the slowest rank's; the value is the multiplies of all ranks over it.
+The step is the slowest rank's; the value is the multiplies of all ranks over it.  When the record carries the
+production codec's measurement (`fiber_codec`, cbg_fiber_codec on the same message), its encode time is added to the
+compute stream (the pipeline encodes each chunk between the products) and its decode time replaces the decode model.
+A file holding several workloads (tools/rank_share_configs.py) is predicted per (config, layout).
 
 usage: python tools/predict_scaling.py profiles/r04l_rank_share_s22_n8.jsonl [--link-GBps 64] [--chunks 2]
 """
@@ -24,8 +27,11 @@ def rank_step(rec, link_gbps, chunks, decode_gbps=5000.0, entry_bytes=12):
     ph = rec["phases_ms"]
     if L == 1 or not rec.get("fiber"):
         compute = sum(p["total_ms"] for p in ph)
-        return bcast + compute, {"bcast": bcast, "compute": compute, "fiber_exposed": 0.0, "decode": 0.0, "merge": 0.0}
-    t_other, t_mine = ph[0]["total_ms"], ph[1]["total_ms"]
+        return bcast + compute, {"bcast": bcast, "compute": compute, "encode": 0.0, "fiber_exposed": 0.0, "decode": 0.0,
+                                 "merge": 0.0}
+    codec = rec.get("fiber_codec") or {}
+    enc = float(codec.get("encode_ms", 0.0))
+    t_other, t_mine = ph[0]["total_ms"] + enc, ph[1]["total_ms"]
     wire = rec["fiber"]["bytes"]
     x = wire / chunks / bw
     send_end = 0.0
@@ -33,12 +39,13 @@ def rank_step(rec, link_gbps, chunks, decode_gbps=5000.0, entry_bytes=12):
         send_end = max(c * t_other / chunks, send_end) + x
     compute_end = t_other + t_mine
     fiber_exposed = max(0.0, send_end - compute_end)
-    # decode: read the wire bytes, write the piece's rows and values
-    decode = (wire + rec.get("recv_nnz", 0) * entry_bytes) / (decode_gbps * 1e9 / 1e3)
+    # decode: the measured codec, else read the wire bytes and write the piece's rows and values at decode_gbps
+    decode = float(codec["decode_ms"]) if "decode_ms" in codec else \
+        (wire + rec.get("recv_nnz", 0) * entry_bytes) / (decode_gbps * 1e9 / 1e3)
     merge = rec["merge_ms"]
     total = bcast + compute_end + fiber_exposed + decode + merge
-    return total, {"bcast": bcast, "compute": compute_end, "fiber_exposed": fiber_exposed, "decode": decode,
-                   "merge": merge}
+    return total, {"bcast": bcast, "compute": compute_end, "encode": enc, "fiber_exposed": fiber_exposed,
+                   "decode": decode, "merge": merge}
 
 
 def predict(records, link_gbps=64.0, chunks=2):
@@ -46,7 +53,8 @@ def predict(records, link_gbps=64.0, chunks=2):
     worst = max(range(len(steps)), key=lambda i: steps[i][0])
     mult = sum(r["multiplies"] for r in records)
     ms = steps[worst][0]
-    return {"ranks": len(records), "layout": records[0]["layout"], "scale": records[0]["scale"],
+    return {"ranks": len(records), "layout": records[0]["layout"], "workload": records[0].get("config",
+                                                                                              records[0].get("scale")),
             "link_GBps": link_gbps, "chunks": chunks, "step_ms": round(ms, 2),
             "multiplies": mult, "multiplies_per_s": mult / (ms / 1e3),
             "slowest_rank": records[worst]["rank"], "parts_ms": {k: round(v, 2) for k, v in steps[worst][1].items()}}
@@ -59,7 +67,11 @@ def main():
     ap.add_argument("--chunks", type=int, default=2)
     a = ap.parse_args()
     recs = [json.loads(l) for l in open(a.jsonl) if l.startswith("{")]
-    print(json.dumps(predict(recs, a.link_GBps, a.chunks)))
+    groups = {}
+    for r in recs:
+        groups.setdefault((r.get("config", ""), r["layout"]), []).append(r)
+    for g in groups.values():
+        print(json.dumps(predict(g, a.link_GBps, a.chunks)))
 
 
 if __name__ == "__main__":

@@ -1,0 +1,193 @@
+#!/usr/bin/env python3
+"""Every rank's share of the 2/4/8-GPU layouts (1x1x2, 2x2, 2x2x2) for BASELINE configs 4 and 5, at full
+size on one GPU -- the real-valued counterparts of `bench.py --rank-share` (R-MAT, multiplicity values).
+
+  config 4  HipMCL expansion A*A of the protein-similarity-like graph (combblas_amd.inputs, n = 2^20 by default)
+  config 5  Galerkin R^T A then (R^T A) R: A = 3D Poisson 7-point on k^3 (k = 128), R = the reference's
+            RestrictionOp (device), as RestrictionOp.cpp:188-196 multiplies
+
+Rank (l, i, j) gets the panels the panel schedule's broadcasts deliver: A(rows_i, K_l) and B(K_l, cols_j), K_l the
+layer-l part of every inner block; with two layers it multiplies the other layer's column half, runs the production
+fiber codec on that message (cbg_fiber_codec: the bytes on the link, bit-exact round trip), multiplies its own half,
+and merges with the partner's message (the partner's product of this half, made here).  The merged piece is checked
+against a one-GPU product A(rows_i, :) * B(:, J_sample) of a seeded column sample: identical structure, values within
+1e-12 of the |A| * |B| bound (PlusTimes<double>: accumulation order differs), plus the symbolic pass's nnz of the
+whole piece.  One JSON line per (config, N, rank); tools/predict_scaling.py turns them into step predictions.
+usage: python tools/rank_share_configs.py [--configs 4,5] [--gpus 2,4,8] [--mcl-n N] [--poisson-k K]"""
+import argparse
+import json
+import os
+import sys
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(HERE))
+
+import numpy as np  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--configs", default="4,5")
+    ap.add_argument("--gpus", default="2,4,8")
+    ap.add_argument("--mcl-n", type=int, default=1 << 20)
+    ap.add_argument("--poisson-k", type=int, default=128)
+    ap.add_argument("--chunks", type=int, default=int(os.environ.get("CBG_FIBER_CHUNKS", "2")))
+    args = ap.parse_args()
+    import tempfile
+    import torch
+    import torch.distributed as dist
+    import combblas_amd as cb
+    from combblas_amd import dist as cbd
+    from combblas_amd.inputs import poisson3d, protein_like_graph
+    import bench
+
+    store = tempfile.NamedTemporaryFile(delete=False)
+    dist.init_process_group("gloo", init_method=f"file://{store.name}", rank=0, world_size=1)
+    ctx = cb.Context(0)
+    be = cbd.GpuBackend(ctx)
+    SR = cb.PlusTimesSRing("f64")
+    dev = be.device
+
+    def host_block(M, r0, r1, c0, c1):
+        nrow, ncol, cp, ir, val = M
+        lcp, lir, lval = cbd.slice_csc(cp, ir, val, r0, r1, c0, c1)
+        return cbd.block_from_host(r1 - r0, c1 - c0, lcp, lir, lval, dev)
+
+    def panels(Am, Bm, q, L, l, i, j):
+        """A(rows_i, K_l) (pieces side by side) and B(K_l, cols_j) (pieces stacked): the panel schedule's operands."""
+        kin = Am[1]
+        r0, r1 = cbd.block_range(Am[0], q, i)
+        c0, c1 = cbd.block_range(Bm[1], q, j)
+        ks = [cbd.piece_range(kin, q, L, k, l) for k in range(q)]
+        AP = bench._hcat([host_block(Am, r0, r1, k0, k1) for (k0, k1) in ks])
+        BP = bench._vstack([host_block(Bm, k0, k1, c0, c1) for (k0, k1) in ks])
+        return AP, BP
+
+    def abs_block(b):
+        return cbd.Block(b.nrow, b.ncol, b.cp, b.ir, b.val.abs())
+
+    def check(M, Am, Bm, r0, r1, c0, c1, nsample, seed):
+        """The rank's merged piece against an independent one-GPU product of sampled columns."""
+        Arow = host_block(Am, r0, r1, 0, Am[1])
+        Bcol = host_block(Bm, 0, Bm[0], c0, c1)
+        est_m, est_z = be.estimate(Arow, Bcol)
+        k = min(M.ncol, int(nsample))
+        g = torch.Generator().manual_seed(int(seed))
+        sel = torch.randperm(M.ncol, generator=g)[:k].sort().values
+        Bs = bench.select_block_cols(Bcol, sel)
+        P = be.multiply(Arow, Bs, SR)
+        Pabs = be.multiply(abs_block(Arow), abs_block(Bs), SR)
+        S = bench.select_block_cols(M, sel)
+        same = P.nnz == S.nnz and torch.equal(P.cp, S.cp) and torch.equal(P.ir, S.ir)
+        err = float(((P.val - S.val).abs() / torch.clamp(Pabs.val, min=1e-300)).max().item()) if same and P.nnz else 0.0
+        return {"sampled_columns": k, "sample_nnz": P.nnz, "structure_equal": bool(same),
+                "max_rel_err_vs_abs_bound": err, "within_1e-12": bool(same and err <= 1e-12),
+                "piece_nnz": M.nnz, "piece_nnz_equals_estimate": M.nnz == est_z, "piece_multiplies_estimate": est_m}
+
+    def run(label, Am, Bm, N, extra):
+        L, q, _ = cbd.grid_for(N)
+        bad = False
+        for r in range(N):
+            l, rem = divmod(r, q * q)
+            i, j = divmod(rem, q)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            AP, BP = panels(Am, Bm, q, L, l, i, j)
+            build_s = time.perf_counter() - t0
+            nc = BP.ncol
+            halves = [cbd.block_range(nc, L, m) for m in range(L)]
+            me, other = (l, 1 - l) if L == 2 else (0, None)
+            rec = {"config": label, "rank": r, "layout": f"{L}x{q}x{q}", "l_i_j": [l, i, j], **extra,
+                   "nnz_A_panel": AP.nnz, "nnz_B_panel": BP.nnz, "panel_build_s": round(build_s, 3)}
+            for rep in range(2):   # the second repetition is recorded
+                st = {}
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                if L == 2:
+                    Po = be.multiply(AP, bench._col_slice_block(BP, *halves[other]), SR, st)
+                    t1 = time.perf_counter()
+                    p_other = ctx.last_profile()
+                    codec = be.fiber_codec(Po, args.chunks) if rep == 1 else None
+                    del Po
+                    torch.cuda.synchronize()
+                    t2 = time.perf_counter()
+                    Pm = be.multiply(AP, bench._col_slice_block(BP, *halves[me]), SR, st)
+                    t3 = time.perf_counter()
+                    p_mine = ctx.last_profile()
+                    PA, PB = panels(Am, Bm, q, L, other, i, j)
+                    Pr = be.multiply(PA, bench._col_slice_block(PB, *halves[me]), SR)
+                    del PA, PB
+                    torch.cuda.synchronize()
+                    t4 = time.perf_counter()
+                    M = be.merge([Pm, Pr] if me == 0 else [Pr, Pm], SR)
+                    torch.cuda.synchronize()
+                    t5 = time.perf_counter()
+                    local_ms, merge_ms = 1e3 * ((t1 - t0) + (t3 - t2)), 1e3 * (t5 - t4)
+                    rec["recv_nnz"] = Pr.nnz
+                    profs = [p_other, p_mine]
+                    del Pm, Pr
+                else:
+                    M = be.multiply(AP, BP, SR, st)
+                    torch.cuda.synchronize()
+                    local_ms, merge_ms, codec = 1e3 * (time.perf_counter() - t0), 0.0, None
+                    profs = [ctx.last_profile()]
+                final = M if rep == 1 else None
+                del M
+                torch.cuda.empty_cache()
+            del AP, BP
+            r0, r1 = cbd.block_range(Am[0], q, i)
+            b0, _ = cbd.block_range(Bm[1], q, j)
+            h0, h1 = halves[me]
+            v = check(final, Am, Bm, r0, r1, b0 + h0, b0 + h1, max(int(np.ceil(1e4 / N)), final.ncol // 64),
+                      7919 * r + 11)
+            del final
+            torch.cuda.empty_cache()
+            rec.update({"multiplies": st.get("multiplies", 0), "local_ms": round(local_ms, 3),
+                        "merge_ms": round(merge_ms, 3), "verified": v,
+                        "phases_ms": [{k: round(float(pp[k]), 3) for k in
+                                       ("flops_ms", "bin_ms", "symbolic_ms", "scan_ms", "numeric_ms", "heavy_ms",
+                                        "total_ms")} for pp in profs],
+                        "fiber_codec": codec,
+                        "fiber": None if codec is None else {"bytes": codec["wire_bytes"],
+                                                            "bytes_per_entry": round(codec["wire_bytes"] /
+                                                                                     max(codec["entries"], 1), 3)}})
+            print(json.dumps(rec), flush=True)
+            bad = bad or not (v["within_1e-12"] and v["piece_nnz_equals_estimate"]
+                              and (codec is None or codec["roundtrip_exact"]))
+        return bad
+
+    bad = False
+    gpus = [int(x) for x in args.gpus.split(",")]
+    for c in [int(x) for x in args.configs.split(",")]:
+        if c == 4:
+            t0 = time.perf_counter()
+            n, cp, ir, val = protein_like_graph(args.mcl_n, seed=1)
+            A = (n, n, cp, ir, val)
+            extra = {"graph_n": n, "nnz": int(cp[-1]), "gen_s": round(time.perf_counter() - t0, 1)}
+            for N in gpus:
+                bad |= run("4: HipMCL expansion A*A", A, A, N, extra)
+        elif c == 5:
+            n, acp, air, aval = poisson3d(args.poisson_k)
+            dA = cb.SpDCCols.from_csc(ctx, n, n, acp, air, aval)
+            dR, dRt = cb.RestrictionOp(dA)
+            R = (n, dR.getncol()) + tuple(dR.to_host())
+            Rt = (dRt.getnrow(), n) + tuple(dRt.to_host())
+            RA = cb.LocalSpGEMMHash(SR, dRt, dA)
+            RAh = (RA.getnrow(), n) + tuple(RA.to_host())
+            for m in (dA, dR, dRt, RA):
+                m.free()
+            A = (n, n, acp, air, aval)
+            extra = {"poisson_k": args.poisson_k, "n": n, "nagg": R[1]}
+            for N in gpus:
+                bad |= run("5a: Galerkin R^T A", Rt, A, N, extra)
+                bad |= run("5b: Galerkin (R^T A) R", RAh, R, N, extra)
+    dist.destroy_process_group()
+    if os.path.exists(store.name):
+        os.unlink(store.name)
+    if bad:
+        sys.exit("rank_share_configs: a piece failed its checks")
+
+
+if __name__ == "__main__":
+    main()
