@@ -588,16 +588,17 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
     ctx->row_handoff = (e && e[0] == '0') ? 0 : 1;
   }
   const unsigned long long hbound = hh[42];
-  if (ctx->row_handoff && hcap > 0 && hbound > 0 && !SRT::kAddIsError && !symbolic_only) {
+  // (16-bit rows: needs subwindows inside 2^16-row blocks, slog <= 16, i.e. nrow <= kMaxSub * 2^16)
+  if (ctx->row_handoff && hcap > 0 && hbound > 0 && !SRT::kAddIsError && !symbolic_only && slog <= 16) {
     size_t fr = 0, tot = 0;
     HIPCHK(hipMemGetInfo(&fr, &tot));
-    const size_t need = sizeof(int32_t) * (hbound + 1);
+    const size_t need = sizeof(uint16_t) * (hbound + 1);
     if (need <= ctx->hrows.n || need < fr / 3) {
       HIPCHK(ctx->hrows.reserve(need));
       HIPCHK(ctx->hmode.reserve(sizeof(int32_t) * (hcap + 1)));
       HIPCHK(ctx->hpoff.reserve(sizeof(int64_t) * (hcap * kMaxParts + 1)));
       HIPCHK(hipMemsetAsync(ctx->hmode.p, 0, sizeof(int32_t) * (hcap + 1), st));
-      ho.rows = ctx->hrows.as<int32_t>();
+      ho.rows = ctx->hrows.as<uint16_t>();
       ho.cursor = sc + 11;
       ho.cap = hbound;
       ho.poff = ctx->hpoff.as<int64_t>();
@@ -793,7 +794,8 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
     cap.add(ctx->items, "items"); cap.add(ctx->oitems, "oitems");
     CAPCHK(cap);
     k_heavy_items_split<SRT, CBG_KNOWN_LOGT, CBG_KNOWN_NT><<<(H + 255) / 256, 256, 0, st>>>(
-        H, ctx->heavy_cols.as<int32_t>(), ctx->nunits.as<int32_t>(), units, nsub, ctx->uspan.as<int2>(), spl.urows,
+        H, ctx->heavy_cols.as<int32_t>(), ctx->nunits.as<int32_t>(), units, nsub, slog, ctx->sub.as<int32_t>(),
+        ctx->uspan.as<int2>(), spl.urows,
         B.cp, ctx->items.as<KnownUnit>(), ctx->oitems.as<HeavyItem>(), sc + 12);
     HIPCHK(hipGetLastError());
   }
@@ -1216,7 +1218,9 @@ __device__ __forceinline__ void block_col_scan2(int32_t* ca, int na, int32_t* cb
 // MODE 0: count pass (cnt[t] = heads of tile t); MODE 1: fill pass at the scanned offsets toff[t].  (A one-pass
 // variant -- tiles claimed in order, offsets by a decoupled look-back -- measured 146 ms against 36.7 for the two
 // passes at s20: the look-back chain serialises the tiles; staging the values in LDS too: 42.4 ms, r04k.)
-template <int SRI, typename V, int MODE>
+// PF: the next tile's rows (and the starts of the columns inside it) are loaded into registers while the current tile
+// merges, so a tile's chain is boundaries -> LDS -> merge path instead of boundaries -> rows -> LDS -> merge path.
+template <int SRI, typename V, int MODE, bool PF>
 __global__ void __launch_bounds__(kFlatNT) __attribute__((amdgpu_waves_per_eu(8, 8))) k_flat_merge(
     int64_t ncol, const int64_t* __restrict__ acp, const int32_t* __restrict__ air, const V* __restrict__ aval,
     const int64_t* __restrict__ bcp, const int32_t* __restrict__ bir, const V* __restrict__ bval,
@@ -1242,6 +1246,19 @@ __global__ void __launch_bounds__(kFlatNT) __attribute__((amdgpu_waves_per_eu(8,
   if (t < ntiles) {
     a0 = sa[t]; a1 = sa[t + 1]; b0 = sb[t]; b1 = sb[t + 1]; c0 = sc[t]; ce = sc[t + 1];
   }
+  constexpr int KX = (T + 1 + NT - 1) / NT;   // tile entries per thread (both runs together hold <= T + 1)
+  int32_t xr[KX];   // PF: row of tile entry y = tid + k*NT (part 0 at y < na, part 1 at y - na)
+  auto fetch = [&](int64_t A0, int64_t A1, int64_t B0, int64_t B1) {
+    const int64_t la = A1 - A0, lb = B1 - B0;
+    const bool okt = la >= 0 && lb >= 0 && la + lb <= T + 1;
+    const int fa = okt ? (int)la : 0, fn = okt ? (int)(la + lb) : 0;
+#pragma unroll
+    for (int k = 0; k < KX; ++k) {
+      const int y = tid + k * NT;
+      xr[k] = y < fa ? air[A0 + y] : y < fn ? bir[B0 + (y - fa)] : 0;
+    }
+  };
+  if (PF && t < ntiles) fetch(a0, a1, b0, b1);
   while (t < ntiles) {
     // the next tile's boundaries, loaded while this one is merged
     const int64_t tn = t + gridDim.x;
@@ -1256,6 +1273,7 @@ __global__ void __launch_bounds__(kFlatNT) __attribute__((amdgpu_waves_per_eu(8,
         cnt[t] = 0;
         ++bad;
       }
+      if (PF && tn < ntiles) fetch(na0, na1, nb0, nb1);
     } else {
       const int na = (int)ta, nb = (int)tb, n = na + nb;
       uint64_t* ka = keys;
@@ -1285,10 +1303,22 @@ __global__ void __launch_bounds__(kFlatNT) __attribute__((amdgpu_waves_per_eu(8,
         __syncthreads();
         block_col_scan2(ca, na, cb, nb, scr);
       }
-      for (int x = tid; x < na; x += NT)
-        ka[x] = ((uint64_t)(uint32_t)(multi ? ca[x] : c0) << 32) | (uint32_t)air[a0 + x];
-      for (int x = tid; x < nb; x += NT)
-        kb[x] = ((uint64_t)(uint32_t)(multi ? cb[x] : c0) << 32) | (uint32_t)bir[b0 + x];
+      if (PF) {
+#pragma unroll
+        for (int k = 0; k < KX; ++k) {   // keys[] holds part 0 at [0, na), part 1 at [na + 1, n + 1)
+          const int y = tid + k * NT;
+          if (y < n) {
+            const int32_t cy = multi ? (y < na ? ca[y] : cb[y - na]) : c0;
+            keys[y < na ? y : y + 1] = ((uint64_t)(uint32_t)cy << 32) | (uint32_t)xr[k];
+          }
+        }
+        if (tn < ntiles) fetch(na0, na1, nb0, nb1);   // in flight while this tile merges
+      } else {
+        for (int x = tid; x < na; x += NT)
+          ka[x] = ((uint64_t)(uint32_t)(multi ? ca[x] : c0) << 32) | (uint32_t)air[a0 + x];
+        for (int x = tid; x < nb; x += NT)
+          kb[x] = ((uint64_t)(uint32_t)(multi ? cb[x] : c0) << 32) | (uint32_t)bir[b0 + x];
+      }
       if (tid == 0) {
         ka[na] = ~0ull;
         kb[nb] = ~0ull;
@@ -1419,6 +1449,10 @@ cbg_status merge2_flat(cbg_ctx* ctx, const cbg_csc_result* parts, cbg_csc_result
   const int64_t dt = parts[0].nnz + parts[1].nnz;
   const char* se = std::getenv("CBG_MERGE_STAGE");   // 0: the fill pass stores from registers
   const bool stage = !se || std::atoi(se) != 0;
+  // row prefetch (k_flat_merge PF): count pass by default, fill pass too with CBG_MERGE_PF=2 (it spills a register
+  // there at 8 waves per SIMD), CBG_MERGE_PF=0 neither
+  static const int pfm = [] { const char* x = std::getenv("CBG_MERGE_PF"); return x ? std::atoi(x) : 1; }();
+  const bool pf = pfm >= 1, pf_fill = pfm >= 2;
   if (ncol >= INT32_MAX) return CBG_EINVAL;   // the staged keys carry 32-bit columns: the per-column merge runs
   std::unique_ptr<Owner> own(new Owner(ctx->pool));
   HIPCHK(own->cp.reserve(8 * (ncol + 1)));
@@ -1449,9 +1483,14 @@ cbg_status merge2_flat(cbg_ctx* ctx, const cbg_csc_result* parts, cbg_csc_result
         ncol, parts[0].colptr, parts[0].row, parts[1].colptr, parts[1].row, ntiles, sa, sb, scol);
     const int g = (int)grid_for(ntiles, 1, kMaxGrid * 8);
     unsigned long long* h = pinned<unsigned long long>(ctx, kPinMerge);   // pairs, nnz(C), disorder
-    k_flat_merge<SRI, V, 0><<<g, kFlatNT, 0, st>>>(ncol, parts[0].colptr, parts[0].row, av, parts[1].colptr,
-                                                   parts[1].row, bv, sa, sb, scol, ntiles, cnt.as<int64_t>(),
-                                                   nullptr, nullptr, nullptr, nullptr, sc, sc + 2, false);
+    if (pf)
+      k_flat_merge<SRI, V, 0, true><<<g, kFlatNT, 0, st>>>(ncol, parts[0].colptr, parts[0].row, av, parts[1].colptr,
+                                                         parts[1].row, bv, sa, sb, scol, ntiles, cnt.as<int64_t>(),
+                                                         nullptr, nullptr, nullptr, nullptr, sc, sc + 2, false);
+    else
+      k_flat_merge<SRI, V, 0, false><<<g, kFlatNT, 0, st>>>(ncol, parts[0].colptr, parts[0].row, av, parts[1].colptr,
+                                                          parts[1].row, bv, sa, sb, scol, ntiles, cnt.as<int64_t>(),
+                                                          nullptr, nullptr, nullptr, nullptr, sc, sc + 2, false);
     k_scan_tiles<<<(int)nst, 256, 0, st>>>(ntiles, cnt.as<int64_t>(), tiles.as<int64_t>());
     k_scan_sums<<<1, 1024, 0, st>>>(nst, tiles.as<int64_t>(), (int64_t*)(sc + 1));
     k_scan_apply<<<(int)nst, 256, 0, st>>>(ntiles, cnt.as<int64_t>(), tiles.as<int64_t>(), toff);
@@ -1467,10 +1506,16 @@ cbg_status merge2_flat(cbg_ctx* ctx, const cbg_csc_result* parts, cbg_csc_result
       HIPCHK(own->ir.reserve(4 * (nnz + 1)));
       HIPCHK(own->val.reserve(sizeof(V) * (nnz + 1)));
     }
-    k_flat_merge<SRI, V, 1><<<g, kFlatNT, 0, st>>>(ncol, parts[0].colptr, parts[0].row, av, parts[1].colptr,
-                                                   parts[1].row, bv, sa, sb, scol, ntiles, nullptr, toff,
-                                                   own->cp.as<int64_t>(), own->ir.as<int32_t>(), own->val.as<V>(),
-                                                   nullptr, nullptr, stage);
+    if (pf_fill)
+      k_flat_merge<SRI, V, 1, true><<<g, kFlatNT, 0, st>>>(ncol, parts[0].colptr, parts[0].row, av, parts[1].colptr,
+                                                         parts[1].row, bv, sa, sb, scol, ntiles, nullptr, toff,
+                                                         own->cp.as<int64_t>(), own->ir.as<int32_t>(), own->val.as<V>(),
+                                                         nullptr, nullptr, stage);
+    else
+      k_flat_merge<SRI, V, 1, false><<<g, kFlatNT, 0, st>>>(ncol, parts[0].colptr, parts[0].row, av, parts[1].colptr,
+                                                          parts[1].row, bv, sa, sb, scol, ntiles, nullptr, toff,
+                                                          own->cp.as<int64_t>(), own->ir.as<int32_t>(),
+                                                          own->val.as<V>(), nullptr, nullptr, stage);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(st));   // split / cnt / tiles go back to the pool on return
   }

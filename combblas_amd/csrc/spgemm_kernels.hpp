@@ -108,6 +108,9 @@ constexpr int kSplitMin = 16;      // A columns at least this long get split-tab
 constexpr int kMaxSub = 2048;      // max subwindows per column (SUBW chosen so nrow/SUBW <= kMaxSub)
 constexpr int kItemUnits = CBG_ITEM_UNITS; // units of one heavy column per workgroup item (k_num_heavy)
 constexpr int kMaxParts = 32;      // symbolic parts per wide column (wider, hypersparse columns: windowed path)
+// 2^16-row block boundaries a rows-known unit may contain: the symbolic -> numeric row handoff stores 16-bit rows and
+// a unit (<= 2^19 rows, heavy_unit_known) carries the rank where each block boundary falls (KnownUnit::thr)
+constexpr int kKnownBlk = 8;
 
 template <typename V>
 struct DevCsc {
@@ -126,7 +129,7 @@ struct Split {
   int32_t nsub;         // subwindows in the row space
   int32_t log;          // log2(SUBW)
   const UnitSeg* useg;  // precomputed unit segments (k_unit_segs)
-  const int32_t* hrows; // sorted output rows of heavy columns written by the symbolic pass (or null)
+  const uint16_t* hrows;// sorted output rows of heavy columns written by the symbolic pass, low 16 bits (or null)
   const UnitRows* urows;// per unit: where its rows lie in hrows (k_build_units)
   const int32_t* ptab;  // part table (k_part_table): ptab[k*pstride + p] = (first entry with row >= p*2^kPartLog) - cp[k]
   int32_t pstride;      // parts of the row space + 1 (0: no table)
@@ -524,7 +527,7 @@ template <class F> struct HasVec2 { static constexpr bool value = false; };   //
 template <typename V, typename IX = int64_t>
 struct SegBuf {         // LDS, NT entries each (+ scan scratch for block mode)
   IX* qb;               // segment start (A index)
-  IX* off;              // exclusive prefix of segment group counts (< A.nnz: a chunk's segments are distinct A columns)
+  IX* off;              // exclusive prefix of segment group counts of one chunk (bounded: see k_sym_part)
   V* bv;                // B value of the segment's nonzero
   int64_t* scratch;     // block mode: NT/64 + 1 entries
   int32_t* len;         // segment length (multiplies)
@@ -862,7 +865,9 @@ struct HeavyOut {       // columns with nnz > kHeavy: list + nnz per subwindow
   // into its sorted output rows, written to `rows` at an offset reserved from `cursor` (capacity `cap`,
   // an upper bound of the heavy outputs); poff[h * kMaxParts + p] = offset of relative part p (or of
   // the whole column, p = 0); mode[h] = 1 whole column in one run, 2 per part, other = unavailable.
-  int32_t* rows;
+  // Only the low 16 bits of each row are stored: the numeric pass rebuilds the high bits from the unit's
+  // per-2^16-row-block rank thresholds (KnownUnit::thr, from the subwindow counts), so the handoff is 2 B per row.
+  uint16_t* rows;
   unsigned long long* cursor;
   unsigned long long cap;
   int64_t* poff;
@@ -955,7 +960,7 @@ __global__ void __launch_bounds__(256) k_sym_wave(const int32_t* __restrict__ li
             while (wd) {
               const int b = __ffs(wd) - 1;
               wd &= wd - 1;
-              ho.rows[pos++] = base + 32 * w2 + b;
+              ho.rows[pos++] = (uint16_t)(base + 32 * w2 + b);
             }
             run += __shfl(inc, kWave - 1, kWave);
           }
@@ -1064,7 +1069,7 @@ __global__ void __launch_bounds__(NT) k_sym_block(const int32_t* __restrict__ li
             while (wd) {
               const int b = __ffs(wd) - 1;
               wd &= wd - 1;
-              ho.rows[pos++] = base + 32 * w + b;
+              ho.rows[pos++] = (uint16_t)(base + 32 * w + b);
             }
           }
         }
@@ -1132,8 +1137,9 @@ __global__ void k_part_items(const int32_t* __restrict__ list, int64_t count, in
   }
 }
 
-// Segment staging of k_sym_part: 32-bit (A.nnz < 2^31; a chunk's segments are distinct A columns, so their offsets
-// stay below A.nnz) lets four 512-thread workgroups share a CU's LDS and the kernel run at <= 64 VGPRs: 8 waves per
+// Segment staging of k_sym_part: 32-bit (A.nnz < 2^31: segment starts are A positions; the group offsets of a chunk
+// stay below NT * 2^kPartLog / kGroupSym <= 2^25 whatever B holds -- a segment is one A column narrowed to one part,
+// at most 2^kPartLog entries since A's rows ascend strictly -- so repeated rows in a B column cannot overflow) lets four 512-thread workgroups share a CU's LDS and the kernel run at <= 64 VGPRs: 8 waves per
 // SIMD instead of 6 (s20 symbolic 23.4 -> 22.1 ms, s21 80.5 -> 75.8 ms, profiles/r04e_*); 64-bit otherwise.
 template <int NT, typename IX>
 constexpr size_t sym_part_lds() {
@@ -1254,7 +1260,7 @@ k_sym_part(const PartItem* __restrict__ items, const int* __restrict__ count_dev
         while (wd) {
           const int b = __ffs(wd) - 1;
           wd &= wd - 1;
-          ho.rows[pos++] = rb + b;
+          ho.rows[pos++] = (uint16_t)(rb + b);
         }
         base += __shfl(inc, kWave - 1, kWave);
       }
@@ -1268,7 +1274,7 @@ k_sym_part(const PartItem* __restrict__ items, const int* __restrict__ count_dev
         while (wd) {
           const int b = __ffs(wd) - 1;
           wd &= wd - 1;
-          ho.rows[pos++] = r0 + 32 * (threadIdx.x * WPT + w) + b;
+          ho.rows[pos++] = (uint16_t)(r0 + 32 * (threadIdx.x * WPT + w) + b);
         }
       }
     }
@@ -2419,11 +2425,12 @@ __device__ __forceinline__ bool heavy_unit_known(const Unit& un, int2 usp, const
   const int64_t nw = (spn + 31) >> 5;
   const int64_t cpad = (un.cnt + 1) & ~1;
   return !SRT::kAddIsError && CBG_RANK_MODE && ur.np >= 1 && ur.np <= 3 && spn > T && un.cnt <= T &&
+         (usp.y >> 16) - (usp.x >> 16) <= kKnownBlk && un.cnt < 0xffff &&
          un.cnt <= known_rpt<NT>() * NT && nw <= 2 * (int64_t)T &&
          cpad * (int64_t)sizeof(Acc) + 4 * (nw + 1) <= kRankBytes;
 }
 
-// everything k_num_heavy_known needs about one unit, in one 80-byte record
+// everything k_num_heavy_known needs about one unit, in one 88-byte record
 struct KnownUnit {
   int64_t outoff;       // first output in C
   int64_t segbase;      // the unit's (unit, B nonzero) segments in Split::useg
@@ -2432,13 +2439,21 @@ struct KnownUnit {
   int32_t o1, o2;       // ranks where pieces 1 and 2 start (o1 = o2 = cnt: one piece)
   int32_t cnt, nb;      // outputs; B nonzeros of the column
   int32_t lo, hi;       // the unit's row range [lo, hi]
-  int32_t pad[2];
+  uint16_t thr[kKnownBlk]; // rank of the unit's first row in 2^16-row block (lo >> 16) + 1 + t (0xffff: none)
 };
-static_assert(sizeof(KnownUnit) == 80, "KnownUnit is 20 words");
+static_assert(sizeof(KnownUnit) == 88, "KnownUnit is 22 words");
 constexpr int kKnownWords = (int)(sizeof(KnownUnit) / 4);
 
 __device__ __forceinline__ int64_t known_row_src(const KnownUnit& H, int i) {
   return i < H.o1 ? H.roff[0] + i : i < H.o2 ? H.roff[1] + (i - H.o1) : H.roff[2] + (i - H.o2);
+}
+
+// row of rank i of the unit from its stored low 16 bits: the 2^16-row block is lo's plus the thresholds passed
+__device__ __forceinline__ int32_t known_row(const KnownUnit& H, int i, uint16_t low) {
+  int blk = H.lo >> 16;
+#pragma unroll
+  for (int t = 0; t < kKnownBlk; ++t) blk += i >= (int)H.thr[t];
+  return (blk << 16) | (int32_t)low;
 }
 
 // k_num_heavy_known: groups of CBG_GROUP_KNOWN entries, CBG_UNROLL_KNOWN groups in flight per lane
@@ -2516,11 +2531,20 @@ __global__ void __launch_bounds__(NT) k_num_heavy_known(const KnownUnit* __restr
   __syncthreads();
   int32_t rr[RPT];
   // rows i = tid + q*NT (coalesced; clamped loads)
+  // the stored low 16 bits only: the loads stay in flight during the current unit's sweep (fix_rows, which needs
+  // them, runs after it)
   auto load_rows = [&](const KnownUnit& H) {
 #pragma unroll
     for (int q = 0; q < RPT; ++q) {
       const int i = tid + q * NT;
       rr[q] = spl.hrows[known_row_src(H, i < H.cnt ? i : 0)];
+    }
+  };
+  auto fix_rows = [&](const KnownUnit& H) {   // full rows from the unit's 2^16-row block thresholds
+#pragma unroll
+    for (int q = 0; q < RPT; ++q) {
+      const int i = tid + q * NT;
+      rr[q] = known_row(H, i < H.cnt ? i : 0, (uint16_t)rr[q]);
     }
   };
   // every wave's last row per q, for the pair-boundary test of the next wave's first lane
@@ -2566,6 +2590,7 @@ __global__ void __launch_bounds__(NT) k_num_heavy_known(const KnownUnit* __restr
     const KnownUnit H0 = hdr[0];
     load_rows(H0);
     fetch(H0, 0, pa0, pa1, pbv);
+    fix_rows(H0);
     put_bnd();
     __syncthreads();
   }
@@ -2679,7 +2704,10 @@ __global__ void __launch_bounds__(NT) k_num_heavy_known(const KnownUnit* __restr
     for (int i = tid; i < cnt; i += NT) out.val[H.outoff + i] = SRT::out(vals[i], A.val, B.val);
     STAMP(10);
     if (tid < kKnownWords && has2) hw[slot * kKnownWords + tid] = nh;
-    if (has1) put_bnd();
+    if (has1) {
+      fix_rows(hdr[slot ^ 1]);
+      put_bnd();
+    }
 #if CBG_HEAVY_DYNAMIC
     if (tid == 0) s_claim = k3;
 #endif
@@ -2705,7 +2733,8 @@ constexpr size_t num_heavy_known_lds() {
 // item); list lengths -> counts[0], counts[1].  Runs after k_unit_segs (segbase).
 template <class SRT, int LOGT, int NT>
 __global__ void k_heavy_items_split(int H, const int32_t* __restrict__ cols, const int32_t* __restrict__ nunits,
-                                    const Unit* __restrict__ units, int32_t nsub, const int2* __restrict__ uspan,
+                                    const Unit* __restrict__ units, int32_t nsub, int32_t log,
+                                    const int32_t* __restrict__ sub, const int2* __restrict__ uspan,
                                     const UnitRows* __restrict__ urows, const int64_t* __restrict__ Bcp,
                                     KnownUnit* __restrict__ known, HeavyItem* __restrict__ oitems,
                                     unsigned long long* __restrict__ counts) {
@@ -2754,7 +2783,16 @@ __global__ void k_heavy_items_split(int H, const int32_t* __restrict__ cols, con
       K.nb = nb;
       K.lo = sp.x;
       K.hi = sp.y;
-      K.pad[0] = K.pad[1] = 0;
+      {   // rank thresholds of the 2^16-row blocks inside the unit (subwindows never straddle one: log <= 16)
+        int nt = 0, acc = 0;
+        int32_t blk = sp.x >> 16;
+        for (int32_t s = un.s0; s < un.s1; ++s) {
+          const int32_t sb = (int32_t)(((int64_t)s << log) >> 16);
+          while (blk < sb && nt < kKnownBlk) { K.thr[nt++] = (uint16_t)acc; ++blk; }
+          acc += sub[(int64_t)h * nsub + s];
+        }
+        for (; nt < kKnownBlk; ++nt) K.thr[nt] = 0xffff;
+      }
       known[bk++] = K;
     } else {
       if (u0 < 0) u0 = u;

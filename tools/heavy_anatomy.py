@@ -2,7 +2,12 @@
 """Anatomy of the heavy-column work at an R-MAT scale (CPU only, sampled): how many A entries the
 heavy units gather versus the useful multiplies, and how many (unit, B nonzero) segments they stage.
 
-    python tools/heavy_anatomy.py [scale] [sample_columns]
+    python tools/heavy_anatomy.py [scale] [sample_columns] [nrow_panel_log]
+
+The second section is k_sym_part's view: every wide column is swept once per 2^18-row part, each B nonzero
+staging one segment (its A column narrowed to the part by the part table); the histogram of the non-empty segment
+lengths says how many vec4 groups and gather lines one part costs.  nrow_panel_log (e.g. 21) restricts A to the
+rows of one 2x2x2 rank panel (the s22 rank-share size: 2^21 rows), as the per-rank product sees it.
 
 Mirrors the unit formation of k_build_units (spgemm_kernels.hpp): subwindows of SUBW rows, units of
 consecutive subwindows with <= UNIT_CAP outputs and a span <= SPAN_CAP rows; an A column of at least
@@ -27,6 +32,11 @@ def main():
     import combblas_amd as cb
     n, cp, ir, val = cb.generate_rmat_host(scale, 16, seed=1)
     A = sp.csc_matrix((np.ones(len(ir)), ir, cp), shape=(n, n))
+    if len(sys.argv) > 3:   # one rank panel: A(rows 0 .. 2^p - 1, :)
+        nr = 1 << int(sys.argv[3])
+        A = A[:nr, :].tocsc()
+        A.sort_indices()
+        cp, ir = A.indptr.astype(np.int64), A.indices.astype(np.int64)
     slog = 13
     while ((n - 1) >> slog) + 1 > 2048:
         slog += 1
@@ -105,6 +115,47 @@ def main():
         print(f"  G={G}: groups {groups}, gathered/group {tot['gathered'] / max(groups, 1):.2f} (fill {tot['gathered'] / max(groups * G, 1):.2f})")
     print(f"  multiplies per unit = {tot['mult'] / max(tot['units'], 1):.0f}, outputs per unit = "
           f"{tot['nnzc'] / max(tot['units'], 1):.0f}, chunks per unit = {tot['chunks'] / max(tot['units'], 1):.2f}")
+    part_anatomy(A, cp, ir, pick, C)
+
+
+def part_anatomy(A, cp, ir, pick, C, plog=18, G=4):
+    """k_sym_part's work per (wide column, part): staged segments (one per B nonzero and part), the non-empty
+    ones, their length histogram, vec4 groups and the 64-byte lines the groups touch."""
+    nrow = A.shape[0]
+    P = ((nrow - 1) >> plog) + 1
+    col = np.repeat(np.arange(A.shape[1]), np.diff(cp))
+    cnt = np.bincount(col * P + (ir >> plog), minlength=A.shape[1] * P).reshape(A.shape[1], P)
+    pos = ir - cp[col]                          # entry's position in its column
+    tot = dict(parts=0, staged=0, nonempty=0, mult=0, groups=0, lines=0, outputs=0)
+    hist = np.zeros(66, np.int64)
+    for t, j in enumerate(pick):
+        rows = C.indices[C.indptr[t]:C.indptr[t + 1]]
+        if len(rows) <= K_HEAVY:
+            continue
+        ks = ir[cp[j]:cp[j + 1]]
+        for p in range(rows[0] >> plog, (rows[-1] >> plog) + 1):
+            L = cnt[ks, p]
+            tot["parts"] += 1
+            tot["staged"] += len(ks)
+            tot["nonempty"] += int((L > 0).sum())
+            tot["mult"] += int(L.sum())
+            tot["groups"] += int(((L + G - 1) // G).sum())
+            tot["outputs"] += int(((rows >> plog) == p).sum())
+            hist += np.bincount(np.minimum(L[L > 0], 65), minlength=66)
+            # 64-byte lines: a part's entries of column k start at cp[k] + cnt[k, :p].sum()
+            start = cp[ks] + cnt[ks, :p].sum(axis=1)
+            nz = L > 0
+            tot["lines"] += int((((start[nz] + L[nz] - 1) * 4) // 64 - (start[nz] * 4) // 64 + 1).sum())
+    del pos
+    print(f"k_sym_part view ({P} parts of 2^{plog} rows over {nrow} rows):")
+    for k, v in tot.items():
+        print(f"  {k:10s} {v:14d}  per part {v / max(tot['parts'], 1):12.1f}")
+    print(f"  nonempty / staged = {tot['nonempty'] / max(tot['staged'], 1):.3f}, multiplies / nonempty segment = "
+          f"{tot['mult'] / max(tot['nonempty'], 1):.2f}, multiplies / group = {tot['mult'] / max(tot['groups'], 1):.2f}, "
+          f"lines / multiply = {tot['lines'] / max(tot['mult'], 1):.3f}, multiplies / output = "
+          f"{tot['mult'] / max(tot['outputs'], 1):.2f}")
+    Lr = np.arange(66)
+    print("  nonempty part-segment lengths:", {int(l): round(float(hist[l] / max(hist.sum(), 1)), 4) for l in Lr if hist[l]})
 
 
 if __name__ == "__main__":
