@@ -54,6 +54,7 @@ constexpr int kNumWave = 4, kNumBlock = 4;
 constexpr int kBlockNT = 512;
 constexpr int kWinNT = 256;
 constexpr int kMaxGrid = 4096;
+constexpr int64_t kSymPartGrid = kMaxGrid * 2;   // k_sym_part's largest grid (HeavyOut::chunk slack)
 // library-internal flag of spgemm_impl: stop after the symbolic pass and the scan (cbg_estimate): the result holds the
 // colptr only, nnz(C) and the multiplies are exact, no output is allocated or computed
 constexpr uint32_t kSymbolicOnly = 1u << 28;
@@ -370,7 +371,7 @@ hipError_t launch_sym_part(hipStream_t st, const PartItem* items, const int* cou
                        : (vec ? (const void*)k_sym_part<NT, true, int64_t> : (const void*)k_sym_part<NT, false, int64_t>);
   hipError_t e = launch_cfg_lds(kf, lds);
   if (e != hipSuccess) return e;
-  const int g = (int)grid_for(cap, 1, kMaxGrid * 2);
+  const int g = (int)grid_for(cap, 1, kSymPartGrid);
   if (w32 && vec)
     k_sym_part<NT, true, int32_t><<<g, NT, lds, st>>>(items, count_dev, annz, Acp, Air, Bcp, Bir, span, spl, nnz, ho);
   else if (w32)
@@ -580,7 +581,7 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
   HIPCHK(ctx->sub.reserve(sizeof(int32_t) * (hcap * nsub + 1)));
   cap.add(ctx->heavy_cols, "heavy_cols"); cap.add(ctx->sub, "sub");
   HeavyOut ho{heavy_n, ctx->heavy_cols.as<int32_t>(), ctx->sub.as<int32_t>(), nsub, slog,
-              nullptr, nullptr, 0, nullptr, nullptr};
+              nullptr, nullptr, 0, nullptr, nullptr, 0};
   // row handoff: scratch for the heavy columns' sorted rows, sized by the bound sum(min(flop, span))
   // over flop-heavy columns (k_col_stats); off if that does not fit comfortably in free memory
   if (ctx->row_handoff < 0) {
@@ -592,7 +593,12 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
   if (ctx->row_handoff && hcap > 0 && hbound > 0 && !SRT::kAddIsError && !symbolic_only && slog <= 16) {
     size_t fr = 0, tot = 0;
     HIPCHK(hipMemGetInfo(&fr, &tot));
-    const size_t need = sizeof(uint16_t) * (hbound + 1);
+    // k_sym_part reserves rows per workgroup in chunks (at most kSymPartGrid workgroups, each leaving < chunk unused);
+    // + a pad: the numeric pass reads aligned 32-bit words
+    int64_t chunk = std::min<int64_t>(16384, (int64_t)hbound / (4 * kSymPartGrid));
+    if (chunk < 512) chunk = 0;
+    const unsigned long long hcapr = hbound + (unsigned long long)(kSymPartGrid * chunk);
+    const size_t need = sizeof(uint16_t) * (hcapr + 2);
     if (need <= ctx->hrows.n || need < fr / 3) {
       HIPCHK(ctx->hrows.reserve(need));
       HIPCHK(ctx->hmode.reserve(sizeof(int32_t) * (hcap + 1)));
@@ -600,7 +606,8 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
       HIPCHK(hipMemsetAsync(ctx->hmode.p, 0, sizeof(int32_t) * (hcap + 1), st));
       ho.rows = ctx->hrows.as<uint16_t>();
       ho.cursor = sc + 11;
-      ho.cap = hbound;
+      ho.cap = hcapr;
+      ho.chunk = chunk;
       ho.poff = ctx->hpoff.as<int64_t>();
       ho.mode = ctx->hmode.as<int32_t>();
       cap.add(ctx->hrows, "hrows"); cap.add(ctx->hmode, "hmode"); cap.add(ctx->hpoff, "hpoff");
@@ -1449,9 +1456,9 @@ cbg_status merge2_flat(cbg_ctx* ctx, const cbg_csc_result* parts, cbg_csc_result
   const int64_t dt = parts[0].nnz + parts[1].nnz;
   const char* se = std::getenv("CBG_MERGE_STAGE");   // 0: the fill pass stores from registers
   const bool stage = !se || std::atoi(se) != 0;
-  // row prefetch (k_flat_merge PF): count pass by default, fill pass too with CBG_MERGE_PF=2 (it spills a register
-  // there at 8 waves per SIMD), CBG_MERGE_PF=0 neither
-  static const int pfm = [] { const char* x = std::getenv("CBG_MERGE_PF"); return x ? std::atoi(x) : 1; }();
+  // row prefetch (k_flat_merge PF) in both passes (s20 1x1x2 partials: 36.8 -> 31.7 ms, profiles/r05b_merge_pf.txt,
+  // although the fill pass spills one register at 8 waves per SIMD); CBG_MERGE_PF=1 count pass only, 0 neither
+  static const int pfm = [] { const char* x = std::getenv("CBG_MERGE_PF"); return x ? std::atoi(x) : 2; }();
   const bool pf = pfm >= 1, pf_fill = pfm >= 2;
   if (ncol >= INT32_MAX) return CBG_EINVAL;   // the staged keys carry 32-bit columns: the per-column merge runs
   std::unique_ptr<Owner> own(new Owner(ctx->pool));

@@ -872,6 +872,7 @@ struct HeavyOut {       // columns with nnz > kHeavy: list + nnz per subwindow
   unsigned long long cap;
   int64_t* poff;
   int32_t* mode;
+  int64_t chunk;        // k_sym_part: rows reserved per workgroup at a time (0: one reservation per part)
 };
 
 __device__ __forceinline__ int64_t reserve_rows(const HeavyOut& ho, int64_t n) {
@@ -1111,6 +1112,9 @@ constexpr int kPartNT = CBG_PART_NT;
 #ifndef CBG_SYM_TESTOR
 #define CBG_SYM_TESTOR 1   // k_sym_part reads a bitmap word before setting a bit (0: no-return ds_or only)
 #endif
+#ifndef CBG_SYM_PREFETCH
+#define CBG_SYM_PREFETCH 1 // k_sym_part stages the next part's first chunk while the current part runs
+#endif
 // first symbolic class (LOGT = class + 5) cut into parts: bitmaps larger than one part; every such
 // column has flop > kHeavy (2*flop > 2^(class+4) words), so the heavy lists can hold it
 constexpr int kWideClass = kPartLog - 9 > 9 ? kPartLog - 9 : 9;
@@ -1167,12 +1171,64 @@ k_sym_part(const PartItem* __restrict__ items, const int* __restrict__ count_dev
   uint8_t* bvs = (uint8_t*)(lens + NT);            // NT
   const SegBuf<uint8_t, SymIx> sb{qb, off, bvs, scr, lens};
   const int count = *count_dev;
+  const int tid = threadIdx.x;
+  // the segment [a0, a1) of B nonzero b (A column Bir[b]) inside part p0 (absolute part index) of the row space
+  auto seg_in_part = [&](int32_t k, int32_t p0, int64_t& a0, int64_t& a1) {
+    const int32_t pr0 = p0 << kPartLog;
+    const int64_t c0 = Acp[k], c1 = Acp[k + 1];
+    if (spl.ptab) {   // every A column narrowed to the part's rows: no gathers of rows outside it
+      const int32_t* t = spl.ptab + (int64_t)k * spl.pstride + p0;
+      a0 = c0 + t[0];
+      a1 = c0 + t[1];
+    } else if (c1 - c0 >= kSplitMin) {
+      const int32_t* t = spl.tab + (int64_t)spl.idx[k] * (spl.nsub + 1);
+      a0 = c0 + t[pr0 >> spl.log];
+      a1 = c0 + t[min(spl.nsub, (int32_t)(((int64_t)pr0 + (1 << kPartLog)) >> spl.log))];
+    } else if (CBG_SYM_SHORT_SEARCH) {   // short column: its rows inside the part by binary search
+      a0 = lower_bound_rows(Air, c0, c1, pr0);
+      a1 = lower_bound_rows(Air, a0, c1, (int64_t)pr0 + (1 << kPartLog));
+    } else {
+      a0 = c0;
+      a1 = c1;
+    }
+  };
+#if CBG_SYM_PREFETCH
+  // the next item's first chunk, staged across the current item in four dependent steps (header; span + B column;
+  // this thread's B row; its A segment), each issued where the previous one has long landed, so a part's chain
+  // starts from registers instead of four round trips to memory
+  PartItem nit{-1, 0, 0};
+  int32_t np0 = 0, nk = -1, plen = 0;
+  int64_t nbs = 0, nbe = 0, pa0 = 0;
+  if (blockIdx.x < count) {
+    nit = items[blockIdx.x];
+    const int2 spn = span[nit.j];
+    np0 = (spn.x >> kPartLog) + nit.p;
+    nbs = Bcp[nit.j];
+    nbe = Bcp[nit.j + 1];
+    nk = nbs + tid < nbe ? Bir[nbs + tid] : -1;
+    if (nk >= 0) {
+      int64_t a1 = 0;
+      seg_in_part(nk, np0, pa0, a1);
+      plen = (int32_t)(a1 - pa0);
+    }
+  }
+#endif
+  int64_t cbase = 0, cleft = 0;   // thread 0: this workgroup's reserved rows (HeavyOut::chunk)
   STAMP_DECL
   STAMP(31);
   for (int i = blockIdx.x; i < count; i += gridDim.x) {
+#if CBG_SYM_PREFETCH
+    const PartItem it = nit;
+    const int64_t bs = nbs, be = nbe;
+    const int64_t fa0 = pa0;   // this thread's first-chunk segment [fa0, fa0 + flen)
+    const int32_t flen = plen;
+    const int in = i + gridDim.x;
+    if (in < count) nit = items[in];     // step 1 for the next item
+#else
     const PartItem it = items[i];
-    const int2 sp = span[it.j];
     const int64_t bs = Bcp[it.j], be = Bcp[it.j + 1];
+#endif
+    const int2 sp = span[it.j];
     const int32_t r0 = ((sp.x >> kPartLog) + it.p) << kPartLog;
     const int32_t s0 = r0 >> spl.log;
     const int32_t s1 = min(spl.nsub, (int32_t)(((int64_t)r0 + (1 << kPartLog)) >> spl.log));
@@ -1182,23 +1238,14 @@ k_sym_part(const PartItem* __restrict__ items, const int* __restrict__ count_dev
     __syncthreads();
     STAMP(26);
     auto seg = [&](int64_t b, int64_t& a0, int64_t& a1, uint8_t&) {
-      const int32_t k = Bir[b];
-      const int64_t c0 = Acp[k], c1 = Acp[k + 1];
-      if (spl.ptab) {   // every A column narrowed to the part's rows: no gathers of rows outside it
-        const int32_t* t = spl.ptab + (int64_t)k * spl.pstride + ((sp.x >> kPartLog) + it.p);
-        a0 = c0 + t[0];
-        a1 = c0 + t[1];
-      } else if (c1 - c0 >= kSplitMin) {
-        const int32_t* t = spl.tab + (int64_t)spl.idx[k] * (spl.nsub + 1);
-        a0 = c0 + t[s0];
-        a1 = c0 + t[s1];
-      } else if (CBG_SYM_SHORT_SEARCH) {   // short column: its rows inside the part by binary search
-        a0 = lower_bound_rows(Air, c0, c1, r0);
-        a1 = lower_bound_rows(Air, a0, c1, (int64_t)r0 + (1 << kPartLog));
-      } else {
-        a0 = c0;
-        a1 = c1;
+#if CBG_SYM_PREFETCH
+      if (b < bs + NT) {   // the first chunk: prefetched
+        a0 = fa0;
+        a1 = fa0 + flen;
+        return;
       }
+#endif
+      seg_in_part(Bir[b], (sp.x >> kPartLog) + it.p, a0, a1);
     };
     auto ld = [&](int64_t q) { return Air[q]; };
     const RowLd4 ld4{Air, annz};
@@ -1215,6 +1262,15 @@ k_sym_part(const PartItem* __restrict__ items, const int* __restrict__ count_dev
     };
     if constexpr (VEC) for_each_multiply<NT, false, kUnrollSym, kGroupSym, uint8_t>(bs, be, sb, seg, ld4, ins);
     else for_each_multiply<NT, false, kUnrollSym, kGroupSym, uint8_t>(bs, be, sb, seg, ld, ins);
+#if CBG_SYM_PREFETCH
+    if (in < count) {   // steps 2 and 3 for the next item
+      const int2 spn = span[nit.j];
+      np0 = (spn.x >> kPartLog) + nit.p;
+      nbs = Bcp[nit.j];
+      nbe = Bcp[nit.j + 1];
+      nk = nbs + tid < nbe ? Bir[nbs + tid] : -1;
+    }
+#endif
     __syncthreads();
     STAMP(27);
     int c = 0;
@@ -1231,13 +1287,37 @@ k_sym_part(const PartItem* __restrict__ items, const int* __restrict__ count_dev
       misc[0] = ptot;
       int64_t off = -1;
       if (ho.rows && ptot > 0) {
-        off = reserve_rows(ho, ptot);
+        if (ho.chunk > 0) {   // rows from this workgroup's reservation: a global atomic every few parts, not every one
+          if (ptot > cleft) {
+            const int64_t want = max((int64_t)ptot, ho.chunk);
+            cbase = reserve_rows(ho, want);
+            cleft = cbase >= 0 ? want : 0;
+          }
+          if (cleft >= ptot) {
+            off = cbase;
+            cbase += ptot;
+            cleft -= ptot;
+          }
+        } else {
+          off = reserve_rows(ho, ptot);
+        }
         ho.poff[(int64_t)it.h * kMaxParts + it.p] = off;
         atomicOr(&ho.mode[it.h], off >= 0 ? 2 : 16);
       }
       misc[4] = (int)(off & 0xffffffff);
       misc[5] = (int)(off >> 32);
     }
+#if CBG_SYM_PREFETCH
+    if (in < count) {   // step 4 for the next item: its first-chunk segment
+      pa0 = 0;
+      plen = 0;
+      if (nk >= 0) {
+        int64_t a1 = 0;
+        seg_in_part(nk, np0, pa0, a1);
+        plen = (int32_t)(a1 - pa0);
+      }
+    }
+#endif
     __syncthreads();
     STAMP(28);
     const int64_t off = (int64_t)(uint32_t)misc[4] | ((int64_t)misc[5] << 32);
@@ -2449,13 +2529,20 @@ __device__ __forceinline__ int64_t known_row_src(const KnownUnit& H, int i) {
 }
 
 // row of rank i of the unit from its stored low 16 bits: the 2^16-row block is lo's plus the thresholds passed
-__device__ __forceinline__ int32_t known_row(const KnownUnit& H, int i, uint16_t low) {
+__device__ __forceinline__ int32_t known_row(const KnownUnit& H, int i, int32_t low) {
   int blk = H.lo >> 16;
 #pragma unroll
   for (int t = 0; t < kKnownBlk; ++t) blk += i >= (int)H.thr[t];
-  return (blk << 16) | (int32_t)low;
+  return (blk << 16) | low;
 }
 
+#ifndef CBG_TICKET_OPAQUE
+#define CBG_TICKET_OPAQUE 0
+#endif
+// CBG_NT_OUT=1: k_num_heavy_known writes C with nontemporal stores (streamed past the L2 that serves A's gathers)
+#ifndef CBG_NT_OUT
+#define CBG_NT_OUT 0
+#endif
 // k_num_heavy_known: groups of CBG_GROUP_KNOWN entries, CBG_UNROLL_KNOWN groups in flight per lane
 // (s20 f64: G=2/U=4 32.4 ms, G=4/U=2 34.5, G=1/U=8 38.1, G=8/U=1 41.4; G=4/U=3 spills)
 #ifndef CBG_UNROLL_KNOWN
@@ -2531,20 +2618,24 @@ __global__ void __launch_bounds__(NT) k_num_heavy_known(const KnownUnit* __restr
   __syncthreads();
   int32_t rr[RPT];
   // rows i = tid + q*NT (coalesced; clamped loads)
-  // the stored low 16 bits only: the loads stay in flight during the current unit's sweep (fix_rows, which needs
-  // them, runs after it)
+  // the aligned 32-bit word holding the row's stored low 16 bits: the loads stay in flight during the current unit's
+  // sweep, and fix_rows (which needs them) runs after it.  (A 16-bit load is zero-extended by a mask that the compiler
+  // places right after it, waiting for the load there; the scratch has 2 bytes of padding for the last word.)
   auto load_rows = [&](const KnownUnit& H) {
 #pragma unroll
     for (int q = 0; q < RPT; ++q) {
       const int i = tid + q * NT;
-      rr[q] = spl.hrows[known_row_src(H, i < H.cnt ? i : 0)];
+      const int64_t src = known_row_src(H, i < H.cnt ? i : 0);
+      rr[q] = *(const int32_t*)(spl.hrows + (src & ~(int64_t)1));
     }
   };
   auto fix_rows = [&](const KnownUnit& H) {   // full rows from the unit's 2^16-row block thresholds
 #pragma unroll
     for (int q = 0; q < RPT; ++q) {
       const int i = tid + q * NT;
-      rr[q] = known_row(H, i < H.cnt ? i : 0, (uint16_t)rr[q]);
+      const int ic = i < H.cnt ? i : 0;
+      const int32_t w = rr[q];
+      rr[q] = known_row(H, ic, (known_row_src(H, ic) & 1) ? (int32_t)((uint32_t)w >> 16) : (w & 0xffff));
     }
   };
   // every wave's last row per q, for the pair-boundary test of the next wave's first lane
@@ -2600,7 +2691,18 @@ __global__ void __launch_bounds__(NT) k_num_heavy_known(const KnownUnit* __restr
     const bool has1 = k1 < n;
 #if CBG_HEAVY_DYNAMIC
     unsigned long long k3 = 0;
+#if CBG_TICKET_OPAQUE
+    // through an address the compiler cannot prove uniform: the atomic optimizer's wave-aggregated form needs the old
+    // value right away (an s_waitcnt on the atomic at the top of every unit); this plain form waits only where k3 is
+    // used, at the end of the unit
+    if (tid == 0) {
+      int32_t z;
+      asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+      k3 = atomicAdd(ticket + z, 1ull);
+    }
+#else
     if (tid == 0) k3 = atomicAdd(ticket, 1ull);   // published at the end of this unit
+#endif
 #endif
     const int32_t lo = __builtin_amdgcn_readfirstlane(H.lo), hi = __builtin_amdgcn_readfirstlane(H.hi);
     const int32_t cnt = __builtin_amdgcn_readfirstlane(H.cnt);
@@ -2614,7 +2716,11 @@ __global__ void __launch_bounds__(NT) k_num_heavy_known(const KnownUnit* __restr
       const int32_t r = rr[q];
       const int32_t up = __shfl_up(r, 1, kWave);   // row i-1 within the wave
       if (i < cnt) {
+#if CBG_NT_OUT
+        __builtin_nontemporal_store(r, &out.row[H.outoff + i]);
+#else
         out.row[H.outoff + i] = r;
+#endif
         const int pr = (r - lo) >> 6;
         const int32_t p = lane ? up : (wv ? bnd[(wv - 1) * RPT + q] : (q ? bnd[(NW - 1) * RPT + q - 1] : r));
         if (i == 0 || ((p - lo) >> 6) != pr) {
@@ -2701,7 +2807,11 @@ __global__ void __launch_bounds__(NT) k_num_heavy_known(const KnownUnit* __restr
       STAMP(4);
     }
     // d. values out, row order
+#if CBG_NT_OUT
+    for (int i = tid; i < cnt; i += NT) __builtin_nontemporal_store(SRT::out(vals[i], A.val, B.val), &out.val[H.outoff + i]);
+#else
     for (int i = tid; i < cnt; i += NT) out.val[H.outoff + i] = SRT::out(vals[i], A.val, B.val);
+#endif
     STAMP(10);
     if (tid < kKnownWords && has2) hw[slot * kKnownWords + tid] = nh;
     if (has1) {
