@@ -590,7 +590,7 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
   }
   const unsigned long long hbound = hh[42];
   // (16-bit rows: needs subwindows inside 2^16-row blocks, slog <= 16, i.e. nrow <= kMaxSub * 2^16)
-  if (ctx->row_handoff && hcap > 0 && hbound > 0 && !SRT::kAddIsError && !symbolic_only && slog <= 16) {
+  if (ctx->row_handoff && hcap > 0 && hbound > 0 && !SRT::kAddIsError && !symbolic_only && (!CBG_ROWS16 || slog <= 16)) {
     size_t fr = 0, tot = 0;
     HIPCHK(hipMemGetInfo(&fr, &tot));
     // k_sym_part reserves rows per workgroup in chunks (at most kSymPartGrid workgroups, each leaving < chunk unused);
@@ -598,13 +598,13 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
     int64_t chunk = std::min<int64_t>(16384, (int64_t)hbound / (4 * kSymPartGrid));
     if (chunk < 512) chunk = 0;
     const unsigned long long hcapr = hbound + (unsigned long long)(kSymPartGrid * chunk);
-    const size_t need = sizeof(uint16_t) * (hcapr + 2);
+    const size_t need = sizeof(HRow) * (hcapr + 2);
     if (need <= ctx->hrows.n || need < fr / 3) {
       HIPCHK(ctx->hrows.reserve(need));
       HIPCHK(ctx->hmode.reserve(sizeof(int32_t) * (hcap + 1)));
       HIPCHK(ctx->hpoff.reserve(sizeof(int64_t) * (hcap * kMaxParts + 1)));
       HIPCHK(hipMemsetAsync(ctx->hmode.p, 0, sizeof(int32_t) * (hcap + 1), st));
-      ho.rows = ctx->hrows.as<uint16_t>();
+      ho.rows = ctx->hrows.as<HRow>();
       ho.cursor = sc + 11;
       ho.cap = hcapr;
       ho.chunk = chunk;

@@ -121,6 +121,18 @@ struct DevCsc {
 };
 
 // split table: for long A columns, tab[idx[k]*(nsub+1) + s] = (first entry with row >= s*SUBW) - cp[k]
+// symbolic -> numeric row handoff element: the whole row (CBG_ROWS16=0, default) or its low 16 bits (1, rebuilt by the
+// numeric pass from the unit's 2^16-row block thresholds).  The 16-bit form halves the handoff bytes (s20: 11.3 -> 5.6 GB
+// written and read) and took the symbolic pass 21.5 -> 21.3 ms, but the rebuild sits on the rows-known kernel's per-unit
+// critical path: heavy 31.2 -> 35.0 ms (profiles/r05f_rows16_ab_s20.txt)
+#ifndef CBG_ROWS16
+#define CBG_ROWS16 0
+#endif
+#if CBG_ROWS16
+typedef uint16_t HRow;
+#else
+typedef int32_t HRow;
+#endif
 struct UnitSeg;
 struct UnitRows;
 struct Split {
@@ -129,7 +141,7 @@ struct Split {
   int32_t nsub;         // subwindows in the row space
   int32_t log;          // log2(SUBW)
   const UnitSeg* useg;  // precomputed unit segments (k_unit_segs)
-  const uint16_t* hrows;// sorted output rows of heavy columns written by the symbolic pass, low 16 bits (or null)
+  const HRow* hrows;    // sorted output rows of heavy columns written by the symbolic pass, low 16 bits (or null)
   const UnitRows* urows;// per unit: where its rows lie in hrows (k_build_units)
   const int32_t* ptab;  // part table (k_part_table): ptab[k*pstride + p] = (first entry with row >= p*2^kPartLog) - cp[k]
   int32_t pstride;      // parts of the row space + 1 (0: no table)
@@ -867,7 +879,7 @@ struct HeavyOut {       // columns with nnz > kHeavy: list + nnz per subwindow
   // the whole column, p = 0); mode[h] = 1 whole column in one run, 2 per part, other = unavailable.
   // Only the low 16 bits of each row are stored: the numeric pass rebuilds the high bits from the unit's
   // per-2^16-row-block rank thresholds (KnownUnit::thr, from the subwindow counts), so the handoff is 2 B per row.
-  uint16_t* rows;
+  HRow* rows;
   unsigned long long* cursor;
   unsigned long long cap;
   int64_t* poff;
@@ -961,7 +973,7 @@ __global__ void __launch_bounds__(256) k_sym_wave(const int32_t* __restrict__ li
             while (wd) {
               const int b = __ffs(wd) - 1;
               wd &= wd - 1;
-              ho.rows[pos++] = (uint16_t)(base + 32 * w2 + b);
+              ho.rows[pos++] = (HRow)(base + 32 * w2 + b);
             }
             run += __shfl(inc, kWave - 1, kWave);
           }
@@ -1070,7 +1082,7 @@ __global__ void __launch_bounds__(NT) k_sym_block(const int32_t* __restrict__ li
             while (wd) {
               const int b = __ffs(wd) - 1;
               wd &= wd - 1;
-              ho.rows[pos++] = (uint16_t)(base + 32 * w + b);
+              ho.rows[pos++] = (HRow)(base + 32 * w + b);
             }
           }
         }
@@ -1113,7 +1125,7 @@ constexpr int kPartNT = CBG_PART_NT;
 #define CBG_SYM_TESTOR 1   // k_sym_part reads a bitmap word before setting a bit (0: no-return ds_or only)
 #endif
 #ifndef CBG_SYM_PREFETCH
-#define CBG_SYM_PREFETCH 1 // k_sym_part stages the next part's first chunk while the current part runs
+#define CBG_SYM_PREFETCH 0 // 1: k_sym_part stages the next part's first chunk while the current part runs (measured +0.5 ms at s20, r05d)
 #endif
 // first symbolic class (LOGT = class + 5) cut into parts: bitmaps larger than one part; every such
 // column has flop > kHeavy (2*flop > 2^(class+4) words), so the heavy lists can hold it
@@ -1340,7 +1352,7 @@ k_sym_part(const PartItem* __restrict__ items, const int* __restrict__ count_dev
         while (wd) {
           const int b = __ffs(wd) - 1;
           wd &= wd - 1;
-          ho.rows[pos++] = (uint16_t)(rb + b);
+          ho.rows[pos++] = (HRow)(rb + b);
         }
         base += __shfl(inc, kWave - 1, kWave);
       }
@@ -1354,7 +1366,7 @@ k_sym_part(const PartItem* __restrict__ items, const int* __restrict__ count_dev
         while (wd) {
           const int b = __ffs(wd) - 1;
           wd &= wd - 1;
-          ho.rows[pos++] = (uint16_t)(r0 + 32 * (threadIdx.x * WPT + w) + b);
+          ho.rows[pos++] = (HRow)(r0 + 32 * (threadIdx.x * WPT + w) + b);
         }
       }
     }
@@ -2539,6 +2551,11 @@ __device__ __forceinline__ int32_t known_row(const KnownUnit& H, int i, int32_t 
 #ifndef CBG_TICKET_OPAQUE
 #define CBG_TICKET_OPAQUE 0
 #endif
+// CBG_CLAIM_AHEAD=1: the rows-known kernel claims unit k+3 at the top of unit k and publishes it at the end; 0: it claims
+// unit k+2 at the top of unit k and reads it after the barrier closing step a (round 4)
+#ifndef CBG_CLAIM_AHEAD
+#define CBG_CLAIM_AHEAD 1
+#endif
 // CBG_NT_OUT=1: k_num_heavy_known writes C with nontemporal stores (streamed past the L2 that serves A's gathers)
 #ifndef CBG_NT_OUT
 #define CBG_NT_OUT 0
@@ -2597,11 +2614,16 @@ __global__ void __launch_bounds__(NT) k_num_heavy_known(const KnownUnit* __restr
   // units k (current), k1 (next: header and rows in flight), k2 (claimed one unit earlier, header loaded during unit
   // k); with the ticket, unit k3 is claimed at the top of unit k and its number published at the end of it, so the
   // atomic's round trip is never waited on
-#if CBG_HEAVY_DYNAMIC
+#if CBG_HEAVY_DYNAMIC && CBG_CLAIM_AHEAD
   __shared__ unsigned long long s_claim;
   if (tid == 0) s_claim = atomicAdd(ticket, 3ull);
   __syncthreads();
   int64_t k = (int64_t)s_claim, k1 = k + 1, k2 = k + 2;
+#elif CBG_HEAVY_DYNAMIC
+  __shared__ unsigned long long s_claim;
+  if (tid == 0) s_claim = atomicAdd(ticket, 2ull);
+  __syncthreads();
+  int64_t k = (int64_t)s_claim, k1 = k + 1;
 #else
   const int64_t G = gridDim.x;
   int64_t k = blockIdx.x, k1 = k + G;
@@ -2626,10 +2648,15 @@ __global__ void __launch_bounds__(NT) k_num_heavy_known(const KnownUnit* __restr
     for (int q = 0; q < RPT; ++q) {
       const int i = tid + q * NT;
       const int64_t src = known_row_src(H, i < H.cnt ? i : 0);
+#if CBG_ROWS16
       rr[q] = *(const int32_t*)(spl.hrows + (src & ~(int64_t)1));
+#else
+      rr[q] = spl.hrows[src];
+#endif
     }
   };
   auto fix_rows = [&](const KnownUnit& H) {   // full rows from the unit's 2^16-row block thresholds
+#if CBG_ROWS16
 #pragma unroll
     for (int q = 0; q < RPT; ++q) {
       const int i = tid + q * NT;
@@ -2637,6 +2664,7 @@ __global__ void __launch_bounds__(NT) k_num_heavy_known(const KnownUnit* __restr
       const int32_t w = rr[q];
       rr[q] = known_row(H, ic, (known_row_src(H, ic) & 1) ? (int32_t)((uint32_t)w >> 16) : (w & 0xffff));
     }
+#endif
   };
   // every wave's last row per q, for the pair-boundary test of the next wave's first lane
   const int lane = lane_id(), wv = tid / kWave;
@@ -2689,7 +2717,9 @@ __global__ void __launch_bounds__(NT) k_num_heavy_known(const KnownUnit* __restr
     STAMP(1);
     const KnownUnit H = hdr[slot];
     const bool has1 = k1 < n;
-#if CBG_HEAVY_DYNAMIC
+#if CBG_HEAVY_DYNAMIC && !CBG_CLAIM_AHEAD
+    if (tid == 0) s_claim = atomicAdd(ticket, 1ull);   // read after the barrier closing step a
+#elif CBG_HEAVY_DYNAMIC
     unsigned long long k3 = 0;
 #if CBG_TICKET_OPAQUE
     // through an address the compiler cannot prove uniform: the atomic optimizer's wave-aggregated form needs the old
@@ -2735,6 +2765,8 @@ __global__ void __launch_bounds__(NT) k_num_heavy_known(const KnownUnit* __restr
     STAMP(7);
 #if !CBG_HEAVY_DYNAMIC
     const int64_t k2 = k + 2 * G;
+#elif !CBG_CLAIM_AHEAD
+    const int64_t k2 = (int64_t)s_claim;
 #endif
     const bool has2 = k2 < n;
     uint32_t nh = 0;   // header of unit k2, written to this unit's ring slot at the end
@@ -2818,14 +2850,14 @@ __global__ void __launch_bounds__(NT) k_num_heavy_known(const KnownUnit* __restr
       fix_rows(hdr[slot ^ 1]);
       put_bnd();
     }
-#if CBG_HEAVY_DYNAMIC
+#if CBG_HEAVY_DYNAMIC && CBG_CLAIM_AHEAD
     if (tid == 0) s_claim = k3;
 #endif
     __syncthreads();
     STAMP(5);
     k = k1;
     k1 = k2;
-#if CBG_HEAVY_DYNAMIC
+#if CBG_HEAVY_DYNAMIC && CBG_CLAIM_AHEAD
     k2 = (int64_t)s_claim;   // k3: published before the barrier above; rewritten only after the next one
 #endif
   }

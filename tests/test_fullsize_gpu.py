@@ -15,6 +15,7 @@ import sys
 
 import numpy as np
 import pytest
+import torch  # noqa: F401  -- before libcbgpu starts HIP: one HIP runtime in the process (torch ships its own)
 
 import combblas_amd as cb
 from helpers import Csc, oracle_spgemm
@@ -25,16 +26,32 @@ sys.path.insert(0, os.path.dirname(HERE))
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(scope="module")
+def backend(gpu_ctx):
+    """combblas_amd.dist's device backend on a one-rank gloo group (it asks the default group for its backend)."""
+    import tempfile
+    import torch.distributed as dist
+    from combblas_amd import dist as cbd
+    made = None
+    if not dist.is_initialized():
+        made = tempfile.NamedTemporaryFile(delete=False)
+        dist.init_process_group("gloo", init_method=f"file://{made.name}", rank=0, world_size=1)
+    yield cbd.GpuBackend(gpu_ctx)
+    if made is not None:
+        dist.destroy_process_group()
+        if os.path.exists(made.name):
+            os.unlink(made.name)
+
+
 def _bits_equal(P, Q):
     import torch
     return (P.nnz == Q.nnz and torch.equal(P.cp, Q.cp) and torch.equal(P.ir, Q.ir)
             and torch.equal(P.val.view(torch.int64), Q.val.view(torch.int64)))
 
 
-def test_gpu_rmat_s20_whole_product(gpu_ctx):
+def test_gpu_rmat_s20_whole_product(gpu_ctx, backend):
     import torch
-    from combblas_amd import dist as cbd
-    be = cbd.GpuBackend(gpu_ctx)
+    be = backend
     SR = cb.PlusTimesSRing("f64")
     s, n, h = 20, 1 << 20, 1 << 19
     seed = cb.G500_SEED
@@ -77,11 +94,11 @@ def test_gpu_rmat_s20_whole_product(gpu_ctx):
     assert np.array_equal(C.val[idx].cpu().numpy(), R.val)
 
 
-def test_gpu_rmat_s22_rank_piece_2x2x2(gpu_ctx):
+def test_gpu_rmat_s22_rank_piece_2x2x2(gpu_ctx, backend):
     import torch
     import bench
     from combblas_amd import dist as cbd
-    be = cbd.GpuBackend(gpu_ctx)
+    be = backend
     SR = cb.PlusTimesSRing("f64")
     s, n = 22, 1 << 22
     L, q, _ = cbd.grid_for(8)

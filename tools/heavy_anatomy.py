@@ -32,7 +32,8 @@ def main():
     import combblas_amd as cb
     n, cp, ir, val = cb.generate_rmat_host(scale, 16, seed=1)
     A = sp.csc_matrix((np.ones(len(ir)), ir, cp), shape=(n, n))
-    if len(sys.argv) > 3:   # one rank panel: A(rows 0 .. 2^p - 1, :)
+    Bfull = A
+    if len(sys.argv) > 3:   # one rank panel: A(rows 0 .. 2^p - 1, :) times columns of the whole matrix
         nr = 1 << int(sys.argv[3])
         A = A[:nr, :].tocsc()
         A.sort_indices()
@@ -41,12 +42,13 @@ def main():
     while ((n - 1) >> slog) + 1 > 2048:
         slog += 1
     alen = np.diff(cp)
-    flop = np.bincount(np.repeat(np.arange(n), alen), weights=alen[ir], minlength=n)
+    bcp, bir = Bfull.indptr.astype(np.int64), Bfull.indices.astype(np.int64)
+    flop = np.bincount(np.repeat(np.arange(n), np.diff(bcp)), weights=alen[bir], minlength=n)
     # heavy candidates: flop > K_HEAVY (nnz(C) > K_HEAVY implies it); sample weighted by flop
     cand = np.nonzero(flop > K_HEAVY)[0]
     rng = np.random.default_rng(0)
     pick = np.sort(rng.choice(cand, size=min(ns, len(cand)), replace=False))
-    C = (A @ A[:, pick]).tocsc()
+    C = (A @ Bfull[:, pick]).tocsc()
     C.sort_indices()
     tot = dict(mult=0, gathered=0, segs=0, nonempty=0, units=0, chunks=0, nnzc=0, heavy=0, nb=0)
     hist = np.zeros(66, np.int64)   # nonempty segment lengths (64+ pooled in the last bin)
@@ -69,7 +71,7 @@ def main():
             acc += sub[s]
         if acc > 0:
             units.append((st, sl + 1))
-        ks = ir[cp[j]:cp[j + 1]]
+        ks = bir[bcp[j]:bcp[j + 1]]
         nb = len(ks)
         tot["nb"] += nb
         tot["units"] += len(units)
@@ -115,10 +117,10 @@ def main():
         print(f"  G={G}: groups {groups}, gathered/group {tot['gathered'] / max(groups, 1):.2f} (fill {tot['gathered'] / max(groups * G, 1):.2f})")
     print(f"  multiplies per unit = {tot['mult'] / max(tot['units'], 1):.0f}, outputs per unit = "
           f"{tot['nnzc'] / max(tot['units'], 1):.0f}, chunks per unit = {tot['chunks'] / max(tot['units'], 1):.2f}")
-    part_anatomy(A, cp, ir, pick, C)
+    part_anatomy(A, cp, ir, bcp, bir, pick, C)
 
 
-def part_anatomy(A, cp, ir, pick, C, plog=18, G=4):
+def part_anatomy(A, cp, ir, bcp, bir, pick, C, plog=18, G=4):
     """k_sym_part's work per (wide column, part): staged segments (one per B nonzero and part), the non-empty
     ones, their length histogram, vec4 groups and the 64-byte lines the groups touch."""
     nrow = A.shape[0]
@@ -132,7 +134,7 @@ def part_anatomy(A, cp, ir, pick, C, plog=18, G=4):
         rows = C.indices[C.indptr[t]:C.indptr[t + 1]]
         if len(rows) <= K_HEAVY:
             continue
-        ks = ir[cp[j]:cp[j + 1]]
+        ks = bir[bcp[j]:bcp[j + 1]]
         for p in range(rows[0] >> plog, (rows[-1] >> plog) + 1):
             L = cnt[ks, p]
             tot["parts"] += 1
