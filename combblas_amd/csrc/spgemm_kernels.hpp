@@ -1124,6 +1124,9 @@ constexpr int kPartNT = CBG_PART_NT;
 #ifndef CBG_SYM_TESTOR
 #define CBG_SYM_TESTOR 1   // k_sym_part reads a bitmap word before setting a bit (0: no-return ds_or only)
 #endif
+#ifndef CBG_SYM_ROWS_LDS
+#define CBG_SYM_ROWS_LDS 0 // 1: k_sym_part stages a part's rows in its (then idle) bitmap LDS and stores them coalesced
+#endif
 #ifndef CBG_SYM_PREFETCH
 #define CBG_SYM_PREFETCH 0 // 1: k_sym_part stages the next part's first chunk while the current part runs (measured +0.5 ms at s20, r05d)
 #endif
@@ -1358,7 +1361,23 @@ k_sym_part(const PartItem* __restrict__ items, const int* __restrict__ count_dev
       }
     }
 #else
-    if (off >= 0) {   // this part's sorted rows for the numeric pass (each thread: its words' rows)
+    const int ptot_u = misc[0];
+    if (CBG_SYM_ROWS_LDS && off >= 0 && ptot_u <= T) {
+      // the bitmap is in registers (wds): its LDS holds the part's rows in order, then the workgroup copies them out
+      // with consecutive lanes on consecutive rows (whole cache lines per store instruction)
+      int pos = ex;
+#pragma unroll
+      for (int w = 0; w < WPT; ++w) {
+        uint32_t wd = wds[w];
+        while (wd) {
+          const int b = __ffs(wd) - 1;
+          wd &= wd - 1;
+          tab[pos++] = (uint32_t)(r0 + 32 * (threadIdx.x * WPT + w) + b);
+        }
+      }
+      __syncthreads();
+      for (int x = threadIdx.x; x < ptot_u; x += NT) ho.rows[off + x] = (HRow)tab[x];
+    } else if (off >= 0) {   // this part's sorted rows for the numeric pass (each thread: its words' rows)
       int64_t pos = off + ex;
 #pragma unroll
       for (int w = 0; w < WPT; ++w) {
@@ -2548,17 +2567,21 @@ __device__ __forceinline__ int32_t known_row(const KnownUnit& H, int i, int32_t 
   return (blk << 16) | low;
 }
 
+// CBG_TICKET_OPAQUE=1 (default): the rows-known kernel's unit claim goes through an address the compiler cannot prove
+// uniform, so it is not rewritten into a wave-aggregated atomic that waits for its result at once (s20 heavy 31.1 ->
+// 31.0 ms, profiles/r05g_variants_s20.txt)
 #ifndef CBG_TICKET_OPAQUE
-#define CBG_TICKET_OPAQUE 0
+#define CBG_TICKET_OPAQUE 1
 #endif
 // CBG_CLAIM_AHEAD=1: the rows-known kernel claims unit k+3 at the top of unit k and publishes it at the end; 0: it claims
 // unit k+2 at the top of unit k and reads it after the barrier closing step a (round 4)
 #ifndef CBG_CLAIM_AHEAD
 #define CBG_CLAIM_AHEAD 1
 #endif
-// CBG_NT_OUT=1: k_num_heavy_known writes C with nontemporal stores (streamed past the L2 that serves A's gathers)
+// CBG_NT_OUT=1 (default): k_num_heavy_known writes C with nontemporal stores, streamed past the L2 that serves A's
+// gathers (s20 heavy 31.1 -> 30.4 ms, profiles/r05g_variants_s20.txt)
 #ifndef CBG_NT_OUT
-#define CBG_NT_OUT 0
+#define CBG_NT_OUT 1
 #endif
 // k_num_heavy_known: groups of CBG_GROUP_KNOWN entries, CBG_UNROLL_KNOWN groups in flight per lane
 // (s20 f64: G=2/U=4 32.4 ms, G=4/U=2 34.5, G=1/U=8 38.1, G=8/U=1 41.4; G=4/U=3 spills)
