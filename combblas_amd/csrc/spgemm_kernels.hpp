@@ -1125,7 +1125,7 @@ constexpr int kPartNT = CBG_PART_NT;
 #define CBG_SYM_TESTOR 1   // k_sym_part reads a bitmap word before setting a bit (0: no-return ds_or only)
 #endif
 #ifndef CBG_SYM_ROWS_LDS
-#define CBG_SYM_ROWS_LDS 0 // 1: k_sym_part stages a part's rows in its (then idle) bitmap LDS and stores them coalesced
+#define CBG_SYM_ROWS_LDS 1 // k_sym_part stages a part's rows in its (then idle) bitmap LDS and stores them coalesced (s20 symbolic 21.6 -> 20.7 ms, profiles/r05h_rows_lds_ab.txt; 0: each thread stores its own rows)
 #endif
 #ifndef CBG_SYM_PREFETCH
 #define CBG_SYM_PREFETCH 0 // 1: k_sym_part stages the next part's first chunk while the current part runs (measured +0.5 ms at s20, r05d)
