@@ -1127,6 +1127,9 @@ constexpr int kPartNT = CBG_PART_NT;
 #ifndef CBG_SYM_ROWS_LDS
 #define CBG_SYM_ROWS_LDS 1 // k_sym_part stages a part's rows in its (then idle) bitmap LDS and stores them coalesced (s20 symbolic 21.6 -> 20.7 ms, profiles/r05h_rows_lds_ab.txt; 0: each thread stores its own rows)
 #endif
+#ifndef CBG_SYM_COLLOOP
+#define CBG_SYM_COLLOOP 0  // 1: k_sym_part items are whole columns (every part swept by one workgroup)
+#endif
 #ifndef CBG_SYM_PREFETCH
 #define CBG_SYM_PREFETCH 0 // 1: k_sym_part stages the next part's first chunk while the current part runs (measured +0.5 ms at s20, r05d)
 #endif
@@ -1148,8 +1151,12 @@ __global__ void k_part_items(const int32_t* __restrict__ list, int64_t count, in
     if (np <= maxparts) {
       const int h = atomicAdd(ho.n, 1);
       ho.cols[h] = j;
+#if CBG_SYM_COLLOOP
+      items[atomicAdd(nitems, 1)] = PartItem{j, np, h};   // one item per column: k_sym_part sweeps its np parts
+#else
       const int e = atomicAdd(nitems, np);
       for (int p = 0; p < np; ++p) items[e + p] = PartItem{j, p, h};
+#endif
     } else {
       wlist[atomicAdd(nwin, 1)] = j;
     }
@@ -1231,7 +1238,30 @@ k_sym_part(const PartItem* __restrict__ items, const int* __restrict__ count_dev
   int64_t cbase = 0, cleft = 0;   // thread 0: this workgroup's reserved rows (HeavyOut::chunk)
   STAMP_DECL
   STAMP(31);
+#if CBG_SYM_COLLOOP
+  // items are columns (j, parts, h): a workgroup sweeps every part of its column, keeping each thread's first-chunk
+  // B row and A column start in registers, so a part after the first stages its segments from the part table alone
+  PartItem ci{0, 0, 0};
+  int pp = 0;
+  int64_t cbs = 0, cbe = 0, cc0 = 0;
+  int32_t ck = -1;
+  for (int i = (int)blockIdx.x - (int)gridDim.x;;) {
+    if (pp >= ci.p) {   // the next column (uniform)
+      i += gridDim.x;
+      if (i >= count) break;
+      ci = items[i];
+      pp = 0;
+      cbs = Bcp[ci.j];
+      cbe = Bcp[ci.j + 1];
+      ck = cbs + tid < cbe ? Bir[cbs + tid] : -1;
+      cc0 = ck >= 0 ? Acp[ck] : 0;
+      if (ci.p <= 0) continue;
+    }
+    const PartItem it{ci.j, pp++, ci.h};
+    const int64_t bs = cbs, be = cbe;
+#else
   for (int i = blockIdx.x; i < count; i += gridDim.x) {
+#endif
 #if CBG_SYM_PREFETCH
     const PartItem it = nit;
     const int64_t bs = nbs, be = nbe;
@@ -1239,7 +1269,7 @@ k_sym_part(const PartItem* __restrict__ items, const int* __restrict__ count_dev
     const int32_t flen = plen;
     const int in = i + gridDim.x;
     if (in < count) nit = items[in];     // step 1 for the next item
-#else
+#elif !CBG_SYM_COLLOOP
     const PartItem it = items[i];
     const int64_t bs = Bcp[it.j], be = Bcp[it.j + 1];
 #endif
@@ -1257,6 +1287,14 @@ k_sym_part(const PartItem* __restrict__ items, const int* __restrict__ count_dev
       if (b < bs + NT) {   // the first chunk: prefetched
         a0 = fa0;
         a1 = fa0 + flen;
+        return;
+      }
+#endif
+#if CBG_SYM_COLLOOP
+      if (spl.ptab && b < bs + NT) {   // the first chunk: this thread's B row and A column start are in registers
+        const int32_t* t = spl.ptab + (int64_t)ck * spl.pstride + ((sp.x >> kPartLog) + it.p);
+        a0 = cc0 + t[0];
+        a1 = cc0 + t[1];
         return;
       }
 #endif
