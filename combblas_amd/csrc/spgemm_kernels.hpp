@@ -2613,6 +2613,10 @@ __device__ __forceinline__ int32_t known_row(const KnownUnit& H, int i, int32_t 
 #endif
 // CBG_CLAIM_AHEAD=1: the rows-known kernel claims unit k+3 at the top of unit k and publishes it at the end; 0: it claims
 // unit k+2 at the top of unit k and reads it after the barrier closing step a (round 4)
+// CBG_VAL_PAIRS=1: the rows-known kernel writes 8-byte values two per 16-byte (nontemporal) store
+#ifndef CBG_VAL_PAIRS
+#define CBG_VAL_PAIRS 0
+#endif
 #ifndef CBG_CLAIM_AHEAD
 #define CBG_CLAIM_AHEAD 1
 #endif
@@ -2900,7 +2904,25 @@ __global__ void __launch_bounds__(NT) k_num_heavy_known(const KnownUnit* __restr
       STAMP(4);
     }
     // d. values out, row order
-#if CBG_NT_OUT
+#if CBG_VAL_PAIRS
+    if constexpr (sizeof(V) == 8) {   // two values per 16-byte store from the first 16-byte aligned output on
+      typedef V v2 __attribute__((ext_vector_type(2)));
+      const int64_t ob = H.outoff;
+      const int head = (int)(ob & 1) < cnt ? (int)(ob & 1) : cnt;   // one value before the aligned part
+      if (tid < head) __builtin_nontemporal_store(SRT::out(vals[0], A.val, B.val), &out.val[ob]);
+      const int npair = (cnt - head) >> 1;
+      for (int p = tid; p < npair; p += NT) {
+        const int i = head + 2 * p;
+        v2 w;
+        w.x = SRT::out(vals[i], A.val, B.val);
+        w.y = SRT::out(vals[i + 1], A.val, B.val);
+        __builtin_nontemporal_store(w, (v2*)&out.val[ob + i]);
+      }
+      if (((cnt - head) & 1) && tid == 0) __builtin_nontemporal_store(SRT::out(vals[cnt - 1], A.val, B.val), &out.val[ob + cnt - 1]);
+    } else {
+      for (int i = tid; i < cnt; i += NT) __builtin_nontemporal_store(SRT::out(vals[i], A.val, B.val), &out.val[H.outoff + i]);
+    }
+#elif CBG_NT_OUT
     for (int i = tid; i < cnt; i += NT) __builtin_nontemporal_store(SRT::out(vals[i], A.val, B.val), &out.val[H.outoff + i]);
 #else
     for (int i = tid; i < cnt; i += NT) out.val[H.outoff + i] = SRT::out(vals[i], A.val, B.val);
