@@ -54,6 +54,9 @@ constexpr int kNumWave = 4, kNumBlock = 4;
 constexpr int kBlockNT = 512;
 constexpr int kWinNT = 256;
 constexpr int kMaxGrid = 4096;
+#ifndef CBG_KNOWN_SORT_DEFAULT
+#define CBG_KNOWN_SORT_DEFAULT 0   // rows-known units in first-subwindow order (CBG_KNOWN_SORT=1 at run time)
+#endif
 constexpr int64_t kSymPartGrid = kMaxGrid * 2;   // k_sym_part's largest grid (HeavyOut::chunk slack)
 // library-internal flag of spgemm_impl: stop after the symbolic pass and the scan (cbg_estimate): the result holds the
 // colptr only, nnz(C) and the multiplies are exact, no output is allocated or computed
@@ -188,6 +191,7 @@ struct cbg_ctx {
   DevBuf nunits, segsz, segoff, useg, icnt, itemoff, items, parts, wide_win;
   DevBuf hrows, hmode, hpoff, urows;   // symbolic -> numeric row handoff of heavy columns
   DevBuf oitems;                       // heavy items the rows-known kernel does not take
+  DevBuf items2, ubkt;                 // the rows-known units in first-subwindow order + bucket counters (CBG_KNOWN_SORT)
   DevBuf ptab;                         // A's part table for k_sym_part (k_part_table)
   DevBuf aos;                          // A's rows and values interleaved (k_num_heavy_known gathers)
   DevBuf gal[9];                       // fused Galerkin product scratch (galerkin.hip)
@@ -207,7 +211,7 @@ inline void release_workspace(cbg_ctx* c) {
                     &c->ovf_list, &c->split_idx, &c->long_cols, &c->split_tab, &c->heavy_cols, &c->sub, &c->units,
                     &c->ucnt, &c->uspan, &c->ulist, &c->fb_units, &c->fb_list, &c->uovf_list, &c->nunits, &c->segsz,
                     &c->segoff, &c->useg, &c->icnt, &c->itemoff, &c->items, &c->parts, &c->wide_win, &c->hrows,
-                    &c->hmode, &c->hpoff, &c->urows, &c->oitems, &c->aos, &c->ptab})
+                    &c->hmode, &c->hpoff, &c->urows, &c->oitems, &c->aos, &c->ptab, &c->items2, &c->ubkt})
     b->release();
   for (DevBuf& b : c->stageA) b.release();
   for (DevBuf& b : c->stageB) b.release();
@@ -731,6 +735,7 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
   // 4. heavy columns -> units (split table + greedy subwindow grouping)
   const int64_t nunit_cap = (int64_t)H * nsub;
   Unit* units = nullptr;
+  const KnownUnit* known_list = nullptr;   // the rows-known unit list the heavy kernel takes (items, or items2 sorted)
   if (H > 0) {
     HIPCHK(ctx->units.reserve(sizeof(Unit) * (nunit_cap + 1)));
     HIPCHK(ctx->ucnt.reserve(sizeof(int64_t) * (nunit_cap + 1)));
@@ -805,6 +810,27 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
         ctx->uspan.as<int2>(), spl.urows,
         B.cp, ctx->items.as<KnownUnit>(), ctx->oitems.as<HeavyItem>(), sc + 12);
     HIPCHK(hipGetLastError());
+    known_list = ctx->items.as<KnownUnit>();
+    // CBG_KNOWN_SORT=1: the rows-known units in first-subwindow order (k_known_bucket)
+    static const bool ksort = [] { const char* x = std::getenv("CBG_KNOWN_SORT"); return x ? x[0] == '1' : CBG_KNOWN_SORT_DEFAULT != 0; }();
+    if (ksort && nsub <= kMaxSub) {
+      HIPCHK(ctx->items2.reserve(sizeof(KnownUnit) * ucap));
+      HIPCHK(ctx->ubkt.reserve(sizeof(unsigned long long) * 3 * (nsub + 1)));
+      cap.add(ctx->items2, "items2"); cap.add(ctx->ubkt, "ubkt");
+      CAPCHK(cap);
+      unsigned long long* bcnt = ctx->ubkt.as<unsigned long long>();
+      unsigned long long* bbase = bcnt + (nsub + 1);
+      unsigned long long* bcur = bbase + (nsub + 1);
+      HIPCHK(hipMemsetAsync(bcnt, 0, sizeof(unsigned long long) * 3 * (nsub + 1), st));
+      const int gs = (int)grid_for(ucap, kSortChunk, 4096);
+      k_known_bucket<false><<<gs, kSortChunk, 0, st>>>(ctx->items.as<KnownUnit>(), sc + 12, slog, nsub, bcnt, nullptr,
+                                                       nullptr, nullptr);
+      k_known_bucket_base<<<1, 1024, 0, st>>>(nsub, bcnt, bbase);
+      k_known_bucket<true><<<gs, kSortChunk, 0, st>>>(ctx->items.as<KnownUnit>(), sc + 12, slog, nsub, nullptr, bbase,
+                                                      bcur, ctx->items2.as<KnownUnit>());
+      HIPCHK(hipGetLastError());
+      known_list = ctx->items2.as<KnownUnit>();
+    }
   }
   if ((s = bin_fill(st, N, nnz, span, flop, nbp, hist, hn, list, &cn)) != CBG_OK) return s;
   if (cn.hist[kNumWave + kNumBlock + 1] != 0) {   // every column above kHeavy must have become units
@@ -853,7 +879,7 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
       }
       CAPCHK(cap);
       // tickets of the persistent kernels: sc[14], sc[15] (zeroed with the scalars)
-      e = launch_num_heavy_known<CBG_KNOWN_LOGT, CBG_KNOWN_NT, SRT, V>(st, grid, ctx->items.as<KnownUnit>(), sc + 12,
+      e = launch_num_heavy_known<CBG_KNOWN_LOGT, CBG_KNOWN_NT, SRT, V>(st, grid, known_list, sc + 12,
                                                                      A, B, spl, ou, sc + 14, arv);
       if (e == hipSuccess)
         e = launch_num_heavy<CBG_HEAVY_LOGT, CBG_HEAVY_NT, SRT, V>(st, grid, ctx->oitems.as<HeavyItem>(), sc + 13,

@@ -3027,6 +3027,69 @@ __global__ void k_heavy_items_split(int H, const int32_t* __restrict__ cols, con
   if (u0 >= 0) oitems[bo++] = HeavyItem{h, u0, nu, 0};
 }
 
+// Rows-known units in first-subwindow order (CBG_KNOWN_SORT): the persistent kernel takes its units in list order, so
+// the units in flight together then cover one row range of many columns and gather only that range of the A columns
+// they share, instead of every range of a few columns.  Counting sort over the subwindow buckets in chunks of 256
+// units: a chunk's bucket counts in LDS, one global atomic per (chunk, bucket) -- not one per unit on a few hundred
+// counters, which serialised at the L2 (round 4: 2.5 ms) -- and the units' ranks inside their chunk from LDS atomics.
+constexpr int kSortChunk = 256;
+template <bool SCATTER>
+__global__ void __launch_bounds__(kSortChunk) k_known_bucket(const KnownUnit* __restrict__ in,
+                                                             const unsigned long long* __restrict__ nknown, int32_t log,
+                                                             int32_t nb, unsigned long long* __restrict__ bcnt,
+                                                             const unsigned long long* __restrict__ bbase,
+                                                             unsigned long long* __restrict__ bcur,
+                                                             KnownUnit* __restrict__ out) {
+  __shared__ int lh[kMaxSub];
+  __shared__ unsigned long long lb[kMaxSub];
+  const int64_t n = (int64_t)*nknown;
+  for (int64_t c0 = (int64_t)blockIdx.x * kSortChunk; c0 < n; c0 += (int64_t)gridDim.x * kSortChunk) {
+    for (int b = threadIdx.x; b < nb; b += kSortChunk) lh[b] = 0;
+    __syncthreads();
+    const int64_t i = c0 + threadIdx.x;
+    int bk = -1, r = 0;
+    if (i < n) {
+      bk = min(nb - 1, max(0, in[i].lo >> log));
+      r = atomicAdd(&lh[bk], 1);
+    }
+    __syncthreads();
+    for (int b = threadIdx.x; b < nb; b += kSortChunk) {
+      const int c = lh[b];
+      if (c) {
+        if (SCATTER) lb[b] = bbase[b] + atomicAdd(&bcur[b], (unsigned long long)c);
+        else atomicAdd(&bcnt[b], (unsigned long long)c);
+      }
+    }
+    if (SCATTER) {
+      __syncthreads();
+      if (i < n) out[lb[bk] + r] = in[i];
+    }
+    __syncthreads();
+  }
+}
+
+// exclusive scan of the nb (<= kMaxSub) bucket counts, one workgroup
+__global__ void __launch_bounds__(1024) k_known_bucket_base(int32_t nb, const unsigned long long* __restrict__ bcnt,
+                                                            unsigned long long* __restrict__ bbase) {
+  __shared__ int64_t scr[1024 / kWave + 1];
+  constexpr int PER = (kMaxSub + 1023) / 1024;
+  int64_t v[PER], t = 0;
+#pragma unroll
+  for (int e = 0; e < PER; ++e) {
+    const int b = threadIdx.x * PER + e;
+    v[e] = b < nb ? (int64_t)bcnt[b] : 0;
+    t += v[e];
+  }
+  int64_t tot;
+  int64_t ex = block_excl_scan64<1024>(t, scr, &tot);
+#pragma unroll
+  for (int e = 0; e < PER; ++e) {
+    const int b = threadIdx.x * PER + e;
+    if (b < nb) bbase[b] = (unsigned long long)ex;
+    ex += v[e];
+  }
+}
+
 // items of every heavy column: ceil(nunits / kItemUnits) consecutive unit groups
 __global__ void k_heavy_items(int H, const int32_t* __restrict__ nunits, const int64_t* __restrict__ itemoff,
                               HeavyItem* __restrict__ items) {
