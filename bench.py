@@ -426,6 +426,29 @@ def piece_reference(be, args, n, r0, r1, c0, c1):
     return Arow, Acol, mults, nnz
 
 
+def piece_checksum(blk, r0, c0, chunk=1 << 27):
+    """entry_checksum_t over a whole output piece (global row and column ids), in column chunks of about `chunk`
+    entries: summed over the ranks it is the checksum of the whole distributed product, the same for every layout of
+    one product (SURVEY 8(d)'s cross-layout identity; R-MAT values are multiplicities, so every layout's sums are
+    bit-identical)."""
+    import torch
+    cp = blk.cp
+    ncol = blk.ncol
+    total = 0
+    a = 0
+    cph = cp.cpu().numpy()
+    while a < ncol:
+        b = int(np.searchsorted(cph, cph[a] + chunk, side="right")) - 1
+        b = min(ncol, max(b, a + 1))
+        lo, hi = int(cph[a]), int(cph[b])
+        if hi > lo:
+            cols = torch.repeat_interleave(torch.arange(a, b, device=cp.device, dtype=torch.int64) + c0,
+                                           torch.diff(cp[a:b + 1]), output_size=hi - lo)
+            total = (total + entry_checksum_t(cols, blk.ir[lo:hi].to(torch.int64) + r0, blk.val[lo:hi])) & ((1 << 64) - 1)
+        a = b
+    return total - (1 << 64) if total >= 1 << 63 else total
+
+
 def verify_piece(be, SR, blk, Arow, Acol, r0, c0, nsample, seed, ref_stride=0):
     """Check one rank's output piece: a seeded random sample of its columns bit for bit against a one-GPU product
     A(r0:r1, :) * A(:, J_sample) (R-MAT values are multiplicities, so PlusTimes<double> sums are exact), and the
@@ -566,7 +589,8 @@ def bench_dist(args, world, rank, local_rank):
             "step_ms": 1e3 * elapsed_local / args.steps}
     recs = [None] * world
     dist.all_gather_object(recs, {"verify": v, "roofline": rrec, "phases": {k: w / args.steps for k, w in phases.items()}})
-    csum = torch.tensor([v.get("ref_sample_checksum", 0), v.get("ref_sample_nnz", 0)], dtype=torch.int64, device=cd)
+    csum = torch.tensor([v.get("ref_sample_checksum", 0), v.get("ref_sample_nnz", 0),
+                         piece_checksum(C.block, r0, c0)], dtype=torch.int64, device=cd)
     dist.all_reduce(csum)   # int64 sums wrap: the uint64 checksum mod 2^64
     ok_all = all(r["verify"]["bit_exact"] and r["verify"]["piece_nnz_equals_estimate"] and r["verify"]["steps_same_nnz"]
                  for r in recs)
@@ -609,6 +633,8 @@ def bench_dist(args, world, rank, local_rank):
                             "estimateFLOP": flops_global, "nnz_symbolic": nnz_global, "ok": ok_all,
                             "per_rank": [r["verify"] for r in recs]},
                "rank0_phases_per_step": {k: round(w, 3) for k, w in recs[0]["phases"].items()},
+               # the whole product's entry checksum (every rank's piece): equal across the layouts of one scale
+               "full_output_checksum": f"{int(csum[2].item()) & ((1 << 64) - 1):016x}",
                "grid_transport": ginfo["kind"],
                # members of every communicator as RCCL itself counts them (ncclCommCount)
                "rccl_ranks": ginfo["ranks"] if ginfo["kind"] == "rccl" else None,

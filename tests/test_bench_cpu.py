@@ -126,3 +126,29 @@ def test_host_cores_record():
     threads, rec = bench.host_cores(1)
     assert 1 <= threads <= 16 and threads <= rec["affinity_cpus"]
     assert rec["os_cpu_count"] == os.cpu_count() and rec["pool_share_cpus"] == 16
+
+
+def test_piece_checksum_matches_entry_checksum():
+    """bench.piece_checksum (device-side, column chunks, global ids) equals entry_checksum of the same entries: the
+    per-rank sums of the distributed line add up to one whole-product checksum whatever the layout."""
+    import numpy as np
+    import torch
+    import bench
+    from combblas_amd import dist as cbd
+    rng = np.random.default_rng(1)
+    n, m = 50, 40
+    cols = [np.sort(rng.choice(n, rng.integers(0, 8), replace=False)) for _ in range(m)]
+    cp = np.r_[0, np.cumsum([len(c) for c in cols])].astype(np.int64)
+    ir = np.concatenate(cols).astype(np.int32)
+    val = rng.integers(1, 9, len(ir)).astype(np.float64)
+    r0, c0 = 7, 11
+    got = bench.piece_checksum(cbd.Block(n, m, torch.tensor(cp), torch.tensor(ir), torch.tensor(val)), r0, c0, chunk=5)
+    # the same entries as one CSC with the global ids: rows + r0 in an (n + r0)-row matrix, columns shifted by c0
+    gcp = np.r_[np.zeros(c0, np.int64), cp]
+    assert f"{got & ((1 << 64) - 1):016x}" == bench.entry_checksum(gcp, ir.astype(np.int64) + r0, val)
+    # split into two column pieces: the checksums add (mod 2^64)
+    a = bench.piece_checksum(cbd.Block(n, 25, torch.tensor(cp[:26]), torch.tensor(ir[:cp[25]]),
+                                       torch.tensor(val[:cp[25]])), r0, c0)
+    b = bench.piece_checksum(cbd.Block(n, 15, torch.tensor(cp[25:] - cp[25]), torch.tensor(ir[cp[25]:]),
+                                       torch.tensor(val[cp[25]:])), r0, c0 + 25)
+    assert (a + b) & ((1 << 64) - 1) == got & ((1 << 64) - 1)
