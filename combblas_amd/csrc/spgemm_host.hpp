@@ -55,7 +55,7 @@ constexpr int kBlockNT = 512;
 constexpr int kWinNT = 256;
 constexpr int kMaxGrid = 4096;
 #ifndef CBG_KNOWN_SORT_DEFAULT
-#define CBG_KNOWN_SORT_DEFAULT 0   // rows-known units in first-subwindow order (CBG_KNOWN_SORT=1 at run time)
+#define CBG_KNOWN_SORT_DEFAULT 1   // rows-known units in first-subwindow order (CBG_KNOWN_SORT=0 at run time: list order); s20 heavy 30.3 -> 29.9 ms, s21 96.6 -> 94.9 ms, profiles/r05p_known_sort_ab.txt
 #endif
 constexpr int64_t kSymPartGrid = kMaxGrid * 2;   // k_sym_part's largest grid (HeavyOut::chunk slack)
 // library-internal flag of spgemm_impl: stop after the symbolic pass and the scan (cbg_estimate): the result holds the

@@ -6,7 +6,8 @@
 #                                      the bench line's traffic fields come from this build), the N = 1 bench line as
 #                                      the driver runs it, rocprofv3 kernel stats, SQ counters
 #   tools/gpu_evidence.sh TAG multi    every rank's share of the 8 / 4 / 2-GPU layouts (verified), RCCL rehearsals of
-#                                      N = 8 and N = 2 (verified bench lines), merge bench, stamps (diag build)
+#                                      N = 8 / 4 / 2 at s19 (verified bench lines whose whole-product checksums must
+#                                      agree across the layouts) and N = 2 at s18, merge bench, stamps (diag build)
 #   tools/gpu_evidence.sh TAG extra    rocprofv3 stats of the s22 2x2x2 rank-0 share, the fiber codec at s21
 set -u
 T=$1
@@ -19,7 +20,7 @@ case ${2:-local} in
     cp "$OUT/${T}_pmc_heavy.json" "profiles/${T}_pmc_heavy.json" && cp "$OUT/${T}_pmc_product.json" "profiles/${T}_pmc_product.json" || exit 20
     tools/gpu_steps.sh "$T" bench:--steps,20,--warmup,5 prof sq || exit $? ;;
   multi)
-    tools/gpu_steps.sh "$T" share:8:22 share:4:21 share:2:21 dist:8:19 dist:2:18 || exit $?
+    tools/gpu_steps.sh "$T" share:8:22 share:4:21 share:2:21 dist:8:19 dist:4:19 dist:2:19 dist:2:18 || exit $?
     timeout -k 10 300 python3 -u tools/bench_merge.py --scale 20 --reps 3 > "$OUT/merge_s20.log" 2>&1 || exit 30
     if [ -f tools/diag/libcbgpu.so ]; then
       timeout -k 10 300 python3 -u tools/diag_stamps.py 20 > "$OUT/diag_stamps_s20.txt" 2>&1 || exit 31
