@@ -98,7 +98,9 @@ constexpr int64_t kHeavy = CBG_HEAVY_MIN;   // nnz(C(:,j)) above which a column 
 #define CBG_RANK_SPAN_CAP 458752   // f64, T=8192, NT=1024, unit cap 6144: <= (9216*12 - 6144*8)/4 words
 #endif
 #ifndef CBG_UNIT_CAP
-#define CBG_UNIT_CAP (3 << (CBG_HEAVY_LOGT - 2))   // rank mode holds up to T outputs; 3/4 T measured best
+// rank mode holds up to T outputs: 7/8 T measured best in round 5 (s20 66.9 -> 66.3 ms, s21 203.4 -> 202.2 ms against
+// 3/4 T; T itself is faster at s20 but slower at s21, profiles/r05s_unit_cap_ab.txt, r05t_unit_cap_ab.txt)
+#define CBG_UNIT_CAP (7 << (CBG_HEAVY_LOGT - 3))
 #endif
 // smallest subwindow: 2^13 rows, or the heavy table's 2^CBG_HEAVY_LOGT when that is smaller (a one-subwindow unit
 // must fit k_num_heavy's dense table)

@@ -23,7 +23,7 @@ import scipy.sparse as sp
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.dirname(HERE))
 
-K_HEAVY, UNIT_CAP, SPAN_CAP, SPLIT_MIN, NT = 4096, 6144, 458752, 16, 1024
+K_HEAVY, UNIT_CAP, SPAN_CAP, SPLIT_MIN, NT = 4096, 7168, 458752, 16, 1024
 
 
 def main():
