@@ -327,7 +327,7 @@ inline void bin_count(hipStream_t st, int64_t n, const int64_t* cnt, const int2*
   if (g > 0) k_bin<<<(int)g, 256, 0, st>>>(n, cnt, span, flop, bp, 0, kHeavy, hist_dev, hist_dev + 32, list);
 }
 // after the host has hist: offsets (the regular classes contiguous in class order, then the lane
-// class), cursors, pass 1
+// class) and pass 1, which derives the same offsets on the device (its cursors hist_dev[32..63] start at zero)
 inline cbg_status bin_fill(hipStream_t st, int64_t n, const int64_t* cnt, const int2* span, const int64_t* flop,
                            BinParams bp, unsigned long long* hist_dev, const unsigned long long* hist_host,
                            int32_t* list, Classes* cl) {
@@ -339,7 +339,6 @@ inline cbg_status bin_fill(hipStream_t st, int64_t n, const int64_t* cnt, const 
   cl->off[kLane8Class] = acc;
   acc += cl->hist[kLane8Class];
   cl->off[kLaneClass] = acc;
-  HIPCHK(hipMemcpyAsync(hist_dev + 32, cl->off.data(), sizeof(unsigned long long) * 32, hipMemcpyHostToDevice, st));
   const int64_t g = (n + 256 * kBinPer - 1) / (256 * kBinPer);
   if (g > 0) k_bin<<<(int)g, 256, 0, st>>>(n, cnt, span, flop, bp, 1, kHeavy, hist_dev, hist_dev + 32, list);
   return CBG_OK;
@@ -701,12 +700,30 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
   k_scan_sums<<<1, 1024, 0, st>>>(ntiles, ctx->scan_tiles.as<int64_t>(), (int64_t*)(sc + 1));
   k_scan_apply<<<(int)ntiles, 256, 0, st>>>(N, nnz, ctx->scan_tiles.as<int64_t>(), colptr);
   HIPCHK(hipGetLastError());
+  // no column can be heavy (hcap = 0 columns above kHeavy multiplies): the numeric binning needs nothing from
+  // the host, so its histogram comes back with nnz(C) in the same read-back (three host syncs per product)
+  const bool early_nbin = !symbolic_only && hcap == 0;
+  BinParams nbp{kNumWave, kNumBlock, 64, 0, kLaneMax};
+  unsigned long long* hn = pinned<unsigned long long>(ctx, kPinNumHist);    // 128 entries
+  unsigned long long* tots = pinned<unsigned long long>(ctx, kPinTotals);   // 2 entries
+  tots[0] = tots[1] = 0;
+  auto numeric_bin_count = [&]() -> hipError_t {
+    hipError_t e = hipMemsetAsync(hist, 0, sizeof(unsigned long long) * 128, st);
+    if (e != hipSuccess) return e;
+    bin_count(st, N, nnz, span, flop, nbp, hist, list);
+    return hipMemcpyAsync(hn, hist, sizeof(unsigned long long) * 128, hipMemcpyDeviceToHost, st);
+  };
+  if (early_nbin) HIPCHK(numeric_bin_count());
   unsigned long long* hsc = pinned<unsigned long long>(ctx, kPinScalars);   // 4 entries
   HIPCHK(hipMemcpyAsync(hsc, sc, 32, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
   HIPCHK(hipEventRecord(ctx->ev[4], st));
   const int64_t mults = (int64_t)hsc[0], nnzc = (int64_t)hsc[1];
   const int H = ((int*)&hsc[2])[0];
+  if (early_nbin && H > 0) {   // a heavy column has nnz <= flop above kHeavy, so hcap = 0 rules it out
+    fprintf(stderr, "cbgpu: %d heavy columns with no column above the heavy bound\n", H);
+    return CBG_EDEVICE;
+  }
   pf.multiplies = mults; pf.nnz_out = nnzc;
   if (symbolic_only) {
     HIPCHK(own->ir.reserve(4));
@@ -782,15 +799,11 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
   // 5. numeric binning (columns and units, one host sync) + kernels; heavy items split into the
   //    rows-known list (k_num_heavy_known) and the rest (k_num_heavy), counts -> sc[12], sc[13]
   Classes cn;
-  BinParams nbp{kNumWave, kNumBlock, 64, 0, kLaneMax};
-  HIPCHK(hipMemsetAsync(hist, 0, sizeof(unsigned long long) * 128, st));
-  bin_count(st, N, nnz, span, flop, nbp, hist, list);
-  unsigned long long* hn = pinned<unsigned long long>(ctx, kPinNumHist);    // 128 entries
-  unsigned long long* tots = pinned<unsigned long long>(ctx, kPinTotals);   // 2 entries
-  tots[0] = tots[1] = 0;
-  HIPCHK(hipMemcpyAsync(hn, hist, sizeof(unsigned long long) * 128, hipMemcpyDeviceToHost, st));
-  if (H > 0) HIPCHK(hipMemcpyAsync(tots, sc + 8, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
-  HIPCHK(hipStreamSynchronize(st));
+  if (!early_nbin) {
+    HIPCHK(numeric_bin_count());
+    if (H > 0) HIPCHK(hipMemcpyAsync(tots, sc + 8, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+  }
   const int64_t segtot = (int64_t)tots[0], nitems = (int64_t)tots[1];
   if (H > 0) {
     HIPCHK(ctx->useg.reserve(sizeof(UnitSeg) * (segtot + 1)));

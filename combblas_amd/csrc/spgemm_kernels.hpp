@@ -448,7 +448,20 @@ __global__ void __launch_bounds__(256) k_bin(int64_t n, const int64_t* __restric
       atomicAdd(&hist[threadIdx.x], (unsigned long long)s_h[threadIdx.x]);
     return;
   }
-  if (used) s_base[threadIdx.x] = s_h[threadIdx.x] ? atomicAdd(&cursor[threadIdx.x], (unsigned long long)s_h[threadIdx.x]) : 0;
+  // the class offsets from pass 0's totals, laid out as bin_fill's host copy (the regular classes in order, then
+  // the lane classes), so that no host-to-device copy sits between the passes; cursor starts at zero
+  if (threadIdx.x == 0) {
+    unsigned long long h[32];
+#pragma unroll
+    for (int c = 0; c < 32; ++c) h[c] = hist[c];
+    unsigned long long acc = 0;
+    for (int c = 0; c < ncls; ++c) { s_base[c] = acc; acc += h[c]; }
+    s_base[kLane8Class] = acc;
+    s_base[kLaneClass] = acc + h[kLane8Class];
+  }
+  __syncthreads();
+  if (used && s_h[threadIdx.x])
+    s_base[threadIdx.x] += atomicAdd(&cursor[threadIdx.x], (unsigned long long)s_h[threadIdx.x]);
   __syncthreads();
 #pragma unroll
   for (int r = 0; r < kBinPer; ++r)
