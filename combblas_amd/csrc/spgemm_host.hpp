@@ -221,8 +221,7 @@ inline void release_workspace(cbg_ctx* c) {
 
 // pinned read-back slots (byte offsets into ctx->pin); a D2H copy into pageable memory goes through a staging
 // buffer and costs tens of microseconds per host sync on small products
-constexpr size_t kPinSymHist = 0, kPinScalars = 1024, kPinNumHist = 1280, kPinTotals = 2432, kPinErr = 2496,
-                 kPinMerge = 2624, kPinBytes = 16384;
+constexpr size_t kPinMerge = 2624, kPinMirror = 4096, kPinBytes = 16384;
 template <typename T>
 inline T* pinned(cbg_ctx* c, size_t off) { return (T*)((char*)c->pin + off); }
 
@@ -548,7 +547,14 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
   unsigned long long* hist = ctx->hist.as<unsigned long long>();
   // scalars: [0] multiplies, [1] nnz(C); ints from byte 16: heavy n, nlong, adderr, col ovf, unit ovf,
   // fallback units, fallback-unit ovf; [16..18] heavy multiplies, B nonzeros, outputs (k_heavy_sums)
-  unsigned long long* sc = ctx->scalars.as<unsigned long long>();
+  // the scalars sit right after the binning histogram and its cursors (hist[0..63]), so that one device-to-host
+  // copy of hist[0..64+k) brings back both; pm mirrors that range in pinned host memory (pm[i] = hist[i])
+  unsigned long long* sc = hist + 64;
+  unsigned long long* pm = pinned<unsigned long long>(ctx, kPinMirror);
+  const unsigned long long* psc = pm + 64;
+  auto mirror = [&](int lo, int hi) {   // hist[lo..hi) -> pm[lo..hi)
+    return hipMemcpyAsync(pm + lo, hist + lo, sizeof(unsigned long long) * (hi - lo), hipMemcpyDeviceToHost, st);
+  };
   int* si = (int*)(sc + 2);
   int *heavy_n = si + 0, *nlong = si + 1, *adderr = si + 2, *ovf_n = si + 3, *uovf_n = si + 4, *fb_n = si + 5,
       *fb_ovf_n = si + 6;
@@ -571,14 +577,12 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
   // 2. symbolic binning + kernels
   Classes cs;
   BinParams sbp{kSymWave, kSymBlock, 64, 1, kLaneMax};
-  unsigned long long* hh = pinned<unsigned long long>(ctx, kPinSymHist);   // 64 entries
   HIPCHK(hipMemsetAsync(hist, 0, sizeof(unsigned long long) * 64, st));
   bin_count(st, N, flop, span, nullptr, sbp, hist, list);
-  HIPCHK(hipMemcpyAsync(hh, hist, sizeof(unsigned long long) * 32, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipMemcpyAsync(hh + 32, sc, 96, hipMemcpyDeviceToHost, st));
+  HIPCHK(mirror(0, 64 + 12));   // the class counts and sc[0..11]
   HIPCHK(hipStreamSynchronize(st));
-  const int NL = ((int*)&hh[34])[1];
-  if ((s = bin_fill(st, N, flop, span, nullptr, sbp, hist, hh, list, &cs)) != CBG_OK) return s;
+  const int NL = ((const int*)&psc[2])[1];
+  if ((s = bin_fill(st, N, flop, span, nullptr, sbp, hist, pm, list, &cs)) != CBG_OK) return s;
   const int64_t hcap = (int64_t)cs.hist[31];
   HIPCHK(ctx->heavy_cols.reserve(sizeof(int32_t) * (hcap + 1)));
   HIPCHK(ctx->sub.reserve(sizeof(int32_t) * (hcap * nsub + 1)));
@@ -591,7 +595,7 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
     const char* e = getenv("CBG_ROW_HANDOFF");
     ctx->row_handoff = (e && e[0] == '0') ? 0 : 1;
   }
-  const unsigned long long hbound = hh[42];
+  const unsigned long long hbound = psc[10];
   // (16-bit rows: needs subwindows inside 2^16-row blocks, slog <= 16, i.e. nrow <= kMaxSub * 2^16)
   if (ctx->row_handoff && hcap > 0 && hbound > 0 && !SRT::kAddIsError && !symbolic_only && (!CBG_ROWS16 || slog <= 16)) {
     size_t fr = 0, tot = 0;
@@ -704,19 +708,19 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
   // the host, so its histogram comes back with nnz(C) in the same read-back (three host syncs per product)
   const bool early_nbin = !symbolic_only && hcap == 0;
   BinParams nbp{kNumWave, kNumBlock, 64, 0, kLaneMax};
-  unsigned long long* hn = pinned<unsigned long long>(ctx, kPinNumHist);    // 128 entries
-  unsigned long long* tots = pinned<unsigned long long>(ctx, kPinTotals);   // 2 entries
-  tots[0] = tots[1] = 0;
-  auto numeric_bin_count = [&]() -> hipError_t {
-    hipError_t e = hipMemsetAsync(hist, 0, sizeof(unsigned long long) * 128, st);
-    if (e != hipSuccess) return e;
-    bin_count(st, N, nnz, span, flop, nbp, hist, list);
-    return hipMemcpyAsync(hn, hist, sizeof(unsigned long long) * 128, hipMemcpyDeviceToHost, st);
+  auto numeric_bin_count = [&]() -> hipError_t {   // (hist[0..63] only: sc follows)
+    hipError_t e = hipMemsetAsync(hist, 0, sizeof(unsigned long long) * 64, st);
+    if (e == hipSuccess) bin_count(st, N, nnz, span, flop, nbp, hist, list);
+    return e;
   };
-  if (early_nbin) HIPCHK(numeric_bin_count());
-  unsigned long long* hsc = pinned<unsigned long long>(ctx, kPinScalars);   // 4 entries
-  HIPCHK(hipMemcpyAsync(hsc, sc, 32, hipMemcpyDeviceToHost, st));
+  if (early_nbin) {
+    HIPCHK(numeric_bin_count());
+    HIPCHK(mirror(0, 64 + 4));   // the numeric class counts and sc[0..3]
+  } else {
+    HIPCHK(mirror(64, 64 + 4));
+  }
   HIPCHK(hipStreamSynchronize(st));
+  const unsigned long long* hsc = psc;
   HIPCHK(hipEventRecord(ctx->ev[4], st));
   const int64_t mults = (int64_t)hsc[0], nnzc = (int64_t)hsc[1];
   const int H = ((int*)&hsc[2])[0];
@@ -801,10 +805,11 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
   Classes cn;
   if (!early_nbin) {
     HIPCHK(numeric_bin_count());
-    if (H > 0) HIPCHK(hipMemcpyAsync(tots, sc + 8, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+    HIPCHK(mirror(0, 64 + 10));   // the numeric class counts and sc[8..9] (zero unless H > 0)
     HIPCHK(hipStreamSynchronize(st));
   }
-  const int64_t segtot = (int64_t)tots[0], nitems = (int64_t)tots[1];
+  const unsigned long long* hn = pm;
+  const int64_t segtot = (int64_t)psc[8], nitems = (int64_t)psc[9];
   if (H > 0) {
     HIPCHK(ctx->useg.reserve(sizeof(UnitSeg) * (segtot + 1)));
     spl.useg = ctx->useg.as<UnitSeg>();
@@ -921,15 +926,12 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
     HIPCHK(hipGetLastError());
   }
   HIPCHK(hipEventRecord(ctx->ev[5], st));
-  int* herr = pinned<int>(ctx, kPinErr);   // 8 ints, then the rows-known unit count
-  unsigned long long& hknown = *pinned<unsigned long long>(ctx, kPinErr + 32);
-  unsigned long long* hsum = pinned<unsigned long long>(ctx, kPinErr + 40);   // 3 entries
-  hknown = 0;
-  hsum[0] = hsum[1] = hsum[2] = 0;
-  HIPCHK(hipMemcpyAsync(herr, si, 8 * sizeof(int), hipMemcpyDeviceToHost, st));
-  if (H > 0) HIPCHK(hipMemcpyAsync(&hknown, sc + 12, sizeof(hknown), hipMemcpyDeviceToHost, st));
-  if (H > 0) HIPCHK(hipMemcpyAsync(hsum, sc + 16, 3 * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+  // the error ints (sc[2..5]), the rows-known unit count sc[12] and the heavy sums sc[16..18] (zero unless H > 0)
+  HIPCHK(mirror(64, 64 + 19));
   HIPCHK(hipStreamSynchronize(st));
+  const int* herr = (const int*)(psc + 2);
+  const unsigned long long hknown = psc[12];
+  const unsigned long long* hsum = psc + 16;
   float t;
   (void)hipEventElapsedTime(&t, ctx->ev[0], ctx->ev[1]); pf.flops_ms = t;
   (void)hipEventElapsedTime(&t, ctx->ev[1], ctx->ev[2]); pf.bin_ms = t;
