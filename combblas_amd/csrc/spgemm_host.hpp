@@ -558,7 +558,7 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
   int* si = (int*)(sc + 2);
   int *heavy_n = si + 0, *nlong = si + 1, *adderr = si + 2, *ovf_n = si + 3, *uovf_n = si + 4, *fb_n = si + 5,
       *fb_ovf_n = si + 6;
-  HIPCHK(hipMemsetAsync(sc, 0, 256, st));
+  HIPCHK(hipMemsetAsync(hist, 0, sizeof(unsigned long long) * 96, st));   // the symbolic histogram and sc together
   HIPCHK(hipMemsetAsync(nnz, 0, sizeof(int64_t) * N, st));
   {
     const int64_t avg = N > 0 ? (B.nnz + N - 1) / N : 0;   // lanes per column ~ the mean B column length
@@ -577,8 +577,7 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
   // 2. symbolic binning + kernels
   Classes cs;
   BinParams sbp{kSymWave, kSymBlock, 64, 1, kLaneMax};
-  HIPCHK(hipMemsetAsync(hist, 0, sizeof(unsigned long long) * 64, st));
-  bin_count(st, N, flop, span, nullptr, sbp, hist, list);
+  bin_count(st, N, flop, span, nullptr, sbp, hist, list);   // (hist zeroed with sc above)
   HIPCHK(mirror(0, 64 + 12));   // the class counts and sc[0..11]
   HIPCHK(hipStreamSynchronize(st));
   const int NL = ((const int*)&psc[2])[1];
