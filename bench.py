@@ -4,6 +4,10 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--scale S] [--no-cpu]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
+Without WORLD_SIZE in the environment, `--gpus N > 1` makes this process a launcher: it starts N rank processes of
+this script (RANK / LOCAL_RANK / WORLD_SIZE set, one GPU each) before any GPU call, relays rank 0's JSON line and
+exits non-zero if any rank fails.  Under torch.distributed.run, WORLD_SIZE must equal --gpus.
+
 Workload (BASELINE.json configs): Graph500 Kronecker / R-MAT, edge factor 16, A*A over PlusTimes<double>,
 inputs built on the GPU from the reference's own Graph500 edge stream (seed 0xDECAFBAD, the reference's
 default SEED; the s20 matrix's hash equals refprobe `gen` output) and resident in HBM before the timed region.
@@ -607,14 +611,19 @@ def bench_dist(args, world, rank, local_rank):
         slow = max(range(world), key=lambda r: recs[r]["roofline"]["local_ms"])
         rs = recs[slow]["roofline"]
         ach = rs["heavy_bytes"] / (rs["heavy_ms"] / 1e3) / 1e9 if rs["heavy_ms"] > 0 else 0.0
+        ngpu = torch.cuda.device_count()
+        rehearsal = backend != "nccl" or world > ngpu
+        kern = ("k_num_heavy_known + k_num_heavy on the slowest rank (its local products per step; HIP events on the "
+                "library stream)")
+        if rehearsal:
+            kern = (f"REHEARSAL, not a hardware roofline: {world} ranks share {ngpu} GPU(s) over {backend}; " + kern)
         out = {"metric": METRIC, "value": mults / elapsed, "unit": "multiplies/s", "n_gpus": world,
                "steps": args.steps, "warmup": args.warmup, "ms_per_step": 1000.0 * elapsed / args.steps,
                "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
                "data": "synthetic", "config": cfg,
                "effective_GBps": balg_bytes(mults / args.steps, nnzc / args.steps, nnzb, n)
                / (elapsed / args.steps) / 1e9,
-               "roofline": {"bound": "hbm", "kernel": "k_num_heavy_known + k_num_heavy on the slowest rank (its local "
-                                                      "products per step; HIP events on the library stream)",
+               "roofline": {"bound": "hbm (rehearsal)" if rehearsal else "hbm", "kernel": kern, "rehearsal": rehearsal,
                             "rank": slow, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                             "frac": ach / HBM_PEAK_GBS, "traffic": None,
                             "algorithmic_bytes_per_step": rs["heavy_bytes"], "avg_ms_per_step": rs["heavy_ms"],
@@ -1007,9 +1016,117 @@ def bench_rank_share(args):
         sys.exit("bench: a rank's piece failed its checks (verified / fiber_codec)")
 
 
+# ------------------------------------------------------------------------- rank launcher (N > 1)
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _visible_device_count():
+    """GPUs this process could use, counted without initialising the GPU (torch.cuda.device_count() does not on
+    this ROCm image; the environment's visibility masks are honoured by it)."""
+    try:
+        import torch
+        return torch.cuda.device_count()
+    except Exception:
+        return 0
+
+
+def launch_ranks(n, argv, grace_s=30.0):
+    """`bench.py --gpus N` without WORLD_SIZE: start N fresh child processes of this script, one per GPU, BEFORE any
+    GPU call in this process (the parent only counts devices), as torch.distributed.run would: RANK = LOCAL_RANK = r,
+    WORLD_SIZE = LOCAL_WORLD_SIZE = N, MASTER_ADDR 127.0.0.1 and a free port.  Rank 0's stdout is this process's
+    stdout (its one JSON line); the other ranks' stdout goes to stderr.  When a rank fails, the others get `grace_s`
+    to finish (they would otherwise wait in a collective for the dead rank), then SIGTERM, then SIGKILL -- each by
+    its own PID.  Returns the exit status: 0 only if every rank exited 0.  The reference's driver likewise sizes its
+    grid from the launched world (3DSpGEMM/mpipspgemm.cpp:34-60)."""
+    import signal
+    import subprocess
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__)] + list(argv), env=env,
+                                      stdout=subprocess.PIPE if r == 0 else sys.stderr.fileno(), text=True))
+
+    def relay(stream):   # rank 0's JSON line to stdout; library chatter (gloo/RCCL banners) to stderr
+        for line in stream:
+            out = sys.stdout if line.startswith("{") else sys.stderr
+            out.write(line)
+            out.flush()
+    import threading
+    relay_thread = threading.Thread(target=relay, args=(procs[0].stdout,), daemon=True)
+    relay_thread.start()
+
+    def forward(signum, _frame):   # the launcher stopped (e.g. a time limit): stop every rank it started
+        for p in procs:
+            if p.poll() is None:
+                p.send_signal(signum)
+        for p in procs:
+            try:
+                p.wait(timeout=10)
+            except subprocess.TimeoutExpired:
+                p.kill()
+        sys.exit(128 + signum)
+    signal.signal(signal.SIGTERM, forward)
+    signal.signal(signal.SIGINT, forward)
+    status = 0
+    failed_at = None
+    while True:
+        codes = [p.poll() for p in procs]
+        for r, c in enumerate(codes):
+            if c not in (None, 0) and status == 0:
+                status = c if c > 0 else 128 - c
+                failed_at = time.monotonic()
+                print(f"bench: rank {r} exited with status {c}", file=sys.stderr, flush=True)
+        if all(c is not None for c in codes):
+            break
+        if failed_at is not None and time.monotonic() - failed_at > grace_s:
+            for p in procs:
+                if p.poll() is None:
+                    p.send_signal(signal.SIGTERM)
+            t = time.monotonic()
+            while any(p.poll() is None for p in procs) and time.monotonic() - t < 10:
+                time.sleep(0.2)
+            for p in procs:
+                if p.poll() is None:
+                    p.kill()
+            for p in procs:
+                p.wait()
+            break
+        time.sleep(0.2)
+    relay_thread.join(timeout=10)
+    return status
+
+
+def launch_probe(world, rank, local_rank):
+    """`--launch-probe` (launcher test, CPU): every rank joins a gloo group and rank 0 prints the line the launched
+    world produced -- the same rendezvous and one-line contract as the real run, without a GPU."""
+    import torch
+    import torch.distributed as dist
+    dist.init_process_group("gloo")
+    recs = [None] * world
+    dist.all_gather_object(recs, {"rank": rank, "local_rank": local_rank, "pid": os.getpid(),
+                                  "world": int(os.environ["WORLD_SIZE"])})
+    t = torch.tensor([float(rank)])
+    dist.all_reduce(t)
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "n_gpus": world, "launch_probe": True, "world": dist.get_world_size(),
+                          "rank_sum": float(t.item()), "ranks": recs}), flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
+    if os.environ.get("CBG_LAUNCH_PROBE_FAIL_RANK") == str(rank):
+        sys.exit(7)
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (ranks); default WORLD_SIZE or 1.  Without WORLD_SIZE, N > 1 starts N ranks itself")
+    ap.add_argument("--launch-probe", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--scale", type=int, default=0, help="R-MAT scale (default 20 + {1:0,2:1,4:1,8:2}[N])")
@@ -1024,9 +1141,22 @@ def main():
                          "('all' or a comma list); one JSON line per rank (local ms, fiber bytes, peak HBM)")
     ap.add_argument("--gpus-virtual", type=int, default=8)
     args = ap.parse_args()
+    if args.rank_share is None and "WORLD_SIZE" not in os.environ and (args.gpus or 1) > 1:
+        # launched as `python bench.py --gpus N`: this process becomes the launcher; it makes no GPU call
+        backend = os.environ.get("CBG_DIST_BACKEND", "nccl")
+        have = _visible_device_count()
+        if not args.launch_probe and backend == "nccl" and have < args.gpus:
+            sys.exit(f"bench: --gpus {args.gpus} needs {args.gpus} visible GPUs for RCCL (found {have}); a rehearsal "
+                     f"with ranks sharing GPUs sets CBG_DIST_BACKEND=rccl-net or gloo")
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus is not None and args.rank_share is None and args.gpus != world:
+        sys.exit(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}: the launched world must match")
+    args.gpus = world
+    if args.launch_probe:
+        return launch_probe(world, rank, local_rank)
     if args.rank_share is not None:
         if not args.scale:
             args.scale = 20 + {1: 0, 2: 1, 4: 1, 8: 2}.get(args.gpus_virtual, 0)

@@ -152,3 +152,44 @@ def test_piece_checksum_matches_entry_checksum():
     b = bench.piece_checksum(cbd.Block(n, 15, torch.tensor(cp[25:] - cp[25]), torch.tensor(ir[cp[25]:]),
                                        torch.tensor(val[cp[25]:])), r0, c0 + 25)
     assert (a + b) & ((1 << 64) - 1) == got & ((1 << 64) - 1)
+
+
+def _run_bench(args, env_extra=None, timeout=240):
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, capture_output=True, text=True,
+                          env=env, timeout=timeout, cwd=ROOT)
+
+
+def test_bench_gpus_n_launches_n_ranks():
+    """`python bench.py --gpus 2` with no WORLD_SIZE starts two fresh rank processes itself (no GPU call in the
+    launcher), rank 0's JSON line is the only stdout line, and the line is the launched world's (n_gpus 2)."""
+    import json
+    r = _run_bench(["--gpus", "2", "--launch-probe", "--no-cpu", "--scale", "8"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [x for x in r.stdout.splitlines() if x.strip()]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["world"] == 2 and d["rank_sum"] == 1.0
+    assert sorted(x["rank"] for x in d["ranks"]) == [0, 1] and {x["world"] for x in d["ranks"]} == {2}
+    assert sorted(x["local_rank"] for x in d["ranks"]) == [0, 1]
+    assert len({x["pid"] for x in d["ranks"]}) == 2
+
+
+def test_bench_launcher_fails_when_a_rank_fails():
+    r = _run_bench(["--gpus", "2", "--launch-probe"], {"CBG_LAUNCH_PROBE_FAIL_RANK": "1"})
+    assert r.returncode == 7, (r.returncode, r.stderr[-3000:])
+    assert "rank 1 exited with status 7" in r.stderr
+
+
+def test_bench_refuses_world_size_mismatch():
+    r = _run_bench(["--gpus", "8", "--launch-probe"], {"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode != 0 and "WORLD_SIZE=2" in r.stderr
+
+
+def test_bench_refuses_more_ranks_than_gpus_for_rccl():
+    """With fewer visible GPUs than --gpus and the production backend, the launcher refuses (no silent sharing)."""
+    r = _run_bench(["--gpus", "4"], {"CBG_DIST_BACKEND": "nccl", "HIP_VISIBLE_DEVICES": ""})
+    assert r.returncode != 0 and "visible GPUs" in r.stderr

@@ -6,6 +6,7 @@
 #   tests              the whole -m gpu suite            tests:<expr>   pytest -m gpu -k <expr>
 #   bench              N = 1 bench line (configs[1])     bench:<args>   bench.py with extra args (',' = ' ')
 #   dist:<N>:<scale>   N ranks on this one GPU over libcbgpu's RCCL grid (RCCL sockets), verified bench line
+#   launch:<N>:<scale> the same, started as `bench.py --gpus N` (the script launches its N ranks itself)
 #   share:<N>:<scale>  every rank's share of the N-GPU layout at full size, verified (bench.py --rank-share)
 #   codec:<scale>      the fiber wire codec on the 1x1x2 message (tools/bench_codec.py) + its rocprofv3 kernel stats
 #   shareprof:<N>:<s>  rocprofv3 kernel stats of rank 0's share of the N-GPU layout at scale s
@@ -42,6 +43,12 @@ for step in "$@"; do
         --steps ${STEPS:-3} --warmup 1 --scale "$b" > "$OUT/dist_n${a}_s${b}.log" 2>&1
       rc=$?; grep '^{' "$OUT/dist_n${a}_s${b}.log" | tail -1 | cut -c1-1500
       [ $rc -eq 0 ] || { grep -v '^{' "$OUT/dist_n${a}_s${b}.log" | tail -8 | cut -c1-400; fail "$step" $rc; } ;;
+    launch)   # the same rehearsal started the way the driver may start it: `bench.py --gpus N`, no WORLD_SIZE
+      CBG_DIST_BACKEND=${BACKEND:-rccl-net} timeout -k 10 600 python3 bench.py --gpus "$a" \
+        --steps ${STEPS:-3} --warmup 1 --scale "$b" > "$OUT/launch_n${a}_s${b}.log" 2> "$OUT/launch_n${a}_s${b}.err"
+      rc=$?; cut -c1-1500 "$OUT/launch_n${a}_s${b}.log"
+      [ $rc -eq 0 ] && [ "$(grep -c . "$OUT/launch_n${a}_s${b}.log")" = 1 ] || \
+        { tail -8 "$OUT/launch_n${a}_s${b}.err" | cut -c1-400; fail "$step" $rc; } ;;
     share)
       timeout -k 10 900 python -u bench.py --rank-share all --gpus-virtual "$a" --scale "$b" \
         > "$OUT/rank_share_s${b}_n${a}.jsonl" 2> "$OUT/rank_share_s${b}_n${a}.err"
