@@ -17,6 +17,9 @@ SR_PLUS_TIMES, SR_MIN_PLUS, SR_SELECT2ND, SR_SELECT_MAX, SR_SELECT_MAX_BOOL, SR_
 # cbg_dtype
 BOOL, I32, I64, F32, F64 = range(5)
 SORTED_COLS, KEEP_ON_DEVICE = 1, 2
+# include/cbgpu.h CBG_ABI_VERSION these declarations follow: the library writes structs the caller allocates
+# (cbg_profile, cbg_grid_stats), so a library of another ABI version is refused at load
+ABI_VERSION = 3
 
 
 class DcscView(ctypes.Structure):
@@ -174,6 +177,9 @@ def lib():
             f = getattr(L, name)
             f.restype = res
             f.argtypes = args
+        v = L.cbg_abi_version() if hasattr(L, "cbg_abi_version") else None
+        if v != ABI_VERSION:
+            raise OSError(f"{LIB_PATH}: cbg_abi_version() = {v}, these bindings are ABI {ABI_VERSION}: rebuild it")
         _lib = L
     return _lib
 

@@ -595,15 +595,14 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
     ctx->row_handoff = (e && e[0] == '0') ? 0 : 1;
   }
   const unsigned long long hbound = psc[10];
-  // (16-bit rows: needs subwindows inside 2^16-row blocks, slog <= 16, i.e. nrow <= kMaxSub * 2^16)
-  if (ctx->row_handoff && hcap > 0 && hbound > 0 && !SRT::kAddIsError && !symbolic_only && (!CBG_ROWS16 || slog <= 16)) {
+  if (ctx->row_handoff && hcap > 0 && hbound > 0 && !SRT::kAddIsError && !symbolic_only) {
     size_t fr = 0, tot = 0;
     HIPCHK(hipMemGetInfo(&fr, &tot));
-    // k_sym_part reserves rows per workgroup in chunks (at most kSymPartGrid workgroups, each leaving < chunk unused);
-    // + a pad: the numeric pass reads aligned 32-bit words
+    // k_sym_part reserves rows per workgroup in chunks: it drops at most 1/7 of the rows it places (a leftover < chunk/8
+    // per chunk at least 7/8 used) plus one chunk per workgroup (at most kSymPartGrid); + a pad
     int64_t chunk = std::min<int64_t>(16384, (int64_t)hbound / (4 * kSymPartGrid));
     if (chunk < 512) chunk = 0;
-    const unsigned long long hcapr = hbound + (unsigned long long)(kSymPartGrid * chunk);
+    const unsigned long long hcapr = hbound + (chunk ? hbound / 7 + 1 : 0) + (unsigned long long)(kSymPartGrid * chunk);
     const size_t need = sizeof(HRow) * (hcapr + 2);
     if (need <= ctx->hrows.n || need < fr / 3) {
       HIPCHK(ctx->hrows.reserve(need));
@@ -1016,10 +1015,8 @@ __device__ __forceinline__ V merge_pair(V a, V b) {
 #ifndef CBG_MERGE_PL
 #define CBG_MERGE_PL 4   // merged positions per lane per window (window = 64 * CBG_MERGE_PL)
 #endif
-#ifndef CBG_MERGE_LDS
-#define CBG_MERGE_LDS 0   // 1: fill pass with values and merged output staged in LDS for coalesced loads/stores
-                          // (measured slower: s22 rank share 85.7 vs 67.8 ms, 24 KB of LDS per block)
-#endif
+// (staging the fill pass's values and merged output in LDS for coalesced loads/stores measured slower: s22 rank share
+// 85.7 vs 67.8 ms, 24 KB of LDS per block; removed in round 6)
 constexpr int kMergePL = CBG_MERGE_PL;
 constexpr int kMergeW = kWave * kMergePL;
 static_assert(kMergeW < 1024, "the merge window's counts are packed in 10-bit fields");
@@ -1034,13 +1031,9 @@ __global__ void __launch_bounds__(256) k_merge2(int64_t ncol, const int64_t* __r
                                                 unsigned long long* __restrict__ disorder) {
   constexpr int W = kMergeW, PL = kMergePL;
   __shared__ int32_t swin[4][2][W];
-  constexpr bool SV = FILL && CBG_MERGE_LDS;
-  __shared__ V svw[SV ? 4 : 1][2][SV ? W : 1];   // fill: the window's values (then the merged output's)
   const int w = threadIdx.x / kWave, l = lane_id();
   int32_t* sa = swin[w][0];
   int32_t* sb = swin[w][1];
-  V* sva = svw[SV ? w : 0][0];
-  V* svb = svw[SV ? w : 0][1];
   for (int64_t j = (int64_t)blockIdx.x * 4 + w; j < ncol; j += (int64_t)gridDim.x * 4) {
     int64_t ia = acp[j], ib = bcp[j];
     const int64_t ea = acp[j + 1], eb = bcp[j + 1];
@@ -1053,10 +1046,6 @@ __global__ void __launch_bounds__(256) k_merge2(int64_t ncol, const int64_t* __r
         const int x = l + r * kWave;
         sa[x] = ia + x < ea ? air[ia + x] : INT32_MAX;
         sb[x] = ib + x < eb ? bir[ib + x] : INT32_MAX;
-        if (SV) {   // coalesced value loads: the merge reads them from LDS
-          sva[x] = ia + x < ea ? (aval ? aval[ia + x] : V(1)) : V(0);
-          svb[x] = ib + x < eb ? (bval ? bval[ib + x] : V(1)) : V(0);
-        }
       }
       wave_sync();
       if (!FILL) {   // the merge needs strictly ascending rows per column: verify in the count pass
@@ -1109,7 +1098,7 @@ __global__ void __launch_bounds__(256) k_merge2(int64_t ncol, const int64_t* __r
       const int incl = pk & 1023;
       const int ptot = __shfl(pk, kWave - 1, kWave);
       const int tot = ptot & 1023, ta = (ptot >> 10) & 1023, tin = ptot >> 20;
-      if (FILL && !SV) {
+      if (FILL) {
         int64_t pos = o + incl - c;
 #pragma unroll
         for (int e = 0; e < PL; ++e)
@@ -1121,37 +1110,6 @@ __global__ void __launch_bounds__(256) k_merge2(int64_t ncol, const int64_t* __r
             cval[pos] = v;
             ++pos;
           }
-      }
-      if (SV) {
-        V ov[PL];
-#pragma unroll
-        for (int e = 0; e < PL; ++e) {
-          const int s = src[e];
-          V v = V(0);
-          if (head[e]) {
-            v = s >= 0 ? sva[s] : svb[-1 - s];
-            if (pair[e]) v = merge_pair<SRI, V>(v, svb[d0 + e - s]);   // part-1 half: (positions so far) - (part-0 taken)
-          }
-          ov[e] = v;
-        }
-        wave_sync();   // every lane's reads of the staged window are done: the output is staged over it
-        int p = incl - c;
-#pragma unroll
-        for (int e = 0; e < PL; ++e)
-          if (head[e]) {
-            sa[p] = row[e];
-            sva[p] = ov[e];
-            ++p;
-          }
-        wave_sync();
-#pragma unroll
-        for (int r = 0; r < PL; ++r) {   // coalesced stores of the window's merged entries
-          const int x = l + r * kWave;
-          if (x < tot) {
-            crow[o + x] = sa[x];
-            cval[o + x] = sva[x];
-          }
-        }
       }
       o += tot;
       ia += ta;

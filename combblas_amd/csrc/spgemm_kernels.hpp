@@ -110,9 +110,6 @@ constexpr int kSplitMin = 16;      // A columns at least this long get split-tab
 constexpr int kMaxSub = 2048;      // max subwindows per column (SUBW chosen so nrow/SUBW <= kMaxSub)
 constexpr int kItemUnits = CBG_ITEM_UNITS; // units of one heavy column per workgroup item (k_num_heavy)
 constexpr int kMaxParts = 32;      // symbolic parts per wide column (wider, hypersparse columns: windowed path)
-// 2^16-row block boundaries a rows-known unit may contain: the symbolic -> numeric row handoff stores 16-bit rows and
-// a unit (<= 2^19 rows, heavy_unit_known) carries the rank where each block boundary falls (KnownUnit::thr)
-constexpr int kKnownBlk = 8;
 
 template <typename V>
 struct DevCsc {
@@ -123,18 +120,10 @@ struct DevCsc {
 };
 
 // split table: for long A columns, tab[idx[k]*(nsub+1) + s] = (first entry with row >= s*SUBW) - cp[k]
-// symbolic -> numeric row handoff element: the whole row (CBG_ROWS16=0, default) or its low 16 bits (1, rebuilt by the
-// numeric pass from the unit's 2^16-row block thresholds).  The 16-bit form halves the handoff bytes (s20: 11.3 -> 5.6 GB
-// written and read) and took the symbolic pass 21.5 -> 21.3 ms, but the rebuild sits on the rows-known kernel's per-unit
-// critical path: heavy 31.2 -> 35.0 ms (profiles/r05f_rows16_ab_s20.txt)
-#ifndef CBG_ROWS16
-#define CBG_ROWS16 0
-#endif
-#if CBG_ROWS16
-typedef uint16_t HRow;
-#else
+// symbolic -> numeric row handoff element: the whole row.  (A 16-bit form rebuilt from per-unit 2^16-row block thresholds
+// halved the handoff bytes, s20 11.3 -> 5.6 GB, but the rebuild sat on the rows-known kernel's per-unit critical path:
+// heavy 31.2 -> 35.0 ms, profiles/r05f_rows16_ab_s20.txt; removed in round 6, it lives in git history.)
 typedef int32_t HRow;
-#endif
 struct UnitSeg;
 struct UnitRows;
 struct Split {
@@ -143,7 +132,7 @@ struct Split {
   int32_t nsub;         // subwindows in the row space
   int32_t log;          // log2(SUBW)
   const UnitSeg* useg;  // precomputed unit segments (k_unit_segs)
-  const HRow* hrows;    // sorted output rows of heavy columns written by the symbolic pass, low 16 bits (or null)
+  const HRow* hrows;    // sorted output rows of heavy columns written by the symbolic pass (or null)
   const UnitRows* urows;// per unit: where its rows lie in hrows (k_build_units)
   const int32_t* ptab;  // part table (k_part_table): ptab[k*pstride + p] = (first entry with row >= p*2^kPartLog) - cp[k]
   int32_t pstride;      // parts of the row space + 1 (0: no table)
@@ -892,8 +881,6 @@ struct HeavyOut {       // columns with nnz > kHeavy: list + nnz per subwindow
   // into its sorted output rows, written to `rows` at an offset reserved from `cursor` (capacity `cap`,
   // an upper bound of the heavy outputs); poff[h * kMaxParts + p] = offset of relative part p (or of
   // the whole column, p = 0); mode[h] = 1 whole column in one run, 2 per part, other = unavailable.
-  // Only the low 16 bits of each row are stored: the numeric pass rebuilds the high bits from the unit's
-  // per-2^16-row-block rank thresholds (KnownUnit::thr, from the subwindow counts), so the handoff is 2 B per row.
   HRow* rows;
   unsigned long long* cursor;
   unsigned long long cap;
@@ -1127,26 +1114,15 @@ constexpr int kPartNT = CBG_PART_NT;
 #ifndef CBG_HEAVY_DYNAMIC
 #define CBG_HEAVY_DYNAMIC 1
 #endif
-#ifndef CBG_KNOWN_OTF
-#define CBG_KNOWN_OTF 0   // 1: k_num_heavy_known computes its unit segments from the split table (r03t: heavy +8 ms)
-#endif
-#ifndef CBG_SYM_SHORT_SEARCH
-#define CBG_SYM_SHORT_SEARCH 0   // 1: k_sym_part narrows a short A column to the part's rows by binary search (r03s: +0.8 ms)
-#endif
-#ifndef CBG_SYM_ROWS_WAVE
-#define CBG_SYM_ROWS_WAVE 0   // 1: k_sym_part emits its rows word-major per wave (measured slower, r03d)
-#endif
+// Measured and removed (round 6; the variants live in git history): k_num_heavy_known computing its unit segments from
+// the split table (r03t: heavy +8 ms); k_sym_part narrowing a short A column by binary search (r03s: +0.8 ms), emitting
+// its rows word-major per wave (r03d), staging the next part's first chunk across the current one (r05d: +0.5 ms) and
+// sweeping every part of a column in one workgroup (r05k: +1.4 ms).
 #ifndef CBG_SYM_TESTOR
 #define CBG_SYM_TESTOR 1   // k_sym_part reads a bitmap word before setting a bit (0: no-return ds_or only)
 #endif
 #ifndef CBG_SYM_ROWS_LDS
 #define CBG_SYM_ROWS_LDS 1 // k_sym_part stages a part's rows in its (then idle) bitmap LDS and stores them coalesced (s20 symbolic 21.6 -> 20.7 ms, profiles/r05h_rows_lds_ab.txt; 0: each thread stores its own rows)
-#endif
-#ifndef CBG_SYM_COLLOOP
-#define CBG_SYM_COLLOOP 0  // 1: k_sym_part items are whole columns (every part swept by one workgroup)
-#endif
-#ifndef CBG_SYM_PREFETCH
-#define CBG_SYM_PREFETCH 0 // 1: k_sym_part stages the next part's first chunk while the current part runs (measured +0.5 ms at s20, r05d)
 #endif
 // first symbolic class (LOGT = class + 5) cut into parts: bitmaps larger than one part; every such
 // column has flop > kHeavy (2*flop > 2^(class+4) words), so the heavy lists can hold it
@@ -1166,12 +1142,8 @@ __global__ void k_part_items(const int32_t* __restrict__ list, int64_t count, in
     if (np <= maxparts) {
       const int h = atomicAdd(ho.n, 1);
       ho.cols[h] = j;
-#if CBG_SYM_COLLOOP
-      items[atomicAdd(nitems, 1)] = PartItem{j, np, h};   // one item per column: k_sym_part sweeps its np parts
-#else
       const int e = atomicAdd(nitems, np);
       for (int p = 0; p < np; ++p) items[e + p] = PartItem{j, p, h};
-#endif
     } else {
       wlist[atomicAdd(nwin, 1)] = j;
     }
@@ -1182,6 +1154,8 @@ __global__ void k_part_items(const int32_t* __restrict__ list, int64_t count, in
 // stay below NT * 2^kPartLog / kGroupSym <= 2^25 whatever B holds -- a segment is one A column narrowed to one part,
 // at most 2^kPartLog entries since A's rows ascend strictly -- so repeated rows in a B column cannot overflow) lets four 512-thread workgroups share a CU's LDS and the kernel run at <= 64 VGPRs: 8 waves per
 // SIMD instead of 6 (s20 symbolic 23.4 -> 22.1 ms, s21 80.5 -> 75.8 ms, profiles/r04e_*); 64-bit otherwise.
+static_assert(((int64_t)kPartNT << kPartLog) < INT32_MAX,
+              "a chunk's staged multiplies (NT segments of <= 2^kPartLog entries each) fit 32-bit offsets");
 template <int NT, typename IX>
 constexpr size_t sym_part_lds() {
   return (size_t)(1 << (kPartLog - 5)) * 4 + (size_t)NT * (2 * sizeof(IX) + 5) + (size_t)(NT / kWave + 1) * 8 +
@@ -1208,7 +1182,6 @@ k_sym_part(const PartItem* __restrict__ items, const int* __restrict__ count_dev
   uint8_t* bvs = (uint8_t*)(lens + NT);            // NT
   const SegBuf<uint8_t, SymIx> sb{qb, off, bvs, scr, lens};
   const int count = *count_dev;
-  const int tid = threadIdx.x;
   // the segment [a0, a1) of B nonzero b (A column Bir[b]) inside part p0 (absolute part index) of the row space
   auto seg_in_part = [&](int32_t k, int32_t p0, int64_t& a0, int64_t& a1) {
     const int32_t pr0 = p0 << kPartLog;
@@ -1221,73 +1194,17 @@ k_sym_part(const PartItem* __restrict__ items, const int* __restrict__ count_dev
       const int32_t* t = spl.tab + (int64_t)spl.idx[k] * (spl.nsub + 1);
       a0 = c0 + t[pr0 >> spl.log];
       a1 = c0 + t[min(spl.nsub, (int32_t)(((int64_t)pr0 + (1 << kPartLog)) >> spl.log))];
-    } else if (CBG_SYM_SHORT_SEARCH) {   // short column: its rows inside the part by binary search
-      a0 = lower_bound_rows(Air, c0, c1, pr0);
-      a1 = lower_bound_rows(Air, a0, c1, (int64_t)pr0 + (1 << kPartLog));
     } else {
       a0 = c0;
       a1 = c1;
     }
   };
-#if CBG_SYM_PREFETCH
-  // the next item's first chunk, staged across the current item in four dependent steps (header; span + B column;
-  // this thread's B row; its A segment), each issued where the previous one has long landed, so a part's chain
-  // starts from registers instead of four round trips to memory
-  PartItem nit{-1, 0, 0};
-  int32_t np0 = 0, nk = -1, plen = 0;
-  int64_t nbs = 0, nbe = 0, pa0 = 0;
-  if (blockIdx.x < count) {
-    nit = items[blockIdx.x];
-    const int2 spn = span[nit.j];
-    np0 = (spn.x >> kPartLog) + nit.p;
-    nbs = Bcp[nit.j];
-    nbe = Bcp[nit.j + 1];
-    nk = nbs + tid < nbe ? Bir[nbs + tid] : -1;
-    if (nk >= 0) {
-      int64_t a1 = 0;
-      seg_in_part(nk, np0, pa0, a1);
-      plen = (int32_t)(a1 - pa0);
-    }
-  }
-#endif
   int64_t cbase = 0, cleft = 0;   // thread 0: this workgroup's reserved rows (HeavyOut::chunk)
   STAMP_DECL
   STAMP(31);
-#if CBG_SYM_COLLOOP
-  // items are columns (j, parts, h): a workgroup sweeps every part of its column, keeping each thread's first-chunk
-  // B row and A column start in registers, so a part after the first stages its segments from the part table alone
-  PartItem ci{0, 0, 0};
-  int pp = 0;
-  int64_t cbs = 0, cbe = 0, cc0 = 0;
-  int32_t ck = -1;
-  for (int i = (int)blockIdx.x - (int)gridDim.x;;) {
-    if (pp >= ci.p) {   // the next column (uniform)
-      i += gridDim.x;
-      if (i >= count) break;
-      ci = items[i];
-      pp = 0;
-      cbs = Bcp[ci.j];
-      cbe = Bcp[ci.j + 1];
-      ck = cbs + tid < cbe ? Bir[cbs + tid] : -1;
-      cc0 = ck >= 0 ? Acp[ck] : 0;
-      if (ci.p <= 0) continue;
-    }
-    const PartItem it{ci.j, pp++, ci.h};
-    const int64_t bs = cbs, be = cbe;
-#else
   for (int i = blockIdx.x; i < count; i += gridDim.x) {
-#endif
-#if CBG_SYM_PREFETCH
-    const PartItem it = nit;
-    const int64_t bs = nbs, be = nbe;
-    const int64_t fa0 = pa0;   // this thread's first-chunk segment [fa0, fa0 + flen)
-    const int32_t flen = plen;
-    const int in = i + gridDim.x;
-    if (in < count) nit = items[in];     // step 1 for the next item
-#elif !CBG_SYM_COLLOOP
     const PartItem it = items[i];
     const int64_t bs = Bcp[it.j], be = Bcp[it.j + 1];
-#endif
     const int2 sp = span[it.j];
     const int32_t r0 = ((sp.x >> kPartLog) + it.p) << kPartLog;
     const int32_t s0 = r0 >> spl.log;
@@ -1298,21 +1215,6 @@ k_sym_part(const PartItem* __restrict__ items, const int* __restrict__ count_dev
     __syncthreads();
     STAMP(26);
     auto seg = [&](int64_t b, int64_t& a0, int64_t& a1, uint8_t&) {
-#if CBG_SYM_PREFETCH
-      if (b < bs + NT) {   // the first chunk: prefetched
-        a0 = fa0;
-        a1 = fa0 + flen;
-        return;
-      }
-#endif
-#if CBG_SYM_COLLOOP
-      if (spl.ptab && b < bs + NT) {   // the first chunk: this thread's B row and A column start are in registers
-        const int32_t* t = spl.ptab + (int64_t)ck * spl.pstride + ((sp.x >> kPartLog) + it.p);
-        a0 = cc0 + t[0];
-        a1 = cc0 + t[1];
-        return;
-      }
-#endif
       seg_in_part(Bir[b], (sp.x >> kPartLog) + it.p, a0, a1);
     };
     auto ld = [&](int64_t q) { return Air[q]; };
@@ -1330,15 +1232,6 @@ k_sym_part(const PartItem* __restrict__ items, const int* __restrict__ count_dev
     };
     if constexpr (VEC) for_each_multiply<NT, false, kUnrollSym, kGroupSym, uint8_t>(bs, be, sb, seg, ld4, ins);
     else for_each_multiply<NT, false, kUnrollSym, kGroupSym, uint8_t>(bs, be, sb, seg, ld, ins);
-#if CBG_SYM_PREFETCH
-    if (in < count) {   // steps 2 and 3 for the next item
-      const int2 spn = span[nit.j];
-      np0 = (spn.x >> kPartLog) + nit.p;
-      nbs = Bcp[nit.j];
-      nbe = Bcp[nit.j + 1];
-      nk = nbs + tid < nbe ? Bir[nbs + tid] : -1;
-    }
-#endif
     __syncthreads();
     STAMP(27);
     int c = 0;
@@ -1356,15 +1249,21 @@ k_sym_part(const PartItem* __restrict__ items, const int* __restrict__ count_dev
       int64_t off = -1;
       if (ho.rows && ptot > 0) {
         if (ho.chunk > 0) {   // rows from this workgroup's reservation: a global atomic every few parts, not every one
-          if (ptot > cleft) {
-            const int64_t want = max((int64_t)ptot, ho.chunk);
-            cbase = reserve_rows(ho, want);
-            cleft = cbase >= 0 ? want : 0;
-          }
-          if (cleft >= ptot) {
-            off = cbase;
-            cbase += ptot;
-            cleft -= ptot;
+          // A part that does not fit the leftover gets its own exact reservation while the leftover is still >= chunk/8
+          // (or the part is over half a chunk); a new chunk replaces a leftover < chunk/8, so at most 1/8 of a chunk is
+          // dropped per chunk that was at least 7/8 used: waste <= used/7 + one chunk per workgroup (host sizing)
+          if (ptot > cleft && (8 * cleft >= ho.chunk || 2 * (int64_t)ptot > ho.chunk)) {
+            off = reserve_rows(ho, ptot);
+          } else {
+            if (ptot > cleft) {
+              cbase = reserve_rows(ho, ho.chunk);
+              cleft = cbase >= 0 ? ho.chunk : 0;
+            }
+            if (ptot <= cleft) {
+              off = cbase;
+              cbase += ptot;
+              cleft -= ptot;
+            }
           }
         } else {
           off = reserve_rows(ho, ptot);
@@ -1375,45 +1274,9 @@ k_sym_part(const PartItem* __restrict__ items, const int* __restrict__ count_dev
       misc[4] = (int)(off & 0xffffffff);
       misc[5] = (int)(off >> 32);
     }
-#if CBG_SYM_PREFETCH
-    if (in < count) {   // step 4 for the next item: its first-chunk segment
-      pa0 = 0;
-      plen = 0;
-      if (nk >= 0) {
-        int64_t a1 = 0;
-        seg_in_part(nk, np0, pa0, a1);
-        plen = (int32_t)(a1 - pa0);
-      }
-    }
-#endif
     __syncthreads();
     STAMP(28);
     const int64_t off = (int64_t)(uint32_t)misc[4] | ((int64_t)misc[5] << 32);
-#if CBG_SYM_ROWS_WAVE
-    if (off >= 0) {
-      // this part's sorted rows for the numeric pass, word-major per wave: at step s the wave's 64 lanes take
-      // 64 consecutive bitmap words, a wave scan of their popcounts places them, and each lane writes its word's
-      // rows -- the stores of one instruction fall in one short run of positions (coalesced), and a lane's
-      // serial work is one word (<= 32 rows), not its 16 words
-      const int l = lane_id();
-      const int w0 = (threadIdx.x / kWave) * kWave * WPT;
-      int64_t base = off + __shfl(ex, 0, kWave);   // rows of the words before the wave's (thread order = word order)
-      for (int s = 0; s < WPT; ++s) {
-        const int wi = w0 + s * kWave + l;
-        uint32_t wd = tab[wi];
-        const int c = __popc(wd);
-        const int inc = wave_incl_scan(c);
-        int64_t pos = base + inc - c;
-        const int32_t rb = r0 + 32 * wi;
-        while (wd) {
-          const int b = __ffs(wd) - 1;
-          wd &= wd - 1;
-          ho.rows[pos++] = (HRow)(rb + b);
-        }
-        base += __shfl(inc, kWave - 1, kWave);
-      }
-    }
-#else
     const int ptot_u = misc[0];
     if (CBG_SYM_ROWS_LDS && off >= 0 && ptot_u <= T) {
       // the bitmap is in registers (wds): its LDS holds the part's rows in order, then the workgroup copies them out
@@ -1442,7 +1305,6 @@ k_sym_part(const PartItem* __restrict__ items, const int* __restrict__ count_dev
         }
       }
     }
-#endif
     if (threadIdx.x == 0 && misc[0]) atomicAdd((unsigned long long*)&nnz[it.j], (unsigned long long)misc[0]);
     const int32_t sf = max(s0, sp.x >> spl.log), sl = min(s1 - 1, sp.y >> spl.log);
     int32_t* dst = ho.sub + (int64_t)it.h * ho.nsub;
@@ -1732,9 +1594,6 @@ __global__ void k_build_units(int H, const int32_t* __restrict__ cols, const int
 // Short A columns are given whole (rows outside a unit are dropped at insert time) unless their row
 // range misses the unit entirely.
 template <class SRT, int LOGT, int NT>
-__device__ __forceinline__ bool heavy_unit_known(const Unit& un, int2 usp, const UnitRows& ur);
-
-template <class SRT, int LOGT, int NT>
 __global__ void __launch_bounds__(256) k_unit_segs(const int32_t* __restrict__ cols, const int32_t* __restrict__ nunits,
                                                    const int64_t* __restrict__ segoff, Unit* __restrict__ units,
                                                    int32_t nsub, const int64_t* __restrict__ Acp,
@@ -1748,22 +1607,6 @@ __global__ void __launch_bounds__(256) k_unit_segs(const int32_t* __restrict__ c
   const int64_t base = segoff[h];
   Unit* U = units + (int64_t)h * nsub;
   for (int u = threadIdx.x; u < nu; u += blockDim.x) U[u].segbase = base + (int64_t)u * nb;
-#if CBG_KNOWN_OTF
-  // units the rows-known kernel takes compute their segments on the fly: when every unit of the column is
-  // one of them, nothing is stored
-  __shared__ int s_other;
-  if (threadIdx.x == 0) s_other = 0;
-  __syncthreads();
-  if (sp.urows) {
-    for (int u = threadIdx.x; u < nu; u += blockDim.x)
-      if (!heavy_unit_known<SRT, LOGT, NT>(U[u], uspan[(int64_t)h * nsub + u], sp.urows[(int64_t)h * nsub + u]))
-        s_other = 1;
-  } else if (threadIdx.x == 0) {
-    s_other = 1;
-  }
-  __syncthreads();
-  if (!s_other) return;
-#endif
   for (int64_t i = threadIdx.x; i < nb; i += blockDim.x) {
     const int32_t k = Bir[bs + i];
     const int64_t c0 = Acp[k], c1 = Acp[k + 1];
@@ -2131,11 +1974,7 @@ __device__ __forceinline__ void num_insert(Table<typename SRT::Acc>& t, bool den
     if (SRT::kAddIsError && (old & bit)) aerr = 1;
     SRT::acc(&t.vals[o], x);
   } else {
-#ifdef CBG_FAKE_INSERT
-    t.keys[mono_home(it.r, wk.lo, mult)] = it.r;   // diagnostic timing only: no probing, no atomics
-#else
     if (!hash_insert_num<SRT>(t, it.r, mono_home(it.r, wk.lo, mult), x, &aerr)) ovf = 1;
-#endif
   }
 }
 
@@ -2588,13 +2427,13 @@ __device__ __forceinline__ bool heavy_unit_known(const Unit& un, int2 usp, const
   const int64_t spn = (int64_t)usp.y - usp.x + 1;
   const int64_t nw = (spn + 31) >> 5;
   const int64_t cpad = (un.cnt + 1) & ~1;
+  // nw <= 2T also bounds the span to 64T = 2^19 rows
   return !SRT::kAddIsError && CBG_RANK_MODE && ur.np >= 1 && ur.np <= 3 && spn > T && un.cnt <= T &&
-         (usp.y >> 16) - (usp.x >> 16) <= kKnownBlk && un.cnt < 0xffff &&
          un.cnt <= known_rpt<NT>() * NT && nw <= 2 * (int64_t)T &&
          cpad * (int64_t)sizeof(Acc) + 4 * (nw + 1) <= kRankBytes;
 }
 
-// everything k_num_heavy_known needs about one unit, in one 88-byte record
+// everything k_num_heavy_known needs about one unit, in one 72-byte record
 struct KnownUnit {
   int64_t outoff;       // first output in C
   int64_t segbase;      // the unit's (unit, B nonzero) segments in Split::useg
@@ -2603,43 +2442,21 @@ struct KnownUnit {
   int32_t o1, o2;       // ranks where pieces 1 and 2 start (o1 = o2 = cnt: one piece)
   int32_t cnt, nb;      // outputs; B nonzeros of the column
   int32_t lo, hi;       // the unit's row range [lo, hi]
-  uint16_t thr[kKnownBlk]; // rank of the unit's first row in 2^16-row block (lo >> 16) + 1 + t (0xffff: none)
 };
-static_assert(sizeof(KnownUnit) == 88, "KnownUnit is 22 words");
+static_assert(sizeof(KnownUnit) == 72, "KnownUnit is 18 words");
 constexpr int kKnownWords = (int)(sizeof(KnownUnit) / 4);
 
 __device__ __forceinline__ int64_t known_row_src(const KnownUnit& H, int i) {
   return i < H.o1 ? H.roff[0] + i : i < H.o2 ? H.roff[1] + (i - H.o1) : H.roff[2] + (i - H.o2);
 }
 
-// row of rank i of the unit from its stored low 16 bits: the 2^16-row block is lo's plus the thresholds passed
-__device__ __forceinline__ int32_t known_row(const KnownUnit& H, int i, int32_t low) {
-  int blk = H.lo >> 16;
-#pragma unroll
-  for (int t = 0; t < kKnownBlk; ++t) blk += i >= (int)H.thr[t];
-  return (blk << 16) | low;
-}
-
-// CBG_TICKET_OPAQUE=1 (default): the rows-known kernel's unit claim goes through an address the compiler cannot prove
-// uniform, so it is not rewritten into a wave-aggregated atomic that waits for its result at once (s20 heavy 31.1 ->
-// 31.0 ms, profiles/r05g_variants_s20.txt)
-#ifndef CBG_TICKET_OPAQUE
-#define CBG_TICKET_OPAQUE 1
-#endif
-// CBG_CLAIM_AHEAD=1: the rows-known kernel claims unit k+3 at the top of unit k and publishes it at the end; 0: it claims
-// unit k+2 at the top of unit k and reads it after the barrier closing step a (round 4)
-// CBG_VAL_PAIRS=1: the rows-known kernel writes 8-byte values two per 16-byte (nontemporal) store
-#ifndef CBG_VAL_PAIRS
-#define CBG_VAL_PAIRS 0
-#endif
-#ifndef CBG_CLAIM_AHEAD
-#define CBG_CLAIM_AHEAD 1
-#endif
-// CBG_NT_OUT=1 (default): k_num_heavy_known writes C with nontemporal stores, streamed past the L2 that serves A's
-// gathers (s20 heavy 31.1 -> 30.4 ms, profiles/r05g_variants_s20.txt)
-#ifndef CBG_NT_OUT
-#define CBG_NT_OUT 1
-#endif
+// The rows-known kernel takes its units from a device ticket (CBG_HEAVY_DYNAMIC), claiming unit k+3 at the top of unit k
+// and publishing it at the end, so the atomic's round trip is never waited on.  The claim goes through an address the
+// compiler cannot prove uniform: the atomic optimizer's wave-aggregated form needs the old value at once (an s_waitcnt at
+// the top of every unit; s20 heavy 31.1 -> 31.0 ms, profiles/r05g_variants_s20.txt).  C is written with nontemporal
+// stores, streamed past the L2 that serves A's gathers (s20 heavy 31.1 -> 30.4 ms, same file).  Measured and removed in
+// round 6 (git history): claiming two ahead, paired 16-byte value stores (no change either way).
+static_assert(CBG_HEAVY_DYNAMIC, "k_num_heavy_known claims its units from the device ticket");
 // k_num_heavy_known: groups of CBG_GROUP_KNOWN entries, CBG_UNROLL_KNOWN groups in flight per lane
 // (s20 f64: G=2/U=4 32.4 ms, G=4/U=2 34.5, G=1/U=8 38.1, G=8/U=1 41.4; G=4/U=3 spills)
 #ifndef CBG_UNROLL_KNOWN
@@ -2692,22 +2509,11 @@ __global__ void __launch_bounds__(NT) k_num_heavy_known(const KnownUnit* __restr
   const int tid = threadIdx.x;
   const int64_t n = (int64_t)*nku;
   // units k (current), k1 (next: header and rows in flight), k2 (claimed one unit earlier, header loaded during unit
-  // k); with the ticket, unit k3 is claimed at the top of unit k and its number published at the end of it, so the
-  // atomic's round trip is never waited on
-#if CBG_HEAVY_DYNAMIC && CBG_CLAIM_AHEAD
+  // k); unit k3 is claimed at the top of unit k and its number published at the end of it
   __shared__ unsigned long long s_claim;
   if (tid == 0) s_claim = atomicAdd(ticket, 3ull);
   __syncthreads();
   int64_t k = (int64_t)s_claim, k1 = k + 1, k2 = k + 2;
-#elif CBG_HEAVY_DYNAMIC
-  __shared__ unsigned long long s_claim;
-  if (tid == 0) s_claim = atomicAdd(ticket, 2ull);
-  __syncthreads();
-  int64_t k = (int64_t)s_claim, k1 = k + 1;
-#else
-  const int64_t G = gridDim.x;
-  int64_t k = blockIdx.x, k1 = k + G;
-#endif
   if (k >= n) return;   // uniform
   STAMP_DECL
   STAMP(0);
@@ -2719,32 +2525,13 @@ __global__ void __launch_bounds__(NT) k_num_heavy_known(const KnownUnit* __restr
   }
   __syncthreads();
   int32_t rr[RPT];
-  // rows i = tid + q*NT (coalesced; clamped loads)
-  // the aligned 32-bit word holding the row's stored low 16 bits: the loads stay in flight during the current unit's
-  // sweep, and fix_rows (which needs them) runs after it.  (A 16-bit load is zero-extended by a mask that the compiler
-  // places right after it, waiting for the load there; the scratch has 2 bytes of padding for the last word.)
+  // rows i = tid + q*NT (coalesced; clamped loads): the loads stay in flight during the current unit's sweep
   auto load_rows = [&](const KnownUnit& H) {
 #pragma unroll
     for (int q = 0; q < RPT; ++q) {
       const int i = tid + q * NT;
-      const int64_t src = known_row_src(H, i < H.cnt ? i : 0);
-#if CBG_ROWS16
-      rr[q] = *(const int32_t*)(spl.hrows + (src & ~(int64_t)1));
-#else
-      rr[q] = spl.hrows[src];
-#endif
+      rr[q] = spl.hrows[known_row_src(H, i < H.cnt ? i : 0)];
     }
-  };
-  auto fix_rows = [&](const KnownUnit& H) {   // full rows from the unit's 2^16-row block thresholds
-#if CBG_ROWS16
-#pragma unroll
-    for (int q = 0; q < RPT; ++q) {
-      const int i = tid + q * NT;
-      const int ic = i < H.cnt ? i : 0;
-      const int32_t w = rr[q];
-      rr[q] = known_row(H, ic, (known_row_src(H, ic) & 1) ? (int32_t)((uint32_t)w >> 16) : (w & 0xffff));
-    }
-#endif
   };
   // every wave's last row per q, for the pair-boundary test of the next wave's first lane
   const int lane = lane_id(), wv = tid / kWave;
@@ -2759,27 +2546,9 @@ __global__ void __launch_bounds__(NT) k_num_heavy_known(const KnownUnit* __restr
     a0 = a1 = 0;
     bv = V(0);
     if (i < H.nb) {
-#if CBG_KNOWN_OTF
-      // the segment of this B nonzero inside the unit's rows, from the split table (what k_unit_segs would have
-      // stored, narrowed to the unit's row span [lo, hi]; prefetched a chunk ahead, so the extra levels of
-      // loads overlap the current sweep)
-      const int32_t k = B.ir[H.bs + i];
-      const int64_t c0 = A.cp[k], c1 = A.cp[k + 1];
-      if (c1 - c0 >= kSplitMin) {
-        const int32_t* t = spl.tab + (int64_t)spl.idx[k] * (spl.nsub + 1);
-        a0 = c0 + t[H.lo >> spl.log];
-        a1 = c0 + t[(H.hi >> spl.log) + 1];
-      } else if (c1 > c0 && A.ir[c1 - 1] >= H.lo && A.ir[c0] <= H.hi) {
-        a0 = c0;
-        a1 = c1;
-      } else {
-        a0 = a1 = c0;
-      }
-#else
       const UnitSeg g = spl.useg[H.segbase + i];
       a0 = g.a0;
       a1 = g.a1;
-#endif
       bv = load_val(B.val, H.bs + i);
     }
   };
@@ -2789,7 +2558,6 @@ __global__ void __launch_bounds__(NT) k_num_heavy_known(const KnownUnit* __restr
     const KnownUnit H0 = hdr[0];
     load_rows(H0);
     fetch(H0, 0, pa0, pa1, pbv);
-    fix_rows(H0);
     put_bnd();
     __syncthreads();
   }
@@ -2797,11 +2565,7 @@ __global__ void __launch_bounds__(NT) k_num_heavy_known(const KnownUnit* __restr
     STAMP(1);
     const KnownUnit H = hdr[slot];
     const bool has1 = k1 < n;
-#if CBG_HEAVY_DYNAMIC && !CBG_CLAIM_AHEAD
-    if (tid == 0) s_claim = atomicAdd(ticket, 1ull);   // read after the barrier closing step a
-#elif CBG_HEAVY_DYNAMIC
     unsigned long long k3 = 0;
-#if CBG_TICKET_OPAQUE
     // through an address the compiler cannot prove uniform: the atomic optimizer's wave-aggregated form needs the old
     // value right away (an s_waitcnt on the atomic at the top of every unit); this plain form waits only where k3 is
     // used, at the end of the unit
@@ -2810,10 +2574,6 @@ __global__ void __launch_bounds__(NT) k_num_heavy_known(const KnownUnit* __restr
       asm volatile("v_mov_b32 %0, 0" : "=v"(z));
       k3 = atomicAdd(ticket + z, 1ull);
     }
-#else
-    if (tid == 0) k3 = atomicAdd(ticket, 1ull);   // published at the end of this unit
-#endif
-#endif
     const int32_t lo = __builtin_amdgcn_readfirstlane(H.lo), hi = __builtin_amdgcn_readfirstlane(H.hi);
     const int32_t cnt = __builtin_amdgcn_readfirstlane(H.cnt);
     const int cpad = (cnt + 1) & ~1;
@@ -2826,11 +2586,7 @@ __global__ void __launch_bounds__(NT) k_num_heavy_known(const KnownUnit* __restr
       const int32_t r = rr[q];
       const int32_t up = __shfl_up(r, 1, kWave);   // row i-1 within the wave
       if (i < cnt) {
-#if CBG_NT_OUT
         __builtin_nontemporal_store(r, &out.row[H.outoff + i]);
-#else
-        out.row[H.outoff + i] = r;
-#endif
         const int pr = (r - lo) >> 6;
         const int32_t p = lane ? up : (wv ? bnd[(wv - 1) * RPT + q] : (q ? bnd[(NW - 1) * RPT + q - 1] : r));
         if (i == 0 || ((p - lo) >> 6) != pr) {
@@ -2843,11 +2599,6 @@ __global__ void __launch_bounds__(NT) k_num_heavy_known(const KnownUnit* __restr
     STAMP(6);
     __syncthreads();
     STAMP(7);
-#if !CBG_HEAVY_DYNAMIC
-    const int64_t k2 = k + 2 * G;
-#elif !CBG_CLAIM_AHEAD
-    const int64_t k2 = (int64_t)s_claim;
-#endif
     const bool has2 = k2 < n;
     uint32_t nh = 0;   // header of unit k2, written to this unit's ring slot at the end
     if (tid < kKnownWords && has2) nh = kw[k2 * kKnownWords + tid];
@@ -2919,45 +2670,16 @@ __global__ void __launch_bounds__(NT) k_num_heavy_known(const KnownUnit* __restr
       STAMP(4);
     }
     // d. values out, row order
-#if CBG_VAL_PAIRS
-    if constexpr (sizeof(V) == 8) {   // two values per 16-byte store from the first 16-byte aligned output on
-      typedef V v2 __attribute__((ext_vector_type(2)));
-      const int64_t ob = H.outoff;
-      const int head = (int)(ob & 1) < cnt ? (int)(ob & 1) : cnt;   // one value before the aligned part
-      if (tid < head) __builtin_nontemporal_store(SRT::out(vals[0], A.val, B.val), &out.val[ob]);
-      const int npair = (cnt - head) >> 1;
-      for (int p = tid; p < npair; p += NT) {
-        const int i = head + 2 * p;
-        v2 w;
-        w.x = SRT::out(vals[i], A.val, B.val);
-        w.y = SRT::out(vals[i + 1], A.val, B.val);
-        __builtin_nontemporal_store(w, (v2*)&out.val[ob + i]);
-      }
-      if (((cnt - head) & 1) && tid == 0) __builtin_nontemporal_store(SRT::out(vals[cnt - 1], A.val, B.val), &out.val[ob + cnt - 1]);
-    } else {
-      for (int i = tid; i < cnt; i += NT) __builtin_nontemporal_store(SRT::out(vals[i], A.val, B.val), &out.val[H.outoff + i]);
-    }
-#elif CBG_NT_OUT
     for (int i = tid; i < cnt; i += NT) __builtin_nontemporal_store(SRT::out(vals[i], A.val, B.val), &out.val[H.outoff + i]);
-#else
-    for (int i = tid; i < cnt; i += NT) out.val[H.outoff + i] = SRT::out(vals[i], A.val, B.val);
-#endif
     STAMP(10);
     if (tid < kKnownWords && has2) hw[slot * kKnownWords + tid] = nh;
-    if (has1) {
-      fix_rows(hdr[slot ^ 1]);
-      put_bnd();
-    }
-#if CBG_HEAVY_DYNAMIC && CBG_CLAIM_AHEAD
+    if (has1) put_bnd();
     if (tid == 0) s_claim = k3;
-#endif
     __syncthreads();
     STAMP(5);
     k = k1;
     k1 = k2;
-#if CBG_HEAVY_DYNAMIC && CBG_CLAIM_AHEAD
     k2 = (int64_t)s_claim;   // k3: published before the barrier above; rewritten only after the next one
-#endif
   }
 }
 
@@ -3023,16 +2745,6 @@ __global__ void k_heavy_items_split(int H, const int32_t* __restrict__ cols, con
       K.nb = nb;
       K.lo = sp.x;
       K.hi = sp.y;
-      {   // rank thresholds of the 2^16-row blocks inside the unit (subwindows never straddle one: log <= 16)
-        int nt = 0, acc = 0;
-        int32_t blk = sp.x >> 16;
-        for (int32_t s = un.s0; s < un.s1; ++s) {
-          const int32_t sb = (int32_t)(((int64_t)s << log) >> 16);
-          while (blk < sb && nt < kKnownBlk) { K.thr[nt++] = (uint16_t)acc; ++blk; }
-          acc += sub[(int64_t)h * nsub + s];
-        }
-        for (; nt < kKnownBlk; ++nt) K.thr[nt] = 0xffff;
-      }
       known[bk++] = K;
     } else {
       if (u0 < 0) u0 = u;

@@ -106,6 +106,10 @@ inline cbg_ctx* context(int device = -1) {
   static thread_local int dev = 0;
   if (device >= 0 && ctx && device != dev) { cbg_destroy(ctx); ctx = nullptr; }
   if (!ctx) {
+    // the library writes structs this header allocates (cbg_profile, cbg_grid_stats): refuse another ABI version
+    if (cbg_abi_version() != CBG_ABI_VERSION)
+      throw std::runtime_error("cbg_abi_version: libcbgpu.so is ABI " + std::to_string(cbg_abi_version()) +
+                               ", this header is ABI " + std::to_string(CBG_ABI_VERSION));
     dev = device >= 0 ? device : node_local_device();
     check(cbg_init(dev, &ctx), "cbg_init");
   }
@@ -557,13 +561,32 @@ struct GridCacheEntry {
 struct GridCache {
   std::vector<GridCacheEntry> v;
 };
+// every live cache: the reference's CommGrid/CCGrid often never free their communicators (CCGrid.h keeps rowWorld),
+// and MPI_Finalize runs delete callbacks only on MPI_COMM_SELF -- so a COMM_SELF attribute (set with the first cache)
+// destroys whatever grids are still cached when MPI finalizes
+inline std::vector<GridCache*>& live_grid_caches() {
+  static std::vector<GridCache*> v;
+  return v;
+}
 inline int grid_cache_delete(MPI_Comm, int, void* attr, void*) {
+  auto& live = live_grid_caches();
+  live.erase(std::remove(live.begin(), live.end(), (GridCache*)attr), live.end());
   delete (GridCache*)attr;
+  return MPI_SUCCESS;
+}
+inline int grid_caches_finalize(MPI_Comm, int, void*, void*) {
+  auto& live = live_grid_caches();
+  for (GridCache* gc : live) gc->v.clear();   // the grids go; the (emptied) caches stay with their communicators
   return MPI_SUCCESS;
 }
 inline int grid_cache_keyval() {
   static int kv = MPI_KEYVAL_INVALID;
-  if (kv == MPI_KEYVAL_INVALID) MPI_Comm_create_keyval(MPI_COMM_NULL_COPY_FN, &grid_cache_delete, &kv, nullptr);
+  if (kv == MPI_KEYVAL_INVALID) {
+    MPI_Comm_create_keyval(MPI_COMM_NULL_COPY_FN, &grid_cache_delete, &kv, nullptr);
+    int fkv = MPI_KEYVAL_INVALID;
+    MPI_Comm_create_keyval(MPI_COMM_NULL_COPY_FN, &grid_caches_finalize, &fkv, nullptr);
+    MPI_Comm_set_attr(MPI_COMM_SELF, fkv, nullptr);
+  }
   return kv;
 }
 inline int& grid_creations() {
@@ -579,6 +602,7 @@ inline cbg_grid* cached_grid(MPI_Comm world, MPI_Comm row, MPI_Comm col, MPI_Com
   if (!flag || !gc) {
     gc = new GridCache;
     MPI_Comm_set_attr(row, kv, gc);
+    live_grid_caches().push_back(gc);
   }
   const bool mpi = grid_over_mpi();
   for (GridCacheEntry& e : gc->v)

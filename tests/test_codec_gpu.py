@@ -117,3 +117,26 @@ def test_profile_heavy_counts(gpu_ctx):
     assert p["heavy_multiplies"] == int(flop[heavy].sum())
     assert p["heavy_nnz_b"] == int(cnt[heavy].sum())
     assert p["heavy_nnz_c"] == int(nz[heavy].sum())
+
+
+def test_codec_five_byte_varints_across_lanes_and_steps(gpu_ctx):
+    """Varint integer values in [2^28, 2^32) take 5 bytes, the longest code: the decoder finds a code's start by looking
+    back into the previous lane or the carried lane 63 of the previous 64-byte step.  Long columns (several thousand
+    encoded bytes) with 5-byte codes at every offset modulo 64 -- so they straddle lane and step boundaries -- mixed
+    with 1-byte codes, still choose the varint form and round trip bit for bit; rows with gaps of every code length."""
+    rng = np.random.default_rng(17)
+    n = (1 << 30) + 12345
+    cols = []
+    for c in range(6):
+        m = 3000 + 17 * c
+        gaps = rng.choice([1, 2, 200, 20000, 3_000_000], m, p=[0.6, 0.2, 0.1, 0.07, 0.03])
+        rows = np.cumsum(gaps) - 1
+        rows = rows[rows < n]
+        v = rng.integers(0, 100, len(rows)).astype(np.float64)
+        big = np.arange(c, len(rows), 37)                      # every offset mod 64 over the column
+        v[big] = rng.integers(1 << 28, 1 << 32, len(big)).astype(np.float64)
+        v[big[::5]] = float((1 << 32) - 1)                     # the largest u32
+        cols.append((rows, v))
+    st = _mat(gpu_ctx, n, len(cols), cols).fiber_codec(3)
+    _check(st, vals=1 << 3)
+    assert st["entries"] == sum(len(c[0]) for c in cols)

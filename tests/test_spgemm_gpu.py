@@ -517,3 +517,27 @@ def test_gpu_flat_merge_tiles(gpu_ctx, monkeypatch, flat, sr, dt):
         cp, ir, val = M.to_host()
         assert_same_product(Csc(n, m, cp, ir, val), R, dt, scale=np.abs(R.val) * 2 if dt == "f64" else None,
                             what=f"flat={flat} merge {sr}")
+
+
+@pytest.mark.parametrize("dt", ["i64", "f64"])
+def test_gpu_repeated_b_rows_in_wide_columns(gpu_ctx, dt):
+    """B columns that name one long A column hundreds of times (repeated rows, unsorted): the wide-column symbolic
+    pass (k_sym_part, 32-bit segment staging) sees chunks of 512 segments of up to 2^18 entries each -- the most a
+    chunk can stage, since a segment is one A column narrowed to one part -- and the rows-known numeric units sum the
+    repeats.  Bit-exact (i64) / within 1e-12 (f64) against the oracle."""
+    rng = np.random.default_rng(31)
+    n = 1 << 20
+    lens = [200_000, 150_000, 3, 40_000, 1]
+    cols = [np.sort(rng.choice(n, L, replace=False)).astype(np.int32) for L in lens]
+    cp = np.r_[0, np.cumsum(lens)]
+    vals = rng.integers(-3, 4, cp[-1]).astype(np.int64) if dt == "i64" else rng.uniform(-1, 1, cp[-1])
+    A = Csc(n, len(lens), cp, np.concatenate(cols), vals)
+    bcols = [np.r_[np.zeros(700, np.int32), [3, 2, 4]],            # 700 x column 0, then others
+             rng.permutation(np.r_[np.ones(600, np.int32), np.full(300, 3, np.int32), [0]]).astype(np.int32),
+             np.array([4, 4, 2, 2, 2], np.int32)]
+    bcp = np.r_[0, np.cumsum([len(c) for c in bcols])]
+    bv = (rng.integers(-2, 3, bcp[-1]).astype(np.int64) if dt == "i64" else rng.uniform(-1, 1, bcp[-1]))
+    B = Csc(len(lens), len(bcols), bcp, np.concatenate(bcols), bv)
+    _check_vs_oracle(gpu_ctx, A, B, "plus_times", dt)
+    prof = gpu_ctx.last_profile()
+    assert prof["bins"][12] > 0 or prof["bins"][13] > 0   # wide / heavy columns took the part and unit paths
