@@ -453,7 +453,28 @@ def piece_checksum(blk, r0, c0, chunk=1 << 27):
     return total - (1 << 64) if total >= 1 << 63 else total
 
 
-def verify_piece(be, SR, blk, Arow, Acol, r0, c0, nsample, seed, ref_stride=0):
+def oracle_piece_sample(blk, Arow, Acol, ncols, seed):
+    """The CHECKER's leg of the distributed checks (test infrastructure, never timed): a seeded sample of `ncols`
+    columns of a rank's output piece against oracle/oracle.c's product A(rows_i, :) * A(:, J_sample) on the host (the
+    reference-pinned restatement of LocalSpGEMMHash, mtSpGEMM.h:465-661), bit for bit (R-MAT multiplicities)."""
+    import torch
+    sys.path.insert(0, os.path.join(HERE, "tests"))
+    from helpers import Csc, oracle_spgemm  # test infrastructure: checker only
+    k = min(blk.ncol, int(ncols))
+    g = torch.Generator().manual_seed(int(seed) ^ 0x5EED)
+    sel = torch.randperm(blk.ncol, generator=g)[:k].sort().values
+    B = select_block_cols(Acol, sel)
+    S = select_block_cols(blk, sel)
+    A = Csc(Arow.nrow, Arow.ncol, Arow.cp.cpu().numpy(), Arow.ir.cpu().numpy(), Arow.val.cpu().numpy())
+    Bh = Csc(B.nrow, B.ncol, B.cp.cpu().numpy(), B.ir.cpu().numpy(), B.val.cpu().numpy())
+    R, mults, rc = oracle_spgemm(A, Bh, "plus_times", "f64")
+    ok = (rc == 0 and np.array_equal(S.cp.cpu().numpy(), R.cp) and np.array_equal(S.ir.cpu().numpy(), R.ir)
+          and np.array_equal(S.val.cpu().numpy().view(np.int64), np.asarray(R.val, np.float64).view(np.int64)))
+    return {"oracle_sample_columns": k, "oracle_sample_nnz": int(R.cp[-1]), "oracle_sample_multiplies": int(mults),
+            "oracle_sample": bool(ok)}
+
+
+def verify_piece(be, SR, blk, Arow, Acol, r0, c0, nsample, seed, ref_stride=0, oracle_cols=0):
     """Check one rank's output piece: a seeded random sample of its columns bit for bit against a one-GPU product
     A(r0:r1, :) * A(:, J_sample) (R-MAT values are multiplicities, so PlusTimes<double> sums are exact), and the
     reference-sample checksum: entry_checksum over the piece's columns j = 0 mod ref_stride (global row ids, column
@@ -469,6 +490,9 @@ def verify_piece(be, SR, blk, Arow, Acol, r0, c0, nsample, seed, ref_stride=0):
                  and torch.equal(P.val.view(torch.int64), S.val.view(torch.int64)))
     rec = {"sampled_columns": k, "sample_nnz": P.nnz, "bit_exact": exact}
     del P, S
+    if oracle_cols:
+        rec.update(oracle_piece_sample(blk, Arow, Acol, oracle_cols, seed))
+        rec["bit_exact"] = rec["bit_exact"] and rec["oracle_sample"]
     if ref_stride:
         first = (-c0) % ref_stride
         jl = torch.arange(first, ncols, ref_stride, dtype=torch.int64)
@@ -582,7 +606,8 @@ def bench_dist(args, world, rank, local_rank):
     flops_global, nnz_global = int(tot[0].item()), int(tot[1].item())
     ref_stride = max(1, int(np.ceil(flops_global / max(args.cpu_mults, 1)))) if not args.no_cpu else 0
     nsample = max(int(np.ceil(1e4 / world)), C.block.ncol // 64)
-    v = verify_piece(be, SR, C.block, Arow, Acol, r0, c0, nsample, args.seed + 7919 * rank, ref_stride)
+    v = verify_piece(be, SR, C.block, Arow, Acol, r0, c0, nsample, args.seed + 7919 * rank, ref_stride,
+                     oracle_cols=0 if args.no_cpu else 256)
     v.update({"rank": rank, "rows": [r0, r1], "cols": [c0, c1], "piece_nnz": C.block.nnz,
               "piece_nnz_equals_estimate": C.block.nnz == est_z, "steps_same_nnz": len(set(nzs)) == 1})
     del Arow, Acol
@@ -636,7 +661,9 @@ def bench_dist(args, world, rank, local_rank):
                             "sampled_columns": sum(r["verify"]["sampled_columns"] for r in recs),
                             "sampled_nnz": sum(r["verify"]["sample_nnz"] for r in recs),
                             "against": "per rank: a seeded sample of its output columns vs a one-GPU product "
-                                       "A(rows_i, :) * A(:, J_sample) built independently of the grid (cbg_rmat_block)",
+                                       "A(rows_i, :) * A(:, J_sample) built independently of the grid (cbg_rmat_block), "
+                                       "and 256 of them vs oracle/oracle.c's product on the host (oracle_sample)",
+                            "oracle_sample": all(r["verify"].get("oracle_sample", False) for r in recs),
                             "multiplies_equal_estimateFLOP": int(mults / args.steps) == flops_global,
                             "nnz_equal_symbolic": int(nnzc / args.steps) == nnz_global,
                             "estimateFLOP": flops_global, "nnz_symbolic": nnz_global, "ok": ok_all,
@@ -983,7 +1010,8 @@ def bench_rank_share(args):
         h0, h1 = halves[me]
         Arow, Acol, est_m, est_z = piece_reference(be, args, n, r0, r1, b0 + h0, b0 + h1)
         nsample = max(int(np.ceil(1e4 / N)), final.ncol // 64)
-        v = verify_piece(be, SR, final, Arow, Acol, r0, b0 + h0, nsample, args.seed + 7919 * r)
+        v = verify_piece(be, SR, final, Arow, Acol, r0, b0 + h0, nsample, args.seed + 7919 * r,
+                         oracle_cols=0 if args.no_cpu else 256)
         v.update({"piece_nnz": final.nnz, "piece_nnz_equals_estimate": final.nnz == est_z,
                   "piece_multiplies_estimate": est_m})
         rec["verified"] = v

@@ -7,8 +7,8 @@ north-star layout (configs[2], s22 on 2x2x2), on the GPU, through size-independe
   parts, and the flat two-way merge; its multiplies equal estimateFLOP (numpy) and a seeded sample of 2048 columns is
   bit-exact against the oracle (oracle/oracle.c, the reference-pinned restatement of LocalSpGEMMHash).
 * s22 2x2x2, rank (0, 0, 0): its output piece C(rows_0, J) -- the layer-0 panel product's own column half merged with
-  the layer-1 partner's -- against a one-GPU product A(rows_0, :) * A(:, J_sample) of a seeded column sample, and the
-  piece's nnz against the symbolic pass (ParFriends.h:3119-3183's exchange + merge, SURVEY 8(d) "scale-22 correctness").
+  the layer-1 partner's -- against a one-GPU product A(rows_0, :) * A(:, J_sample) of a seeded column sample, 256 of
+  those columns against the oracle's product on the host, and the piece's nnz against the symbolic pass (ParFriends.h:3119-3183's exchange + merge, SURVEY 8(d) "scale-22 correctness").
 """
 import os
 import sys
@@ -129,5 +129,5 @@ def test_gpu_rmat_s22_rank_piece_2x2x2(gpu_ctx, backend):
     h0, h1 = halves[0]
     Arow, Acol, est_m, est_z = bench.piece_reference(be, Args, n, r0, r1, b0 + h0, b0 + h1)
     assert piece.nnz == est_z
-    v = bench.verify_piece(be, SR, piece, Arow, Acol, r0, b0 + h0, 4096, seed + 7919)
-    assert v["bit_exact"], v
+    v = bench.verify_piece(be, SR, piece, Arow, Acol, r0, b0 + h0, 4096, seed + 7919, oracle_cols=256)
+    assert v["bit_exact"] and v["oracle_sample"] and v["oracle_sample_nnz"] > 0, v

@@ -54,6 +54,11 @@ for step in "$@"; do
         > "$OUT/rank_share_s${b}_n${a}.jsonl" 2> "$OUT/rank_share_s${b}_n${a}.err"
       rc=$?; cut -c1-400 "$OUT/rank_share_s${b}_n${a}.jsonl"
       [ $rc -eq 0 ] || { tail -8 "$OUT/rank_share_s${b}_n${a}.err"; fail "$step" $rc; } ;;
+    cfgshare)   # cfgshare:<configs>:<gpus list with '.' for ','>  (MCL_N env: graph size) configs 4/5 rank shares
+      timeout -k 10 1000 python3 -u tools/rank_share_configs.py --configs "$a" --gpus "${b//./,}" \
+        --mcl-n "${MCL_N:-1048576}" > "$OUT/cfgshare_${a//,/}_${b//./}.jsonl" 2> "$OUT/cfgshare_${a//,/}_${b//./}.err"
+      rc=$?; grep '^{' "$OUT/cfgshare_${a//,/}_${b//./}.jsonl" | cut -c1-300
+      [ $rc -eq 0 ] || { tail -8 "$OUT/cfgshare_${a//,/}_${b//./}.err"; fail "$step" $rc; } ;;
     codec)
       timeout -k 10 300 python -u tools/bench_codec.py --scale "${a:-21}" > "$OUT/codec_s${a:-21}.json" 2>&1 || \
         { tail -5 "$OUT/codec_s${a:-21}.json"; fail "$step" 1; }

@@ -81,9 +81,60 @@ def main():
         S = bench.select_block_cols(M, sel)
         same = P.nnz == S.nnz and torch.equal(P.cp, S.cp) and torch.equal(P.ir, S.ir)
         err = float(((P.val - S.val).abs() / torch.clamp(Pabs.val, min=1e-300)).max().item()) if same and P.nnz else 0.0
-        return {"sampled_columns": k, "sample_nnz": P.nnz, "structure_equal": bool(same),
-                "max_rel_err_vs_abs_bound": err, "within_1e-12": bool(same and err <= 1e-12),
-                "piece_nnz": M.nnz, "piece_nnz_equals_estimate": M.nnz == est_z, "piece_multiplies_estimate": est_m}
+        rec = {"sampled_columns": k, "sample_nnz": P.nnz, "structure_equal": bool(same),
+               "max_rel_err_vs_abs_bound": err, "within_1e-12": bool(same and err <= 1e-12),
+               "piece_nnz": M.nnz, "piece_nnz_equals_estimate": M.nnz == est_z, "piece_multiplies_estimate": est_m}
+        rec.update(oracle_check(M, Arow, Bcol, 256, seed))
+        rec["within_1e-12"] = rec["within_1e-12"] and rec["oracle_sample"]
+        return rec
+
+    def oracle_check(M, Arow, Bcol, ncols, seed):
+        """CHECKER (test infrastructure): 256 seeded columns of the piece against oracle/oracle.c's product on the host
+        (the reference-pinned restatement of LocalSpGEMMHash), structure exact, values within 1e-12 of |A|*|B|."""
+        sys.path.insert(0, os.path.join(os.path.dirname(HERE), "tests"))
+        from helpers import Csc, oracle_spgemm
+        k = min(M.ncol, int(ncols))
+        g = torch.Generator().manual_seed(int(seed) ^ 0x5EED)
+        sel = torch.randperm(M.ncol, generator=g)[:k].sort().values
+        Bs = bench.select_block_cols(Bcol, sel)
+        S = bench.select_block_cols(M, sel)
+        h = lambda b, f=lambda v: v: Csc(b.nrow, b.ncol, b.cp.cpu().numpy(), b.ir.cpu().numpy(), f(b.val.cpu().numpy()))
+        R, _, rc = oracle_spgemm(h(Arow), h(Bs), "plus_times", "f64")
+        Ra, _, rca = oracle_spgemm(h(Arow, np.abs), h(Bs, np.abs), "plus_times", "f64")
+        same = (rc == 0 and rca == 0 and np.array_equal(S.cp.cpu().numpy(), R.cp)
+                and np.array_equal(S.ir.cpu().numpy(), R.ir))
+        err = float(np.max(np.abs(S.val.cpu().numpy() - R.val) / np.maximum(Ra.val, 1e-300))) if same and len(R.val) else 0.0
+        return {"oracle_sample_columns": k, "oracle_sample_nnz": int(R.cp[-1]), "oracle_max_rel_err": err,
+                "oracle_sample": bool(same and err <= 1e-12)}
+
+    def prune_share(M, Am, Bm, q, i, b0, h0, h1):
+        """configs[3]: the rank's part of the distributed MCLPruneRecoverySelect (ParFriends.h:185-353, MCL.cpp:573-587).
+        With q = 1 the piece holds complete columns and is pruned as is; with q > 1 the rank prunes column group i of
+        its piece's columns, completed along the processor column (dist._gather_columns: rows of all q row blocks),
+        built here as one product A * B(:, group).  Records the prune time and the gathered entries."""
+        d = cb.MCL_DEFAULTS
+        if q == 1:
+            full = M
+            gathered = 0
+        else:
+            g0, g1 = cbd.block_range(h1 - h0, q, i)
+            full = be.multiply(host_block(Am, 0, Am[0], 0, Am[1]), host_block(Bm, 0, Bm[0], b0 + h0 + g0, b0 + h0 + g1), SR)
+            gathered = int(full.nnz)
+        ts = []
+        for rep in range(2):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            P, stp = be.mcl_prune(full, d["hardThreshold"], d["selectNum"], d["recoverNum"], d["recoverPct"])
+            torch.cuda.synchronize()
+            ts.append(1e3 * (time.perf_counter() - t0))
+            kept = int(P.nnz)
+            del P
+        rec = {"prune_ms": round(ts[-1], 3), "prune_columns": int(full.ncol), "prune_in_nnz": int(full.nnz),
+               "prune_kept_nnz": kept, "gathered_entries": gathered,
+               "gather_bytes_offrank": int(gathered * 12 * (q - 1) / q) if q > 1 else 0, **stp}
+        del full
+        torch.cuda.empty_cache()
+        return rec
 
     def run(label, Am, Bm, N, extra):
         L, q, _ = cbd.grid_for(N)
@@ -141,6 +192,8 @@ def main():
             h0, h1 = halves[me]
             v = check(final, Am, Bm, r0, r1, b0 + h0, b0 + h1, max(int(np.ceil(1e4 / N)), final.ncol // 64),
                       7919 * r + 11)
+            if label.startswith("4"):
+                rec["prune"] = prune_share(final, Am, Bm, q, i, b0, h0, h1)
             del final
             torch.cuda.empty_cache()
             rec.update({"multiplies": st.get("multiplies", 0), "local_ms": round(local_ms, 3),
@@ -157,6 +210,51 @@ def main():
                               and (codec is None or codec["roundtrip_exact"]))
         return bad
 
+    def anchor4(Am, extra):
+        """configs[3] at N = 1 on the same graph: the expansion product and MCLPruneRecoverySelect on one GPU (the
+        denominator of the 2/4/8-GPU predictions), the prune's kept entries against the oracle's prune on a sample."""
+        A = host_block(Am, 0, Am[0], 0, Am[1])
+        d = cb.MCL_DEFAULTS
+        rec = {"config": "4: HipMCL expansion A*A", "rank": 0, "layout": "1 GPU", **extra}
+        for rep in range(2):
+            st = {}
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            C = be.multiply(A, A, SR, st)
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            P, stp = be.mcl_prune(C, d["hardThreshold"], d["selectNum"], d["recoverNum"], d["recoverPct"])
+            torch.cuda.synchronize()
+            t2 = time.perf_counter()
+            prof = ctx.last_profile()
+            nnz_c, nnz_p = C.nnz, P.nnz
+            if rep == 0:
+                del P
+            del C
+            torch.cuda.empty_cache()
+        mults = st.get("multiplies", 0)
+        rec.update({"multiplies": mults, "local_ms": round(1e3 * (t1 - t0), 3), "prune_ms": round(1e3 * (t2 - t1), 3),
+                    "expansion_ms": round(1e3 * (t2 - t0), 3), "nnz_C": nnz_c, "nnz_pruned": nnz_p, **stp,
+                    "multiplies_per_s_expansion": mults / (t2 - t0), "merge_ms": 0.0, "fiber": None,
+                    "nnz_A_panel": A.nnz, "nnz_B_panel": A.nnz})
+        # the pruned columns of a seeded sample against the oracle's MCLPruneRecoverySelect of the same columns
+        sys.path.insert(0, os.path.join(os.path.dirname(HERE), "tests"))
+        from helpers import Csc, oracle_spgemm, oracle_mcl_prune
+        g = torch.Generator().manual_seed(4242)
+        sel = torch.randperm(A.ncol, generator=g)[:256].sort().values
+        Bs = bench.select_block_cols(A, sel)
+        h = lambda b: Csc(b.nrow, b.ncol, b.cp.cpu().numpy(), b.ir.cpu().numpy(), b.val.cpu().numpy())
+        R, _, rc = oracle_spgemm(h(A), h(Bs), "plus_times", "f64")
+        O = oracle_mcl_prune(R, d["hardThreshold"], d["selectNum"], d["recoverNum"], d["recoverPct"])
+        S = bench.select_block_cols(P, sel)
+        ok = rc == 0 and np.array_equal(S.cp.cpu().numpy(), O[0].cp) and np.array_equal(S.ir.cpu().numpy(), O[0].ir)
+        rec["verified"] = {"oracle_prune_sample_columns": 256, "oracle_prune_structure_equal": bool(ok),
+                           "oracle_prune_sample_nnz": int(O[0].cp[-1])}
+        del P
+        torch.cuda.empty_cache()
+        print(json.dumps(rec), flush=True)
+        return not ok
+
     bad = False
     gpus = [int(x) for x in args.gpus.split(",")]
     for c in [int(x) for x in args.configs.split(",")]:
@@ -166,7 +264,10 @@ def main():
             A = (n, n, cp, ir, val)
             extra = {"graph_n": n, "nnz": int(cp[-1]), "gen_s": round(time.perf_counter() - t0, 1)}
             for N in gpus:
-                bad |= run("4: HipMCL expansion A*A", A, A, N, extra)
+                if N == 1:
+                    bad |= anchor4(A, extra)
+                else:
+                    bad |= run("4: HipMCL expansion A*A", A, A, N, extra)
         elif c == 5:
             n, acp, air, aval = poisson3d(args.poisson_k)
             dA = cb.SpDCCols.from_csc(ctx, n, n, acp, air, aval)
