@@ -133,6 +133,10 @@ __global__ void k_split_hdr(int64_t n, int64_t* hdr, int64_t* __restrict__ aux) 
     hdr[i] = v & 0xffffffffLL;
   }
 }
+// x[i] += base, i in [0, n)
+__global__ void k_add_base(int64_t n, int64_t* __restrict__ x, int64_t base) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) x[i] += base;
+}
 // column headers of a message: count | aux << 32 (aux = escapes of the u16 gaps, or the column's varint row bytes)
 __global__ void k_pack_hdr(int64_t n, const int64_t* __restrict__ cp, const int64_t* __restrict__ aux,
                            int64_t* __restrict__ hdr) {   // aux == nullptr: no aux
@@ -157,10 +161,15 @@ __device__ __forceinline__ bool as_u32(double x, uint32_t* u) {   // an integer 
 // entries or 256 bytes): one wave scan per step instead of one per 64 entries, four loads in flight per lane.
 constexpr int kCodeEpl = 4;
 constexpr int kCodeStep = kCodeEpl * kWave;
+// The codec kernels run in one-wave workgroups (4 KB of LDS at most): the fiber pipeline decodes a received chunk while
+// the own columns multiply, and a one-wave workgroup fits beside the persistent heavy grid (152.7 KB of LDS and 16
+// waves per CU) and in the CUs it leaves to the transfer.
+constexpr int kCodecNT = kWave;
+inline int codec_grid(int64_t ncol) { return (int)grid_for(ncol, 1, kMaxGrid * 8); }
 
 // one wave per column: escapes of the u16 gaps, varint bytes of the row gaps, varint bytes of the values; over
 // the message: bad[0] values that do not survive f32, bad[1] not u16, bad[2] not u32 integers
-__global__ void __launch_bounds__(256) k_code_count(int64_t ncol, const int64_t* __restrict__ cp,
+__global__ void __launch_bounds__(kCodecNT) k_code_count(int64_t ncol, const int64_t* __restrict__ cp,
                                                     const int32_t* __restrict__ ir, const double* __restrict__ val,
                                                     int64_t* __restrict__ esc, int64_t* __restrict__ rbytes,
                                                     int64_t* __restrict__ vbytes, unsigned long long* __restrict__ bad) {
@@ -234,10 +243,10 @@ __global__ void __launch_bounds__(256) k_code_count(int64_t ncol, const int64_t*
 // MODE 0: row gaps of ir, MODE 1: values (u32 integers) of val -> varint bytes at off[c] of column c.  A step's codes
 // are assembled in the wave's LDS slice (one wave scan places them), then copied out with coalesced byte stores.
 template <int MODE>
-__global__ void __launch_bounds__(256) k_var_encode(int64_t ncol, const int64_t* __restrict__ cp,
-                                                    const int32_t* __restrict__ ir, const double* __restrict__ val,
-                                                    const int64_t* __restrict__ off, uint8_t* __restrict__ out) {
-  __shared__ uint8_t stage[256 / kWave][kCodeStep * 5];
+__global__ void __launch_bounds__(kCodecNT) k_var_encode(int64_t ncol, const int64_t* __restrict__ cp,
+                                                         const int32_t* __restrict__ ir, const double* __restrict__ val,
+                                                         const int64_t* __restrict__ off, uint8_t* __restrict__ out) {
+  __shared__ uint8_t stage[kCodecNT / kWave][kCodeStep * 5];
   const int l = lane_id();
   uint8_t* sb = stage[threadIdx.x / kWave];
   for (int64_t c = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / kWave; c < ncol;
@@ -311,11 +320,11 @@ __global__ void __launch_bounds__(256) k_var_encode(int64_t ncol, const int64_t*
 constexpr int kDecEpl = 8;
 constexpr int kDecStep = kDecEpl * kWave;
 template <int MODE>
-__global__ void __launch_bounds__(256) k_var_decode(int64_t ncol, const int64_t* __restrict__ cp,
-                                                    const int64_t* __restrict__ off, const uint8_t* __restrict__ in,
-                                                    int32_t* __restrict__ ir, double* __restrict__ val) {
+__global__ void __launch_bounds__(kCodecNT) k_var_decode(int64_t ncol, const int64_t* __restrict__ cp,
+                                                         const int64_t* __restrict__ off, const uint8_t* __restrict__ in,
+                                                         int32_t* __restrict__ ir, double* __restrict__ val) {
   // a step's decoded entries (<= 512) go through the wave's LDS slice and out with coalesced stores
-  __shared__ uint64_t stage[256 / kWave][kDecStep];
+  __shared__ uint64_t stage[kCodecNT / kWave][kDecStep];
   const int l = lane_id();
   uint64_t* sb = stage[threadIdx.x / kWave];
   const int64_t stride = ((int64_t)gridDim.x * blockDim.x) / kWave;
@@ -508,7 +517,9 @@ struct cbg_grid {
   ncclComm_t fiber_ctl = nullptr;
   cbg_transport cb{};
   hipStream_t cs = nullptr;          // communication stream
+  hipStream_t ds = nullptr;          // fiber pipeline: decodes received chunks while the own columns multiply
   hipEvent_t ev_comm[2] = {}, ev_used[2] = {}, ev_t[4] = {};
+  hipEvent_t ev_rx[8] = {};          // fiber pipeline: chunk c has arrived (recorded on cs after its transfer)
   std::vector<hipEvent_t> ev_stage;  // timing events of the schedules, created once and reused by every call
   hipError_t stage_event(size_t i, hipEvent_t* e) {
     while (ev_stage.size() <= i) {
@@ -1339,7 +1350,7 @@ cbg_status fiber_encode(hipStream_t cst, const Scanner& scan, unsigned long long
     for (PoolBuf* pb : {&m.saux, &m.svr, &m.sescoff, &m.svroff}) HIPCHK(pb->reserve(8 * (oc + 1)));
     if (vcheck) { HIPCHK(m.svv.reserve(8 * (oc + 1))); HIPCHK(m.svvoff.reserve(8 * (oc + 1))); }
     HIPCHK(hipMemsetAsync(dbad, 0, 24, cst));
-    k_code_count<<<(int)grid_for(oc, 4, kMaxGrid * 2), 256, 0, cst>>>(
+    k_code_count<<<codec_grid(oc), kCodecNT, 0, cst>>>(
         oc, Po.cp, Po.ir, vcheck ? (const double*)Po.val : nullptr, m.saux.as<int64_t>(), m.svr.as<int64_t>(),
         vcheck ? m.svv.as<int64_t>() : nullptr, dbad);
     HIPCHK(hipGetLastError());
@@ -1368,7 +1379,7 @@ cbg_status fiber_encode(hipStream_t cst, const Scanner& scan, unsigned long long
     m.srow_p = m.srow.p;
   } else if (m.rfmt == 2) {
     HIPCHK(m.srow.reserve(m.srow_b + 16));
-    k_var_encode<0><<<(int)grid_for(oc, 4, kMaxGrid * 2), 256, 0, cst>>>(oc, Po.cp, Po.ir, nullptr,
+    k_var_encode<0><<<codec_grid(oc), kCodecNT, 0, cst>>>(oc, Po.cp, Po.ir, nullptr,
                                                                          m.svroff.as<int64_t>(), m.srow.as<uint8_t>());
     m.srow_p = m.srow.p;
   }
@@ -1387,7 +1398,7 @@ cbg_status fiber_encode(hipStream_t cst, const Scanner& scan, unsigned long long
       k_f64_to_u16<<<(int)grid_for(n, 256, kMaxGrid), 256, 0, cst>>>(n, (const double*)Po.val,
                                                                     m.sval.as<unsigned short>());
     else
-      k_var_encode<1><<<(int)grid_for(oc, 4, kMaxGrid * 2), 256, 0, cst>>>(oc, Po.cp, nullptr, (const double*)Po.val,
+      k_var_encode<1><<<codec_grid(oc), kCodecNT, 0, cst>>>(oc, Po.cp, nullptr, (const double*)Po.val,
                                                                            m.svvoff.as<int64_t>(), m.sval.as<uint8_t>());
     m.sval_p = m.sval.p;
   }
@@ -1422,7 +1433,7 @@ cbg_status fiber_decode(hipStream_t cst, const Scanner& scan, int64_t* dtot_a, i
                                                                            (const unsigned short*)in.rows, in.esc, rir,
                                                                            eoff);
     else
-      k_var_decode<0><<<(int)grid_for(m.mc, 4, kMaxGrid * 2), 256, 0, cst>>>(m.mc, ccp, m.rauxoff.as<int64_t>(),
+      k_var_decode<0><<<codec_grid(m.mc), kCodecNT, 0, cst>>>(m.mc, ccp, m.rauxoff.as<int64_t>(),
                                                                               (const uint8_t*)in.rows, rir, nullptr);
     if (has_val) {
       double* dv = (double*)rv;
@@ -1436,7 +1447,7 @@ cbg_status fiber_decode(hipStream_t cst, const Scanner& scan, int64_t* dtot_a, i
       else {
         HIPCHK(m.rvoff.reserve(8 * (m.mc + 1)));
         CBGCHK(scan(m.mc, in.vhdr, m.rvoff.as<int64_t>(), dtot_v));
-        k_var_decode<1><<<(int)grid_for(m.mc, 4, kMaxGrid * 2), 256, 0, cst>>>(m.mc, ccp, m.rvoff.as<int64_t>(),
+        k_var_decode<1><<<codec_grid(m.mc), kCodecNT, 0, cst>>>(m.mc, ccp, m.rvoff.as<int64_t>(),
                                                                                 (const uint8_t*)in.vals, nullptr, dv);
       }
     }
@@ -1486,7 +1497,11 @@ cbg_status fiber_pipeline(cbg_grid* G, const cbg_dcsc_view& va, const cbg_dcsc_v
   HIPCHK(tiles.reserve(8 * ((std::max(myc, ocw) + kScanTile - 1) / kScanTile + 1)));
   std::vector<std::unique_ptr<FiberMsg>> msgs;
   std::shared_ptr<Owner> rx(new Owner(ctx->pool));   // received headers (val), rows + values (ir)
+  std::shared_ptr<Owner> co(new Owner(ctx->pool));   // the received piece's colptr
+  PoolBuf dtiles, dscal;                               // the overlapped decodes' scan tiles and totals
+  dtiles.pool = dscal.pool = ctx->pool;
   StreamFence fence(cst, G->cs);   // transfers into / out of the buffers above end before they return to the pool
+  StreamFence dfence(G->ds);       // and so do the overlapped decodes (destroyed first: declared last)
   // columns [c0, c1) of B as a view: rebased colptr, rows and values from cp[c0]
   auto col_view = [&](int64_t c0, int64_t c1, PoolBuf& cpbuf, cbg_dcsc_view* v) -> cbg_status {
     int64_t e[2] = {0, 0};
@@ -1595,6 +1610,7 @@ cbg_status fiber_pipeline(cbg_grid* G, const cbg_dcsc_view& va, const cbg_dcsc_v
       if (has_val && m.svh_b) NCCLCHK(ncclSend(svh_p, (size_t)m.svh_b, ncclInt8, other, f, G->cs));
       if (m.rvh_b) NCCLCHK(ncclRecv(m.rvhdr.p, (size_t)m.rvh_b, ncclInt8, other, f, G->cs));
       NCCLCHK(ncclGroupEnd());
+      HIPCHK(hipEventRecord(G->ev_rx[c], G->cs));   // chunk c has arrived: the decode stream may start on it
       in_flight = true;
     } else {   // caller transport: synchronous segments (member `other` only)
       int64_t sb[2] = {0, 0}, rb[2] = {0, 0};
@@ -1613,7 +1629,67 @@ cbg_status fiber_pipeline(cbg_grid* G, const cbg_dcsc_view& va, const cbg_dcsc_v
     }
   }
   if (async) HIPCHK(hipEventRecord(G->ev_t[2], G->cs));
-  // 2. the own columns, while the chunks travel on the communication stream
+  // 2. the received piece's storage, taken before the own product: with RCCL every chunk is decoded on the decode
+  //    stream as soon as it has arrived, while the own columns multiply on the compute stream (one-wave codec
+  //    workgroups fit beside the product's persistent grids and in the CUs left to the transfer).  When the storage
+  //    does not fit now (or CBG_FIBER_DECODE_OVERLAP=0), the chunks are decoded after the own product, as before.
+  static const bool overlap_env = [] {
+    const char* x = std::getenv("CBG_FIBER_DECODE_OVERLAP");
+    return !(x && x[0] == '0');
+  }();
+  const bool has_val = msgs.empty() || msgs[0]->P.val != nullptr;
+  int64_t rnnz = 0;
+  for (auto& mp : msgs) rnnz += mp->rnnz;
+  const int64_t ir_bytes = (4 * rnnz + 15) & ~15LL;
+  HIPCHK(co->cp.reserve(8 * (myc + 1)));
+  HIPCHK(raux.reserve(8 * (myc + 1)));
+  bool early = async && overlap_env && (int)msgs.size() <= 8;
+  if (early) {   // only with room to spare for the own product (its output and workspace come after this)
+    size_t fr = 0, tot = 0;
+    HIPCHK(hipMemGetInfo(&fr, &tot));
+    const double need = (double)(ir_bytes + vs * rnnz + 16);
+    early = (double)fr - need >= 0.3 * (double)tot && rx->ir.reserve((size_t)need) == hipSuccess;
+    if (!early) (void)hipGetLastError();
+  }
+  auto decode_all = [&](hipStream_t dst, const Scanner& dsc, int64_t* dt3) -> cbg_status {
+    char* rbase = rx->ir.as<char>();
+    int32_t* rir = (int32_t*)rbase;
+    char* rv = rbase + ir_bytes;
+    int64_t eoff = 0;
+    for (size_t c = 0; c < msgs.size(); ++c) {
+      FiberMsg& m = *msgs[c];
+      if (dst != cst) HIPCHK(hipStreamWaitEvent(dst, G->ev_rx[c], 0));   // chunk c's streams and headers landed
+      int64_t* ccp = co->cp.as<int64_t>() + m.c0;   // -> absolute entry offsets of the chunk's columns
+      if (m.mc > 0) {
+        k_split_hdr<<<(int)grid_for(m.mc, 256, kMaxGrid), 256, 0, dst>>>(m.mc, rcnt + m.c0, raux.as<int64_t>() + m.c0);
+        CBGCHK(dsc(m.mc, rcnt + m.c0, ccp, dt3 + 0));
+        k_add_base<<<(int)grid_for(m.mc + 1, 256, kMaxGrid), 256, 0, dst>>>(m.mc + 1, ccp, eoff);
+      } else {
+        HIPCHK(hipMemcpyAsync(ccp, &eoff, 8, hipMemcpyHostToDevice, dst));
+        HIPCHK(hipStreamSynchronize(dst));   // (eoff lives on the host stack)
+      }
+      const RecvStreams in{m.rrow.p, m.resc.as<int32_t>(), m.rvbuf.p, m.rvhdr.as<int64_t>()};
+      CBGCHK(fiber_decode(dst, dsc, dt3 + 1, dt3 + 2, vs, has_val, m, in, ccp, raux.as<int64_t>() + m.c0, eoff, rir,
+                          rv));
+      eoff += m.rnnz;
+    }
+    HIPCHK(hipGetLastError());
+    return CBG_OK;
+  };
+  if (early) {
+    // every buffer the overlapped decodes touch is reserved here, before any of them runs (a growing pool buffer
+    // hands its old block back to the pool while queued kernels may still use it)
+    HIPCHK(dtiles.reserve(8 * ((myc + kScanTile - 1) / kScanTile + 1)));
+    HIPCHK(dscal.reserve(64));
+    for (auto& mp : msgs) {
+      HIPCHK(mp->rauxoff.reserve(8 * (mp->mc + 1)));
+      HIPCHK(mp->rvoff.reserve(8 * (mp->mc + 1)));
+    }
+    const Scanner dscan{G->ds, &dtiles};
+    CBGCHK(decode_all(G->ds, dscan, dscal.as<int64_t>()));
+    HIPCHK(hipEventRecord(G->ev_t[3], G->ds));
+  }
+  // 3. the own columns, while the chunks travel on the communication stream (and are decoded on arrival)
   cbg_dcsc_view vm;
   CBGCHK(col_view(cb[me], cb[me + 1], cpm, &vm));
   cbg_csc_result Rm;
@@ -1621,7 +1697,7 @@ cbg_status fiber_pipeline(cbg_grid* G, const cbg_dcsc_view& va, const cbg_dcsc_v
   CBGCHK(local(vm, &Rm, &mm));
   mults += mm;
   Piece Pm = piece_of_result(Rm);
-  // 3. join; decode every chunk into the received piece (colptr from all chunks' counts); the merge in layer order
+  // 4. join; the received piece (decoded above, or now: colptr from all chunks' counts); the merge in layer order
   double t0 = now_ms();
   float xfer_ms = 0.f;
   if (async) {
@@ -1629,32 +1705,19 @@ cbg_status fiber_pipeline(cbg_grid* G, const cbg_dcsc_view& va, const cbg_dcsc_v
     HIPCHK(hipEventSynchronize(G->ev_t[2]));
     (void)hipEventElapsedTime(&xfer_ms, G->ev_t[1], G->ev_t[2]);
   }
-  const bool has_val = msgs.empty() || msgs[0]->P.val != nullptr;
-  int64_t rnnz = 0;
-  for (auto& mp : msgs) rnnz += mp->rnnz;
-  const int64_t ir_bytes = (4 * rnnz + 15) & ~15LL;
-  if (rx->ir.reserve(ir_bytes + vs * rnnz + 16) != hipSuccess) {   // next to the two products' pieces: give the
-    (void)hipGetLastError();                                        // idle product workspace back and retry once
-    release_workspace(ctx);
-    HIPCHK(rx->ir.reserve(ir_bytes + vs * rnnz + 16));
+  if (early) {
+    HIPCHK(hipStreamWaitEvent(cst, G->ev_t[3], 0));
+  } else {
+    if (rx->ir.reserve(ir_bytes + vs * rnnz + 16) != hipSuccess) {   // next to the two products' pieces: give the
+      (void)hipGetLastError();                                        // idle product workspace back and retry once
+      release_workspace(ctx);
+      HIPCHK(rx->ir.reserve(ir_bytes + vs * rnnz + 16));
+    }
+    CBGCHK(decode_all(cst, scan, dtot + 3));
   }
   char* rbase = rx->ir.as<char>();
   int32_t* rir = (int32_t*)rbase;
   char* rv = rbase + ir_bytes;
-  HIPCHK(raux.reserve(8 * (myc + 1)));
-  if (myc > 0) k_split_hdr<<<(int)grid_for(myc, 256, kMaxGrid), 256, 0, cst>>>(myc, rcnt, raux.as<int64_t>());
-  std::shared_ptr<Owner> co(new Owner(ctx->pool));
-  HIPCHK(co->cp.reserve(8 * (myc + 1)));
-  CBGCHK(scan(myc, rcnt, co->cp.as<int64_t>(), dtot + 4));
-  int64_t eoff = 0;
-  for (auto& mp : msgs) {
-    FiberMsg& m = *mp;
-    const int64_t* ccp = co->cp.as<int64_t>() + m.c0;   // absolute entry offsets of the chunk's columns
-    const RecvStreams in{m.rrow.p, m.resc.as<int32_t>(), m.rvbuf.p, m.rvhdr.as<int64_t>()};
-    CBGCHK(fiber_decode(cst, scan, dtot + 3, dtot + 5, vs, has_val, m, in, ccp, raux.as<int64_t>() + m.c0, eoff, rir,
-                        rv));
-    eoff += m.rnnz;
-  }
   Piece Pr;
   Pr.nrow = Pm.nrow; Pr.ncol = myc; Pr.nnz = rnnz;
   Pr.cp = co->cp.as<int64_t>();
@@ -1796,6 +1859,8 @@ cbg_status grid_common(cbg_ctx* ctx, int32_t world, int32_t rank, int32_t layers
     HIPCHK(hipEventCreateWithFlags(&G->ev_used[i], hipEventDisableTiming));
   }
   for (int i = 0; i < 4; ++i) HIPCHK(hipEventCreate(&G->ev_t[i]));   // fiber pipeline: fences + transfer timing
+  HIPCHK(hipStreamCreateWithFlags(&G->ds, hipStreamNonBlocking));
+  for (hipEvent_t& e : G->ev_rx) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   *out = G;
   return CBG_OK;
 }
@@ -1862,6 +1927,9 @@ cbg_status cbg_grid_destroy(cbg_grid* G) {
     if (G->ev_t[i]) (void)hipEventDestroy(G->ev_t[i]);
   for (hipEvent_t e : G->ev_stage) (void)hipEventDestroy(e);
   if (G->cs) (void)hipStreamDestroy(G->cs);
+  for (hipEvent_t e : G->ev_rx)
+    if (e) (void)hipEventDestroy(e);
+  if (G->ds) (void)hipStreamDestroy(G->ds);
   delete G;
   return CBG_OK;
 }

@@ -59,6 +59,10 @@ for step in "$@"; do
         --mcl-n "${MCL_N:-1048576}" > "$OUT/cfgshare_${a//,/}_${b//./}.jsonl" 2> "$OUT/cfgshare_${a//,/}_${b//./}.err"
       rc=$?; grep '^{' "$OUT/cfgshare_${a//,/}_${b//./}.jsonl" | cut -c1-300
       [ $rc -eq 0 ] || { tail -8 "$OUT/cfgshare_${a//,/}_${b//./}.err"; fail "$step" $rc; } ;;
+    overlap)   # overlap:<N>:<scale>  own-half product || fiber codec on one GPU (tools/overlap_probe.py), ranks 0
+      timeout -k 10 600 python3 -u tools/overlap_probe.py --gpus-virtual "$a" --scale "$b" > "$OUT/overlap_n${a}_s${b}.json" \
+        2> "$OUT/overlap_n${a}_s${b}.err" || { tail -8 "$OUT/overlap_n${a}_s${b}.err"; fail "$step" 1; }
+      cut -c1-900 "$OUT/overlap_n${a}_s${b}.json" ;;
     codec)
       timeout -k 10 300 python -u tools/bench_codec.py --scale "${a:-21}" > "$OUT/codec_s${a:-21}.json" 2>&1 || \
         { tail -5 "$OUT/codec_s${a:-21}.json"; fail "$step" 1; }

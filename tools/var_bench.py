@@ -27,7 +27,15 @@ if __name__ == "__main__":
         if r.returncode == 0:
             import json
             j = json.loads(line)
-            print(n, "ms/step %.2f" % j["ms_per_step"], "nnz_C", j["config"].get("nnz_C"), j.get("phases_ms"), flush=True)
+            if "ms_per_step" in j:
+                print(n, "ms/step %.2f" % j["ms_per_step"], "nnz_C", j["config"].get("nnz_C"), j.get("phases_ms"),
+                      flush=True)
+            else:   # bench.py --rank-share: one line per rank
+                for x in r.stdout.strip().splitlines():
+                    if x.startswith("{"):
+                        d = json.loads(x)
+                        print(n, "rank", d.get("rank"), {k: d.get(k) for k in ("local_ms", "symbolic_ms", "heavy_ms",
+                                                                              "merge_ms", "heavy_GBps")}, flush=True)
         else:
             print(n, "rc", r.returncode, r.stderr[-2000:], flush=True)
         if r.returncode != 0:
