@@ -16,7 +16,7 @@ import argparse
 import json
 
 
-def rank_step(rec, link_gbps, chunks, decode_gbps=5000.0, entry_bytes=12):
+def rank_step(rec, link_gbps, chunks, decode_gbps=5000.0, entry_bytes=12, decode_hidden=0.0):
     """Milliseconds of one rank's step (see the module docstring); returns (total, parts)."""
     bw = link_gbps * 1e9 / 1e3   # bytes per ms
     L = int(rec["layout"].split("x")[0])
@@ -43,13 +43,16 @@ def rank_step(rec, link_gbps, chunks, decode_gbps=5000.0, entry_bytes=12):
     decode = float(codec["decode_ms"]) if "decode_ms" in codec else \
         (wire + rec.get("recv_nnz", 0) * entry_bytes) / (decode_gbps * 1e9 / 1e3)
     merge = rec["merge_ms"]
+    # the pipeline decodes each chunk on a decode stream while the own half multiplies: the share of the decode the
+    # overlap probe (tools/overlap_probe.py: product || codec on one GPU) measured as hidden leaves the step
+    decode *= max(0.0, 1.0 - decode_hidden)
     total = bcast + compute_end + fiber_exposed + decode + merge
     return total, {"bcast": bcast, "compute": compute_end, "encode": enc, "fiber_exposed": fiber_exposed,
                    "decode": decode, "merge": merge}
 
 
-def predict(records, link_gbps=64.0, chunks=2):
-    steps = [rank_step(r, link_gbps, chunks) for r in records]
+def predict(records, link_gbps=64.0, chunks=2, decode_hidden=0.0):
+    steps = [rank_step(r, link_gbps, chunks, decode_hidden=decode_hidden) for r in records]
     worst = max(range(len(steps)), key=lambda i: steps[i][0])
     mult = sum(r["multiplies"] for r in records)
     ms = steps[worst][0]
@@ -64,14 +67,30 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("jsonl")
     ap.add_argument("--link-GBps", type=float, default=64.0)
+    ap.add_argument("--link-from", default=None,
+                    help="tools/p2p_probe.py output: its measured link_GBps replaces --link-GBps")
     ap.add_argument("--chunks", type=int, default=2)
+    ap.add_argument("--decode-hidden", type=float, default=0.0,
+                    help="share of the decode hidden behind the own-half product (tools/overlap_probe.py)")
+    ap.add_argument("--overlap-from", default=None,
+                    help="tools/overlap_probe.py output: the hidden share of the whole codec (hidden_frac_of_codec, "
+                         "encode + decode overlapped together) as --decode-hidden -- conservative for the decode alone")
     a = ap.parse_args()
+    if a.link_from:
+        rec = json.load(open(a.link_from))
+        if rec.get("link_GBps"):
+            a.link_GBps = float(rec["link_GBps"])
+    if a.overlap_from:
+        o = json.loads([x for x in open(a.overlap_from) if x.startswith("{")][-1])
+        a.decode_hidden = min(1.0, max(0.0, float(o["hidden_frac_of_codec"])))
     recs = [json.loads(l) for l in open(a.jsonl) if l.startswith("{")]
     groups = {}
     for r in recs:
         groups.setdefault((r.get("config", ""), r["layout"]), []).append(r)
     for g in groups.values():
-        print(json.dumps(predict(g, a.link_GBps, a.chunks)))
+        p = predict(g, a.link_GBps, a.chunks, a.decode_hidden)
+        p["decode_hidden"] = round(a.decode_hidden, 3)
+        print(json.dumps(p))
 
 
 if __name__ == "__main__":
