@@ -413,6 +413,135 @@ __global__ void __launch_bounds__(kCodecNT) k_var_decode(int64_t ncol, const int
   }
 }
 
+
+// One pass instead of k_code_count + k_var_encode<0> + k_var_encode<1>: a wave per column counts every candidate form
+// (escapes of the u16 gaps, the value checks) AND writes the varint codes of the row gaps and of the values into the
+// column's worst-case slot (WR bytes per row gap: vlen of the largest row; 5 per value) at WR * cp[c] / 5 * cp[c], with
+// the column's code bytes in rbytes[c] / vbytes[c].  k_compact_codes then packs the slots into the message (2.4 bytes
+// per R-MAT entry read and written, against a second 12-byte read of the partial).  Value codes are written only when
+// every value so far is a u32 integer (a message whose values do not code ships them in another form).
+__global__ void __launch_bounds__(kCodecNT) k_code_encode(int64_t ncol, const int64_t* __restrict__ cp,
+                                                          const int32_t* __restrict__ ir, const double* __restrict__ val,
+                                                          int wr, uint8_t* __restrict__ rslot,
+                                                          uint8_t* __restrict__ vslot, int64_t* __restrict__ esc,
+                                                          int64_t* __restrict__ rbytes, int64_t* __restrict__ vbytes,
+                                                          unsigned long long* __restrict__ bad) {
+  __shared__ uint8_t stage[2][kCodeStep * 5];
+  const int l = lane_id();
+  int64_t b32 = 0, b16 = 0, bvar = 0;
+  for (int64_t c = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / kWave; c < ncol;
+       c += ((int64_t)gridDim.x * blockDim.x) / kWave) {
+    const int64_t s = cp[c], e = cp[c + 1];
+    int64_t ne = 0, orow = 0, oval = 0;   // escapes; code bytes written so far (uniform)
+    uint8_t* rdst = rslot + (int64_t)wr * s;
+    uint8_t* vdst = vslot ? vslot + 5 * s : nullptr;
+    int32_t prev = 0;
+    int32_t rn[kCodeEpl];
+    double xn[kCodeEpl];
+    auto load = [&](int64_t b) {   // clamped, unconditional (see k_code_count)
+#pragma unroll
+      for (int k = 0; k < kCodeEpl; ++k) {
+        const int64_t i = min(b + k, e - 1);
+        rn[k] = ir[i];
+        if (val) xn[k] = val[i];
+      }
+    };
+    if (s < e) load(s + kCodeEpl * l);
+    for (int64_t i0 = s; i0 < e; i0 += kCodeStep) {
+      const int64_t base = i0 + kCodeEpl * l;
+      int32_t r[kCodeEpl];
+      double x[kCodeEpl];
+#pragma unroll
+      for (int k = 0; k < kCodeEpl; ++k) { r[k] = rn[k]; x[k] = val ? xn[k] : 0.0; }
+      if (i0 + kCodeStep < e) load(base + kCodeStep);
+      const int32_t up = (int32_t)dpp_prev_lane((uint32_t)r[kCodeEpl - 1]);
+      const int32_t before = l == 0 ? prev : up;
+      uint32_t g[kCodeEpl], u[kCodeEpl];
+      int rl[kCodeEpl], vl[kCodeEpl];
+      int rt = 0, vt = 0;
+#pragma unroll
+      for (int k = 0; k < kCodeEpl; ++k) {
+        const bool in = base + k < e;
+        const int64_t d = (int64_t)r[k] - (k ? r[k - 1] : before);
+        g[k] = (uint32_t)d;
+        ne += in && d > (int64_t)kGapMax;
+        rl[k] = in ? vlen32(g[k]) : 0;
+        rt += rl[k];
+        u[k] = 0;
+        vl[k] = 0;
+        if (val && in) {
+          const double v = x[k];
+          b32 += __double_as_longlong((double)(float)v) != __double_as_longlong(v);
+          const bool in16 = v >= 0.0 && v <= 65535.0;
+          b16 += !(in16 && __double_as_longlong((double)(unsigned short)v) == __double_as_longlong(v));
+          const bool ok = as_u32(v, &u[k]);
+          bvar += !ok;
+          vl[k] = ok ? vlen32(u[k]) : 5;
+          vt += vl[k];
+        }
+      }
+      prev = (int32_t)last_lane((uint32_t)r[kCodeEpl - 1]);
+      // row codes: one wave scan places them in the row stage; value codes likewise in the value stage
+      const int ri = dpp_incl_scan(rt);
+      const int RT = (int)last_lane((uint32_t)ri);
+      int p = ri - rt;
+#pragma unroll
+      for (int k = 0; k < kCodeEpl; ++k)
+        for (int b = 0; b < rl[k]; ++b)
+          stage[0][p++] = (uint8_t)(((g[k] >> (7 * b)) & 0x7Fu) | (b + 1 < rl[k] ? 0x80u : 0u));
+      int VT = 0;
+      if (vdst) {
+        const int vi = dpp_incl_scan(vt);
+        VT = (int)last_lane((uint32_t)vi);
+        int q = vi - vt;
+#pragma unroll
+        for (int k = 0; k < kCodeEpl; ++k)
+          for (int b = 0; b < vl[k]; ++b)
+            stage[1][q++] = (uint8_t)(((u[k] >> (7 * b)) & 0x7Fu) | (b + 1 < vl[k] ? 0x80u : 0u));
+      }
+      wave_sync();
+      for (int q = l; q < RT; q += kWave) rdst[orow + q] = stage[0][q];
+      if (vdst)
+        for (int q = l; q < VT; q += kWave) vdst[oval + q] = stage[1][q];
+      wave_sync();   // the stages are written again by the next step
+      orow += RT;
+      oval += VT;
+    }
+    ne = wave_sum64(ne);
+    if (l == 0) {
+      esc[c] = ne;
+      rbytes[c] = orow;
+      if (vbytes) vbytes[c] = oval;
+    }
+  }
+  b32 = wave_sum64(b32);
+  b16 = wave_sum64(b16);
+  bvar = wave_sum64(bvar);
+  if (l == 0 && b32) atomicAdd(bad, (unsigned long long)b32);
+  if (l == 0 && b16) atomicAdd(bad + 1, (unsigned long long)b16);
+  if (l == 0 && bvar) atomicAdd(bad + 2, (unsigned long long)bvar);
+}
+
+// the columns' code slots (w bytes per entry, column c at w * cp[c]) packed into one stream at off[c] (a scan of
+// the code bytes): a wave per column, consecutive lanes on consecutive bytes
+__global__ void __launch_bounds__(kCodecNT) k_compact_codes(int64_t ncol, const int64_t* __restrict__ cp, int w,
+                                                            const uint8_t* __restrict__ slot,
+                                                            const int64_t* __restrict__ off, uint8_t* __restrict__ out) {
+  const int l = lane_id();
+  for (int64_t c = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) / kWave; c < ncol;
+       c += ((int64_t)gridDim.x * blockDim.x) / kWave) {
+    const uint8_t* src = slot + (int64_t)w * cp[c];
+    const int64_t o = off[c], n = off[c + 1] - o;
+    uint8_t* dst = out + o;
+    int64_t q = l;
+    for (; q + 3 * kWave < n; q += 4 * kWave) {   // four bytes in flight per lane
+      const uint8_t b0 = src[q], b1 = src[q + kWave], b2 = src[q + 2 * kWave], b3 = src[q + 3 * kWave];
+      dst[q] = b0; dst[q + kWave] = b1; dst[q + 2 * kWave] = b2; dst[q + 3 * kWave] = b3;
+    }
+    for (; q < n; q += kWave) dst[q] = src[q];
+  }
+}
+
 __global__ void k_gap_encode(int64_t ncol, const int64_t* __restrict__ cp, const int32_t* __restrict__ ir,
                              const int64_t* __restrict__ eoff, unsigned short* __restrict__ gap,
                              int32_t* __restrict__ esc) {
@@ -1346,7 +1475,37 @@ cbg_status fiber_encode(hipStream_t cst, const Scanner& scan, unsigned long long
   const bool vcheck = opt.narrow && dt == CBG_F64 && has_val && vs == 8 && n > 0;
   int64_t tot[3] = {0, 0, 0};
   unsigned long long bad[3] = {0, 0, 0};
-  if (coded || vcheck) {
+  // one pass (k_code_encode): the counts and the varint codes in per-column worst-case slots, packed below once the
+  // forms are chosen; the two-pass path (k_code_count, then the encoders re-read the partial) when the slots do not
+  // fit or varint codes are off (CBG_FIBER_ONEPASS=0 forces it)
+  static const bool onepass_env = [] {
+    const char* x = std::getenv("CBG_FIBER_ONEPASS");
+    return !(x && x[0] == '0');
+  }();
+  int wr = 1;
+  while (wr < 5 && (Po.nrow - 1) >> (7 * wr)) ++wr;   // varint bytes of the largest row (gap)
+  PoolBuf slot;
+  slot.pool = m.saux.pool;
+  const bool onepass = coded && opt.var && onepass_env &&
+                       slot.reserve((size_t)(wr + (vcheck ? 5 : 0)) * n + 16) == hipSuccess;
+  if (!onepass) (void)hipGetLastError();
+  uint8_t* rslot = onepass ? slot.as<uint8_t>() : nullptr;
+  uint8_t* vslot = onepass && vcheck ? rslot + (int64_t)wr * n : nullptr;
+  if (onepass) {
+    for (PoolBuf* pb : {&m.saux, &m.svr, &m.sescoff, &m.svroff}) HIPCHK(pb->reserve(8 * (oc + 1)));
+    if (vcheck) { HIPCHK(m.svv.reserve(8 * (oc + 1))); HIPCHK(m.svvoff.reserve(8 * (oc + 1))); }
+    HIPCHK(hipMemsetAsync(dbad, 0, 24, cst));
+    k_code_encode<<<codec_grid(oc), kCodecNT, 0, cst>>>(
+        oc, Po.cp, Po.ir, vcheck ? (const double*)Po.val : nullptr, wr, rslot, vslot, m.saux.as<int64_t>(),
+        m.svr.as<int64_t>(), vcheck ? m.svv.as<int64_t>() : nullptr, dbad);
+    HIPCHK(hipGetLastError());
+    CBGCHK(scan(oc, m.saux.as<int64_t>(), m.sescoff.as<int64_t>(), dtot + 0));
+    CBGCHK(scan(oc, m.svr.as<int64_t>(), m.svroff.as<int64_t>(), dtot + 1));
+    if (vcheck) CBGCHK(scan(oc, m.svv.as<int64_t>(), m.svvoff.as<int64_t>(), dtot + 2));
+    HIPCHK(hipMemcpyAsync(tot, dtot, 24, hipMemcpyDeviceToHost, cst));
+    HIPCHK(hipMemcpyAsync(bad, dbad, 24, hipMemcpyDeviceToHost, cst));
+    HIPCHK(hipStreamSynchronize(cst));
+  } else if (coded || vcheck) {
     for (PoolBuf* pb : {&m.saux, &m.svr, &m.sescoff, &m.svroff}) HIPCHK(pb->reserve(8 * (oc + 1)));
     if (vcheck) { HIPCHK(m.svv.reserve(8 * (oc + 1))); HIPCHK(m.svvoff.reserve(8 * (oc + 1))); }
     HIPCHK(hipMemsetAsync(dbad, 0, 24, cst));
@@ -1379,8 +1538,12 @@ cbg_status fiber_encode(hipStream_t cst, const Scanner& scan, unsigned long long
     m.srow_p = m.srow.p;
   } else if (m.rfmt == 2) {
     HIPCHK(m.srow.reserve(m.srow_b + 16));
-    k_var_encode<0><<<codec_grid(oc), kCodecNT, 0, cst>>>(oc, Po.cp, Po.ir, nullptr,
-                                                                         m.svroff.as<int64_t>(), m.srow.as<uint8_t>());
+    if (onepass)
+      k_compact_codes<<<codec_grid(oc), kCodecNT, 0, cst>>>(oc, Po.cp, wr, rslot, m.svroff.as<int64_t>(),
+                                                            m.srow.as<uint8_t>());
+    else
+      k_var_encode<0><<<codec_grid(oc), kCodecNT, 0, cst>>>(oc, Po.cp, Po.ir, nullptr, m.svroff.as<int64_t>(),
+                                                            m.srow.as<uint8_t>());
     m.srow_p = m.srow.p;
   }
   HIPCHK(m.sesc.reserve(16));   // a transport may be handed the escape buffers with zero bytes
@@ -1397,13 +1560,18 @@ cbg_status fiber_encode(hipStream_t cst, const Scanner& scan, unsigned long long
     else if (m.vfmt == 2)
       k_f64_to_u16<<<(int)grid_for(n, 256, kMaxGrid), 256, 0, cst>>>(n, (const double*)Po.val,
                                                                     m.sval.as<unsigned short>());
+    else if (onepass)
+      k_compact_codes<<<codec_grid(oc), kCodecNT, 0, cst>>>(oc, Po.cp, 5, vslot, m.svvoff.as<int64_t>(),
+                                                            m.sval.as<uint8_t>());
     else
       k_var_encode<1><<<codec_grid(oc), kCodecNT, 0, cst>>>(oc, Po.cp, nullptr, (const double*)Po.val,
-                                                                           m.svvoff.as<int64_t>(), m.sval.as<uint8_t>());
+                                                            m.svvoff.as<int64_t>(), m.sval.as<uint8_t>());
     m.sval_p = m.sval.p;
   }
   m.svh_p = m.vfmt == 3 ? (const void*)m.svv.p : (const void*)m.sesc.p;
   HIPCHK(hipGetLastError());
+  // the slots go back to the pool on return: the packing reads them first (the count exchange syncs here anyway)
+  if (onepass) HIPCHK(hipStreamSynchronize(cst));
   return CBG_OK;
 }
 

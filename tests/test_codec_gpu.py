@@ -140,3 +140,32 @@ def test_codec_five_byte_varints_across_lanes_and_steps(gpu_ctx):
     st = _mat(gpu_ctx, n, len(cols), cols).fiber_codec(3)
     _check(st, vals=1 << 3)
     assert st["entries"] == sum(len(c[0]) for c in cols)
+
+
+def test_codec_one_pass_equals_two_pass(gpu_ctx):
+    """The one-pass encoder (k_code_encode: counts + codes into per-column slots, then packed) produces the same wire
+    bytes and forms as the two-pass one (k_code_count, then k_var_encode re-reading the partial; CBG_FIBER_ONEPASS=0,
+    read once per process, so it runs in a child process), and both round-trip bit for bit."""
+    import json
+    import os
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    script = (
+        "import sys, json; sys.path.insert(0, %r)\n"
+        "import numpy as np, combblas_amd as cb\n"
+        "ctx = cb.Context(0)\n"
+        "n, cp, ir, val = cb.generate_rmat_host(13, 16, seed=9)\n"
+        "A = cb.SpDCCols.from_csc(ctx, n, n, cp, ir, val)\n"
+        "C = cb.LocalSpGEMMHash(cb.PlusTimesSRing('f64'), A, A)\n"
+        "print(json.dumps(C.fiber_codec(3)))\n") % os.path.dirname(here)
+    outs = []
+    for onepass in ("1", "0"):
+        r = subprocess.run([sys.executable, "-c", script], capture_output=True, text=True, timeout=300,
+                           env=dict(os.environ, CBG_FIBER_ONEPASS=onepass))
+        assert r.returncode == 0, r.stderr[-2000:]
+        outs.append(json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1]))
+    for st in outs:
+        _check(st, rows=1 << 2, vals=1 << 3)
+    keys = ("wire_bytes", "row_bytes", "value_bytes", "value_header_bytes", "header_bytes", "entries")
+    assert {k: outs[0][k] for k in keys} == {k: outs[1][k] for k in keys}
