@@ -958,12 +958,34 @@ def bench_rank_share(args):
             return P
 
         phase_keys = ("flops_ms", "bin_ms", "symbolic_ms", "scan_ms", "numeric_ms", "heavy_ms", "total_ms")
+        gather = L == 2 and args.fiber_mode == "gather"
+        if gather:   # the fiber gather (grid.hip fiber_gather): the partner's operands, as they would arrive
+            PA, PB = panels(other, i, j)
+            mine_b = _col_slice_block(BP, *halves[me])
+            sent_b = _col_slice_block(BP, *halves[other])
+            ent = 4 + 8   # row + f64 value
+            rec["gather_bytes_sent"] = AP.nnz * ent + 8 * (AP.ncol + 1) + sent_b.nnz * ent + 8 * (sent_b.ncol + 1)
+            part_b = _col_slice_block(PB, *halves[me])
+            rec["gather_bytes_recv"] = PA.nnz * ent + 8 * (PA.ncol + 1) + part_b.nnz * ent + 8 * (part_b.ncol + 1)
+            A2 = _hcat([AP, PA] if me == 0 else [PA, AP])
+            B2 = _vstack([mine_b, part_b] if me == 0 else [part_b, mine_b])
+            del PA, PB, mine_b, sent_b, part_b
+            torch.cuda.empty_cache()
         for rep in range(2):   # the second repetition is recorded (code objects loaded, pool warm)
             floor[0] = torch.cuda.mem_get_info()[0]
             st = {}
             torch.cuda.synchronize()
             t0 = time.perf_counter()
-            if L == 2:
+            if gather:
+                Pm = be.multiply(A2, B2, SR, st)
+                sample()
+                local_ms = 1e3 * (time.perf_counter() - t0)
+                merge_ms, wire = 0.0, None
+                nnz_out = Pm.nnz
+                profs = [ctx.last_profile()]
+                final = Pm if rep == 1 else None
+                del Pm
+            elif L == 2:
                 Po = be.multiply(AP, _col_slice_block(BP, *halves[other]), SR, st)
                 sample()
                 t1 = time.perf_counter()
@@ -1003,6 +1025,8 @@ def bench_rank_share(args):
             torch.cuda.synchronize()
             torch.cuda.empty_cache()
         del AP, BP
+        if gather:
+            del A2, B2
         torch.cuda.empty_cache()
         # the rank's finished piece C(rows_i, columns) against its independent reference (verify_piece)
         r0, r1 = cbd.block_range(n, q, i)
@@ -1015,7 +1039,8 @@ def bench_rank_share(args):
         v.update({"piece_nnz": final.nnz, "piece_nnz_equals_estimate": final.nnz == est_z,
                   "piece_multiplies_estimate": est_m})
         rec["verified"] = v
-        if L == 2:
+        rec["fiber_mode"] = "gather" if gather else ("reduce" if L == 2 else "none")
+        if L == 2 and not gather:
             rec["fiber_codec"] = codec
             rec["fiber_codec_vs_estimate"] = round(codec["wire_bytes"] / max(wire["bytes"], 1), 5)
         del final, Arow, Acol
@@ -1036,7 +1061,7 @@ def bench_rank_share(args):
                     "peak_hbm_GB": round((total - floor[0]) / 1e9, 2), "hbm_total_GB": round(total / 1e9, 1)})
         print(json.dumps(rec), flush=True)
         bad = bad or not (v["bit_exact"] and v["piece_nnz_equals_estimate"]
-                          and (L == 1 or codec["roundtrip_exact"]))
+                          and (L == 1 or gather or codec["roundtrip_exact"]))
     dist.destroy_process_group()
     if os.path.exists(store.name):
         os.unlink(store.name)
@@ -1168,6 +1193,9 @@ def main():
                     help="with --gpus-virtual N: run these ranks' shares of the N-GPU layout on this one GPU "
                          "('all' or a comma list); one JSON line per rank (local ms, fiber bytes, peak HBM)")
     ap.add_argument("--gpus-virtual", type=int, default=8)
+    ap.add_argument("--fiber-mode", choices=["gather", "reduce"], default="gather",
+                    help="--rank-share on two-layer layouts: the fiber gather of the operands (what the grid takes for "
+                         "A*A) or the reduction of partial products (codec + merge)")
     args = ap.parse_args()
     if args.rank_share is None and "WORLD_SIZE" not in os.environ and (args.gpus or 1) > 1:
         # launched as `python bench.py --gpus N`: this process becomes the launcher; it makes no GPU call

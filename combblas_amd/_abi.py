@@ -19,7 +19,7 @@ BOOL, I32, I64, F32, F64 = range(5)
 SORTED_COLS, KEEP_ON_DEVICE = 1, 2
 # include/cbgpu.h CBG_ABI_VERSION these declarations follow: the library writes structs the caller allocates
 # (cbg_profile, cbg_grid_stats), so a library of another ABI version is refused at load
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 
 class DcscView(ctypes.Structure):
@@ -60,7 +60,7 @@ class GridStats(ctypes.Structure):
                 ("fiber_xfer_ms", ctypes.c_double),
                 ("heavy_ms", ctypes.c_double), ("heavy_multiplies", ctypes.c_int64), ("heavy_nnz_b", ctypes.c_int64),
                 ("heavy_nnz_c", ctypes.c_int64), ("local_nnz_out", ctypes.c_int64), ("local_nnz_b", ctypes.c_int64),
-                ("local_ncol_b", ctypes.c_int64), ("local_products", ctypes.c_int32)]
+                ("local_ncol_b", ctypes.c_int64), ("local_products", ctypes.c_int32), ("fiber_mode", ctypes.c_int32)]
 
 
 class CodecStats(ctypes.Structure):

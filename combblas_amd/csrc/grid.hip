@@ -987,6 +987,18 @@ cbg_status panel_rows_dt(cbg_ctx* ctx, cbg_dtype dt, const std::vector<Piece>& b
 
 cbg_status fiber_pipeline(cbg_grid* G, const cbg_dcsc_view& va, const cbg_dcsc_view& vb, cbg_semiring sr,
                           cbg_dtype dt, Piece* out, cbg_grid_stats* st);
+cbg_status fiber_gather(cbg_grid* G, const cbg_dcsc_view& va, const cbg_dcsc_view& vb, cbg_semiring sr,
+                        cbg_dtype dt, Piece* out, cbg_grid_stats* st);
+cbg_status fiber_gather_ok(cbg_grid* G, const cbg_dcsc_view& va, const cbg_dcsc_view& vb, size_t vs, bool* out);
+// The two-layer plain product's fiber step: the operand gather when every rank finds it cheaper (fiber_gather_ok),
+// else the reduction pipeline.  CBG_FIBER_GATHER=0 always takes the reduction.
+cbg_status fiber_step(cbg_grid* G, const cbg_dcsc_view& va, const cbg_dcsc_view& vb, cbg_semiring sr, cbg_dtype dt,
+                      Piece* out, cbg_grid_stats* st) {
+  static const bool gather_env = [] { const char* e = std::getenv("CBG_FIBER_GATHER"); return !(e && e[0] == '0'); }();
+  bool gather = false;
+  if (gather_env) CBGCHK(fiber_gather_ok(G, va, vb, dt_size(dt), &gather));
+  return gather ? fiber_gather(G, va, vb, sr, dt, out, st) : fiber_pipeline(G, va, vb, sr, dt, out, st);
+}
 // Internal flag: L = 2, plain product -- the layer product runs in two column halves with the fiber exchange
 // of the other layer's half overlapping the own half (fiber_pipeline); parts then holds the reduced piece.
 constexpr uint32_t kFiberPipe = 1u << 29;
@@ -1127,7 +1139,7 @@ cbg_status summa_layer_impl(cbg_grid* G, const cbg_dcsc_view* Av, const cbg_dcsc
     cbg_dcsc_view vb = view_of(BP, dt, BP.val != nullptr);
     if (flags & kFiberPipe) {   // product + fiber reduction, overlapped
       Piece P;
-      CBGCHK(fiber_pipeline(G, va, vb, sr, dt, &P, st));
+      CBGCHK(fiber_step(G, va, vb, sr, dt, &P, st));
       if (st) st->stages += q;
       parts->push_back(P);
     } else {
@@ -1201,7 +1213,7 @@ cbg_status summa_layer_impl(cbg_grid* G, const cbg_dcsc_view* Av, const cbg_dcsc
     cbg_dcsc_view va = view_of(Ah[0], dt, Ah[0].val != nullptr);
     cbg_dcsc_view vb = view_of(Bh[0], dt, Bh[0].val != nullptr);
     Piece P;
-    CBGCHK(fiber_pipeline(G, va, vb, sr, dt, &P, st));
+    CBGCHK(fiber_step(G, va, vb, sr, dt, &P, st));
     if (st) ++st->stages;
     parts->push_back(P);
     return CBG_OK;
@@ -1639,9 +1651,177 @@ cbg_status fiber_decode(hipStream_t cst, const Scanner& scan, int64_t* dtot_a, i
 // more bytes per column: its value bytes), u16, f32 or the native f64.  A multiplicity-valued product (R-MAT A*A)
 // travels at ~2-3 bytes per entry.  CBG_FIBER_GAPS=0: int32 rows; CBG_FIBER_NARROW=0: native values;
 // CBG_FIBER_VARINT=0: no varint codes.
+
+// sum over B nonzeros b of the length of A column Bir[b]: estimateFLOP of a product (mtSpGEMM.h:1117-1135), one total
+__global__ void k_flops_total(int64_t nb, const int32_t* __restrict__ bir, const int64_t* __restrict__ acp,
+                              unsigned long long* __restrict__ out) {
+  int64_t f = 0;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nb; i += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t k = bir[i];
+    f += acp[k + 1] - acp[k];
+  }
+  f = wave_sum64(f);
+  if (lane_id() == 0 && f) atomicAdd(out, (unsigned long long)f);
+}
+
+// L = 2, plain product: the fiber GATHER.  Rank (l, i, j) and its fiber partner (1-l, i, j) swap their layer operands
+// instead of their partial products: each sends its A operand (the layer-l panel A(i, K_l), or its own piece when q = 1)
+// and the columns of its B operand that the partner keeps (B(K_l, J_other)), receives A(i, K_{1-l}) and B(K_{1-l}, J_l),
+// and multiplies A(i, [K_0 K_1]) * B([K_0; K_1], J_l) once -- the piece C(i, J_l) that the fiber reduction
+// (Reductions.h:36-130, ParFriends.h:3119-3183) makes from two partials, here with no partial written twice, no codec
+// and no merge.  The inner dimension is laid out in layer order on both ranks (layer 0's part first).  For A*A of a
+// power-law graph the operands are ~1/100 of the partial products (s22 on 2x2x2: ~0.3 GB against ~4.8 GB coded), so the
+// fiber moves far fewer bytes and the rank does the same multiplies.  Chosen by cbg_spgemm_grid when the partial's
+// multiplies exceed kGatherRatio x the operand entries to send, on every rank (fiber_mode()).
+constexpr double kGatherRatio = 4.0;
+
+// the decision, agreed over the world: every rank estimates the multiplies of the half it would send as a partial
+// (k_flops_total over its B operand's other columns) against the entries it would send instead, and checks that the
+// gathered operands fit comfortably in free HBM
+cbg_status fiber_gather_ok(cbg_grid* G, const cbg_dcsc_view& va, const cbg_dcsc_view& vb, size_t vs, bool* out) {
+  cbg_ctx* ctx = G->ctx;
+  hipStream_t cst = ctx->stream;
+  const int other = 1 - G->layer;
+  const int64_t ncol = vb.ncol;
+  const int64_t cb[3] = {0, ncol / 2, ncol};
+  int64_t e[2] = {0, 0};
+  if (ncol > 0) {
+    HIPCHK(hipMemcpyAsync(&e[0], (const int64_t*)vb.cp + cb[other], 8, hipMemcpyDeviceToHost, cst));
+    HIPCHK(hipMemcpyAsync(&e[1], (const int64_t*)vb.cp + cb[other + 1], 8, hipMemcpyDeviceToHost, cst));
+  }
+  HIPCHK(G->small.reserve(256));
+  unsigned long long* d = (unsigned long long*)G->small.as<int64_t>() + 24;
+  HIPCHK(hipMemsetAsync(d, 0, 8, cst));
+  HIPCHK(hipStreamSynchronize(cst));
+  const int64_t nb = e[1] - e[0];
+  if (nb > 0)
+    k_flops_total<<<(int)grid_for(nb, 256, kMaxGrid), 256, 0, cst>>>(nb, (const int32_t*)vb.ir + e[0],
+                                                                     (const int64_t*)va.cp, d);
+  HIPCHK(hipGetLastError());
+  unsigned long long flops = 0;
+  HIPCHK(hipMemcpyAsync(&flops, d, 8, hipMemcpyDeviceToHost, cst));
+  HIPCHK(hipStreamSynchronize(cst));
+  const int64_t send = va.nnz + nb;
+  size_t fr = 0, tot = 0;
+  HIPCHK(hipMemGetInfo(&fr, &tot));
+  const double bytes = 2.0 * (double)(va.nnz + vb.nnz) * (4.0 + (double)vs) * 2.0;   // received + layer-order copies
+  const bool mine = (double)flops >= kGatherRatio * (double)send && bytes < 0.25 * (double)fr;
+  return all_ok(G, mine, out);
+}
+
+cbg_status fiber_gather(cbg_grid* G, const cbg_dcsc_view& va, const cbg_dcsc_view& vb, cbg_semiring sr,
+                        cbg_dtype dt, Piece* out, cbg_grid_stats* st) {
+  cbg_ctx* ctx = G->ctx;
+  hipStream_t cst = ctx->stream;
+  const size_t vs = dt_size(dt);
+  const int me = G->layer, other = 1 - me;
+  const int64_t ncol = vb.ncol;
+  const int64_t cb[3] = {0, ncol / 2, ncol};
+  const double t0 = now_ms();
+  // my operands as pieces: A whole; B's columns of each half (rebased colptr, arrays from the column's first entry)
+  auto piece_of_view = [&](const cbg_dcsc_view& v) {
+    Piece p;
+    p.nrow = v.nrow; p.ncol = v.ncol; p.nnz = v.nnz;
+    p.cp = (const int64_t*)v.cp; p.ir = (const int32_t*)v.ir; p.val = v.val;
+    return p;
+  };
+  const Piece Am = piece_of_view(va);
+  const bool has_val = va.val != nullptr;
+  std::shared_ptr<Owner> bo(new Owner(ctx->pool)), bm(new Owner(ctx->pool));
+  auto col_piece = [&](int64_t c0, int64_t c1, Owner& o, Piece* p) -> cbg_status {
+    int64_t e[2] = {0, 0};
+    HIPCHK(hipMemcpyAsync(&e[0], (const int64_t*)vb.cp + c0, 8, hipMemcpyDeviceToHost, cst));
+    HIPCHK(hipMemcpyAsync(&e[1], (const int64_t*)vb.cp + c1, 8, hipMemcpyDeviceToHost, cst));
+    HIPCHK(hipStreamSynchronize(cst));
+    HIPCHK(o.cp.reserve(8 * (c1 - c0 + 1)));
+    k_cp_rebase<<<(int)grid_for(c1 - c0 + 1, 256, kMaxGrid), 256, 0, cst>>>(c1 - c0, (const int64_t*)vb.cp, c0,
+                                                                              o.cp.as<int64_t>());
+    HIPCHK(hipGetLastError());
+    p->nrow = vb.nrow; p->ncol = c1 - c0; p->nnz = e[1] - e[0];
+    p->cp = o.cp.as<int64_t>();
+    p->ir = (const int32_t*)vb.ir + e[0];
+    p->val = vb.val ? (const void*)((const char*)vb.val + vs * e[0]) : nullptr;
+    return CBG_OK;
+  };
+  Piece Bo, Bm;
+  CBGCHK(col_piece(cb[other], cb[other + 1], *bo, &Bo));   // what the partner keeps
+  CBGCHK(col_piece(cb[me], cb[me + 1], *bm, &Bm));         // what I keep
+  // sizes: [A nrow, A ncol, A nnz, B nrow, B ncol, B nnz, has values, 0] to the partner
+  HIPCHK(G->small.reserve(256));
+  int64_t* dsn = G->small.as<int64_t>();
+  const int64_t sz[8] = {Am.nrow, Am.ncol, Am.nnz, Bo.nrow, Bo.ncol, Bo.nnz, has_val ? 1 : 0, 0};
+  int64_t r8[8] = {0};
+  HIPCHK(hipMemcpyAsync(dsn, sz, 64, hipMemcpyHostToDevice, cst));
+  int64_t segs[2] = {0, 0};
+  segs[other] = 64;   // (only the partner's segment: both buffers start with it)
+  CBGCHK(t_alltoallv(G, CBG_GROUP_FIBER, dsn, segs, dsn + 16, segs, G->fiber_ctl));
+  HIPCHK(hipMemcpyAsync(r8, dsn + 16, 64, hipMemcpyDeviceToHost, cst));
+  HIPCHK(hipStreamSynchronize(cst));
+  // values travel when either side has them (an empty operand may come without a value array)
+  const bool hv = has_val || r8[6] != 0;
+  if (r8[0] != Am.nrow || r8[4] != Bm.ncol ||
+      (hv && ((Am.nnz && !Am.val) || (Bo.nnz && !Bo.val) || (Bm.nnz && !Bm.val) || (r8[2] + r8[5] && !r8[6]))))
+    return CBG_EDIM;
+  // receive storage: the partner's A operand and B(K_other, J_me)
+  std::shared_ptr<Owner> ar(new Owner(ctx->pool)), br(new Owner(ctx->pool));
+  Piece Ar, Br;
+  Ar.nrow = r8[0]; Ar.ncol = r8[1]; Ar.nnz = r8[2];
+  Br.nrow = r8[3]; Br.ncol = r8[4]; Br.nnz = r8[5];
+  for (auto* pr : {&Ar, &Br}) {
+    Owner& o = pr == &Ar ? *ar : *br;
+    HIPCHK(o.cp.reserve(8 * (pr->ncol + 1)));
+    HIPCHK(o.ir.reserve(4 * pr->nnz + 16));
+    HIPCHK(o.val.reserve(vs * pr->nnz + 16));
+    pr->cp = o.cp.as<int64_t>(); pr->ir = o.ir.as<int32_t>(); pr->val = hv ? o.val.p : nullptr;
+  }
+  // the exchange: six arrays, each one (grouped) send/recv pair on the fiber communicator
+  int64_t sent = 0;
+  auto swap = [&](const void* sp, int64_t sn, void* rp, int64_t rn) -> cbg_status {
+    int64_t sb[2] = {0, 0}, rb[2] = {0, 0};
+    sb[other] = sn; rb[other] = rn;
+    sent += sn;
+    if (sn || rn) CBGCHK(t_alltoallv(G, CBG_GROUP_FIBER, sp, sb, rp, rb));
+    return CBG_OK;
+  };
+  CBGCHK(swap(Am.cp, 8 * (Am.ncol + 1), (void*)Ar.cp, 8 * (Ar.ncol + 1)));
+  CBGCHK(swap(Am.ir, 4 * Am.nnz, (void*)Ar.ir, 4 * Ar.nnz));
+  if (hv) CBGCHK(swap(Am.val, (int64_t)vs * Am.nnz, (void*)Ar.val, (int64_t)vs * Ar.nnz));
+  CBGCHK(swap(Bo.cp, 8 * (Bo.ncol + 1), (void*)Br.cp, 8 * (Br.ncol + 1)));
+  CBGCHK(swap(Bo.ir, 4 * Bo.nnz, (void*)Br.ir, 4 * Br.nnz));
+  if (hv) CBGCHK(swap(Bo.val, (int64_t)vs * Bo.nnz, (void*)Br.val, (int64_t)vs * Br.nnz));
+  const double t1 = now_ms();
+  // operands in layer order: A(i, [K_0 K_1]) side by side, B([K_0; K_1], J_me) stacked by rows
+  std::vector<Piece> as = me == 0 ? std::vector<Piece>{Am, Ar} : std::vector<Piece>{Ar, Am};
+  std::vector<Piece> bs = me == 0 ? std::vector<Piece>{Bm, Br} : std::vector<Piece>{Br, Bm};
+  Piece A2, B2;
+  CBGCHK(panel_cols(ctx, as, vs, hv, &A2));
+  CBGCHK(panel_rows_dt(ctx, dt, bs, hv, &B2));
+  HIPCHK(hipStreamSynchronize(cst));   // the copies are done: the received operands go back to the pool
+  as.clear();
+  bs.clear();
+  Ar = Br = Bo = Bm = Piece();
+  ar.reset(); br.reset(); bo.reset(); bm.reset();
+  const cbg_dcsc_view a2 = view_of(A2, dt, hv), b2 = view_of(B2, dt, hv);
+  cbg_csc_result C;
+  int64_t m = 0;
+  CBGCHK(cbg_spgemm_local(ctx, &a2, &b2, sr, dt, CBG_SORTED_COLS, &C, &m));
+  note_local(st, ctx, b2);
+  *out = piece_of_result(C);
+  out->reduced = true;
+  if (st) {
+    st->multiplies += m;
+    st->local_ms += now_ms() - t1;
+    st->fiber_bytes += sent;
+    st->fiber_ms += t1 - t0;
+    st->fiber_mode = 2;
+  }
+  return CBG_OK;
+}
+
 cbg_status fiber_pipeline(cbg_grid* G, const cbg_dcsc_view& va, const cbg_dcsc_view& vb, cbg_semiring sr,
                           cbg_dtype dt, Piece* out, cbg_grid_stats* st) {
   cbg_ctx* ctx = G->ctx;
+  if (st) st->fiber_mode = 1;
   hipStream_t cst = ctx->stream;
   const size_t vs = dt_size(dt);
   const int me = G->layer, other = 1 - me;

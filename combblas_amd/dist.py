@@ -1068,6 +1068,9 @@ def _stats_update(stats, st):
     for k in ("heavy_multiplies", "heavy_nnz_b", "heavy_nnz_c", "local_nnz_out", "local_nnz_b", "local_ncol_b",
               "local_products"):
         stats[k] = stats.get(k, 0) + int(getattr(st, k))
+    # the two-layer fiber step the grid took (cbg_grid_stats.fiber_mode): a name, so per-step sums skip it
+    if int(st.fiber_mode):
+        stats["fiber_mode"] = {1: "reduce", 2: "gather"}.get(int(st.fiber_mode), str(int(st.fiber_mode)))
 
 
 class GpuBackend:

@@ -51,9 +51,10 @@
 extern "C" {
 #endif
 
-#define CBG_ABI_VERSION 3   /* 2: cbg_grid_stats.fiber_xfer_ms after stages; cbg_device_count
+#define CBG_ABI_VERSION 4   /* 2: cbg_grid_stats.fiber_xfer_ms after stages; cbg_device_count
                                3: cbg_profile heavy_* counts; cbg_grid_stats heavy / local-product sums;
-                                  cbg_fiber_codec */
+                                  cbg_fiber_codec
+                               4: cbg_grid_stats.fiber_mode */
 
 typedef enum {
   CBG_OK = 0,
@@ -317,6 +318,9 @@ typedef struct {
   int64_t heavy_multiplies, heavy_nnz_b, heavy_nnz_c;
   int64_t local_nnz_out, local_nnz_b, local_ncol_b;
   int32_t local_products;
+  /* ABI 4: the two-layer fiber step taken: 0 none (one layer), 1 the reduction of partial products (codec + merge),
+   * 2 the gather of the layer operands (one product, no partials) */
+  int32_t fiber_mode;
 } cbg_grid_stats;
 
 /* RCCL unique id (128 bytes) made on one rank and handed to all (any out-of-band channel). */

@@ -46,7 +46,7 @@ def test_no_oracle_in_product_library():
 def test_abi_version_and_strerror():
     from combblas_amd import _abi
     lib = _abi.lib()
-    assert lib.cbg_abi_version() == 3
+    assert lib.cbg_abi_version() == 4
     assert b"3002" in lib.cbg_strerror(3002)
     assert b"BoolCopy" in lib.cbg_strerror(13)
 

@@ -68,9 +68,9 @@ def test_rccl_native_grid_single_rank():
     spawn_case(1, "gpu-rccl", FIXTURE_CASES[:3], 29634, body=run_fixture_case)
 
 
-@pytest.mark.parametrize("staged", [False, True])
+@pytest.mark.parametrize("staged,fiber", [(False, "auto"), (True, "auto"), (False, "reduce")])
 @pytest.mark.parametrize("world,port", [(2, 29671), (4, 29672), (8, 29673)])
-def test_reference_fixtures_over_rccl_multirank(world, port, staged, monkeypatch):
+def test_reference_fixtures_over_rccl_multirank(world, port, staged, fiber, monkeypatch):
     """The production RCCL grid at world 2 / 4 / 8 (1x1x2, 2x2, 2x2x2) with every rank on cuda:0: libcbgpu's
     own communicators (ncclCommInitRank + ncclCommSplit), asynchronous ncclBroadcast of the stage pieces on
     the communication stream, grouped ncclSend/ncclRecv fiber all-to-all-v, ncclAllGather of the sizes.
@@ -79,9 +79,14 @@ def test_reference_fixtures_over_rccl_multirank(world, port, staged, monkeypatch
     C.mtx, G500 s10 under six semirings) must come out on every rank's piece, and RCCL must report the
     grid's group sizes."""
     from dist_support import run_fixture_case
+    if world == 4 and fiber == "reduce":
+        pytest.skip("one layer: no fiber step")
     if staged:
         monkeypatch.setenv("CBG_GRID_STAGED", "1")
-    spawn_case(world, "gpu-rccl-net", FIXTURE_CASES, port + (10 if staged else 0), body=run_fixture_case)
+    if fiber == "reduce":   # two layers: the reduction pipeline (codec + merge) instead of the operand gather
+        monkeypatch.setenv("CBG_FIBER_GATHER", "0")
+    spawn_case(world, "gpu-rccl-net", FIXTURE_CASES, port + (10 if staged else 0) + (20 if fiber == "reduce" else 0),
+               body=run_fixture_case)
 
 
 @pytest.mark.parametrize("world,port", [(2, 29641), (4, 29642), (8, 29643)])

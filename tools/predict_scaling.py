@@ -2,7 +2,8 @@
 """Predicted N-GPU step time of the mandated layouts from the one-GPU rank shares (`bench.py --rank-share`).
 
 Per rank: the panel broadcasts (its A and B panels less the pieces it owns, over one link), then on two-layer grids
-the fiber pipeline -- the other layer's column half multiplied in C chunks, each chunk's message sent as soon as it
+either the fiber gather (records with fiber_mode "gather": the partners swap their layer operands over one link, then
+one product) or the fiber pipeline -- the other layer's column half multiplied in C chunks, each chunk's message sent as soon as it
 is made while the next chunk and then the own half multiply (one link per direction, the partner's message arriving
 on the same schedule) -- then the decode of the received message and the merge; one-layer grids multiply once.
 The step is the slowest rank's; the value is the multiplies of all ranks over it.  When the record carries the
@@ -25,6 +26,13 @@ def rank_step(rec, link_gbps, chunks, decode_gbps=5000.0, entry_bytes=12, decode
     panel_bytes = (rec["nnz_A_panel"] + rec["nnz_B_panel"]) * entry_bytes * (q - 1) / q
     bcast = panel_bytes / bw
     ph = rec["phases_ms"]
+    if rec.get("fiber_mode") == "gather":
+        # the fiber gather: the partners swap their layer operands (both directions at once, one link), then one
+        # product of the full inner dimension for the own column half; no codec, no merge
+        xfer = max(rec.get("gather_bytes_sent", 0), rec.get("gather_bytes_recv", 0)) / bw
+        compute = sum(p["total_ms"] for p in ph)
+        return bcast + xfer + compute, {"bcast": bcast, "gather": xfer, "compute": compute, "encode": 0.0,
+                                        "fiber_exposed": 0.0, "decode": 0.0, "merge": 0.0}
     if L == 1 or not rec.get("fiber"):
         compute = sum(p["total_ms"] for p in ph)
         return bcast + compute, {"bcast": bcast, "compute": compute, "encode": 0.0, "fiber_exposed": 0.0, "decode": 0.0,
