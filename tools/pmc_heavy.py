@@ -80,6 +80,18 @@ def all_dispatches(path, counter):
     return tot
 
 
+def by_kernel(path, counter):
+    """counter summed per kernel (short name: the text before the template / argument list)"""
+    tot = {}
+    for f in glob.glob(os.path.join(path, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            if r["Counter_Name"] == counter:
+                name = r["Kernel_Name"].split("(")[0].split("<")[0].replace("cbg::(anonymous namespace)::", "")
+                name = name.replace("(anonymous namespace)::", "").replace("void ", "").strip()
+                tot[name] = tot.get(name, 0.0) + float(r["Counter_Value"])
+    return tot
+
+
 def run_product(tag, scale):
     """Whole-product HBM traffic: FETCH_SIZE / WRITE_SIZE summed over EVERY kernel of bench.py runs with 1 and 3
     timed products (+1 warmup, the generator, ...): the difference is two complete products' traffic, so the
@@ -99,6 +111,7 @@ def run_product(tag, scale):
             if r.returncode != 0:
                 sys.exit(r.returncode)
             tot[(ctr, steps)] = all_dispatches(d, ctr) * 1024.0
+            tot[(ctr, steps, "k")] = by_kernel(d, ctr)
     fetch = (tot[("FETCH_SIZE", 3)] - tot[("FETCH_SIZE", 1)]) / 2
     write = (tot[("WRITE_SIZE", 3)] - tot[("WRITE_SIZE", 1)]) / 2
     res = {"what": "one whole product (every kernel), R-MAT A*A", "scale": scale, "edgefactor": 16,
@@ -106,6 +119,15 @@ def run_product(tag, scale):
            "bytes_per_product": fetch + write, "bytes_per_product_fetch_doubled": 2 * fetch + write,
            "note": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (KiB x 1024) summed over all dispatches; (3 products - 1 "
                    "product) / 2; the guide's gfx950 x2 FETCH correction applies to 16-B/lane streams (upper bound)"}
+    # per kernel, per product (the same difference): where the product's bytes go
+    kern = {}
+    for ctr, key in (("FETCH_SIZE", "fetch"), ("WRITE_SIZE", "write")):
+        a, b = tot[(ctr, 1, "k")], tot[(ctr, 3, "k")]
+        for k in set(a) | set(b):
+            v = (b.get(k, 0.0) - a.get(k, 0.0)) / 2 * 1024.0
+            if abs(v) >= 1e6:
+                kern.setdefault(k, {})[key] = v
+    res["per_kernel"] = dict(sorted(kern.items(), key=lambda kv: -(kv[1].get("write", 0) + kv[1].get("fetch", 0))))
     dst = os.path.join(out, f"{tag}_pmc_product.json")
     json.dump(res, open(dst, "w"), indent=1)
     print(json.dumps(res))
