@@ -1726,7 +1726,8 @@ cbg_status fiber_gather(cbg_grid* G, const cbg_dcsc_view& va, const cbg_dcsc_vie
     return p;
   };
   const Piece Am = piece_of_view(va);
-  const bool has_val = va.val != nullptr;
+  // A and B carry values or not independently (a pattern operand, e.g. SelectMax<bool>'s A)
+  const bool hva_mine = va.val != nullptr, hvb_mine = vb.val != nullptr;
   std::shared_ptr<Owner> bo(new Owner(ctx->pool)), bm(new Owner(ctx->pool));
   auto col_piece = [&](int64_t c0, int64_t c1, Owner& o, Piece* p) -> cbg_status {
     int64_t e[2] = {0, 0};
@@ -1749,7 +1750,7 @@ cbg_status fiber_gather(cbg_grid* G, const cbg_dcsc_view& va, const cbg_dcsc_vie
   // sizes: [A nrow, A ncol, A nnz, B nrow, B ncol, B nnz, has values, 0] to the partner
   HIPCHK(G->small.reserve(256));
   int64_t* dsn = G->small.as<int64_t>();
-  const int64_t sz[8] = {Am.nrow, Am.ncol, Am.nnz, Bo.nrow, Bo.ncol, Bo.nnz, has_val ? 1 : 0, 0};
+  const int64_t sz[8] = {Am.nrow, Am.ncol, Am.nnz, Bo.nrow, Bo.ncol, Bo.nnz, hva_mine ? 1 : 0, hvb_mine ? 1 : 0};
   int64_t r8[8] = {0};
   HIPCHK(hipMemcpyAsync(dsn, sz, 64, hipMemcpyHostToDevice, cst));
   int64_t segs[2] = {0, 0};
@@ -1757,10 +1758,10 @@ cbg_status fiber_gather(cbg_grid* G, const cbg_dcsc_view& va, const cbg_dcsc_vie
   CBGCHK(t_alltoallv(G, CBG_GROUP_FIBER, dsn, segs, dsn + 16, segs, G->fiber_ctl));
   HIPCHK(hipMemcpyAsync(r8, dsn + 16, 64, hipMemcpyDeviceToHost, cst));
   HIPCHK(hipStreamSynchronize(cst));
-  // values travel when either side has them (an empty operand may come without a value array)
-  const bool hv = has_val || r8[6] != 0;
-  if (r8[0] != Am.nrow || r8[4] != Bm.ncol ||
-      (hv && ((Am.nnz && !Am.val) || (Bo.nnz && !Bo.val) || (Bm.nnz && !Bm.val) || (r8[2] + r8[5] && !r8[6]))))
+  // an operand's values travel when either side has them (an empty operand may come without a value array)
+  const bool hva = hva_mine || r8[6] != 0, hvb = hvb_mine || r8[7] != 0;
+  if (r8[0] != Am.nrow || r8[4] != Bm.ncol || (hva && ((Am.nnz && !Am.val) || (r8[2] && !r8[6]))) ||
+      (hvb && ((Bo.nnz && !Bo.val) || (Bm.nnz && !Bm.val) || (r8[5] && !r8[7]))))
     return CBG_EDIM;
   // receive storage: the partner's A operand and B(K_other, J_me)
   std::shared_ptr<Owner> ar(new Owner(ctx->pool)), br(new Owner(ctx->pool));
@@ -1772,7 +1773,8 @@ cbg_status fiber_gather(cbg_grid* G, const cbg_dcsc_view& va, const cbg_dcsc_vie
     HIPCHK(o.cp.reserve(8 * (pr->ncol + 1)));
     HIPCHK(o.ir.reserve(4 * pr->nnz + 16));
     HIPCHK(o.val.reserve(vs * pr->nnz + 16));
-    pr->cp = o.cp.as<int64_t>(); pr->ir = o.ir.as<int32_t>(); pr->val = hv ? o.val.p : nullptr;
+    pr->cp = o.cp.as<int64_t>(); pr->ir = o.ir.as<int32_t>();
+    pr->val = (pr == &Ar ? hva : hvb) ? o.val.p : nullptr;
   }
   // the exchange: six arrays, each one (grouped) send/recv pair on the fiber communicator
   int64_t sent = 0;
@@ -1785,23 +1787,23 @@ cbg_status fiber_gather(cbg_grid* G, const cbg_dcsc_view& va, const cbg_dcsc_vie
   };
   CBGCHK(swap(Am.cp, 8 * (Am.ncol + 1), (void*)Ar.cp, 8 * (Ar.ncol + 1)));
   CBGCHK(swap(Am.ir, 4 * Am.nnz, (void*)Ar.ir, 4 * Ar.nnz));
-  if (hv) CBGCHK(swap(Am.val, (int64_t)vs * Am.nnz, (void*)Ar.val, (int64_t)vs * Ar.nnz));
+  if (hva) CBGCHK(swap(Am.val, (int64_t)vs * Am.nnz, (void*)Ar.val, (int64_t)vs * Ar.nnz));
   CBGCHK(swap(Bo.cp, 8 * (Bo.ncol + 1), (void*)Br.cp, 8 * (Br.ncol + 1)));
   CBGCHK(swap(Bo.ir, 4 * Bo.nnz, (void*)Br.ir, 4 * Br.nnz));
-  if (hv) CBGCHK(swap(Bo.val, (int64_t)vs * Bo.nnz, (void*)Br.val, (int64_t)vs * Br.nnz));
+  if (hvb) CBGCHK(swap(Bo.val, (int64_t)vs * Bo.nnz, (void*)Br.val, (int64_t)vs * Br.nnz));
   const double t1 = now_ms();
   // operands in layer order: A(i, [K_0 K_1]) side by side, B([K_0; K_1], J_me) stacked by rows
   std::vector<Piece> as = me == 0 ? std::vector<Piece>{Am, Ar} : std::vector<Piece>{Ar, Am};
   std::vector<Piece> bs = me == 0 ? std::vector<Piece>{Bm, Br} : std::vector<Piece>{Br, Bm};
   Piece A2, B2;
-  CBGCHK(panel_cols(ctx, as, vs, hv, &A2));
-  CBGCHK(panel_rows_dt(ctx, dt, bs, hv, &B2));
+  CBGCHK(panel_cols(ctx, as, vs, hva, &A2));
+  CBGCHK(panel_rows_dt(ctx, dt, bs, hvb, &B2));
   HIPCHK(hipStreamSynchronize(cst));   // the copies are done: the received operands go back to the pool
   as.clear();
   bs.clear();
   Ar = Br = Bo = Bm = Piece();
   ar.reset(); br.reset(); bo.reset(); bm.reset();
-  const cbg_dcsc_view a2 = view_of(A2, dt, hv), b2 = view_of(B2, dt, hv);
+  const cbg_dcsc_view a2 = view_of(A2, dt, hva), b2 = view_of(B2, dt, hvb);
   cbg_csc_result C;
   int64_t m = 0;
   CBGCHK(cbg_spgemm_local(ctx, &a2, &b2, sr, dt, CBG_SORTED_COLS, &C, &m));
