@@ -151,11 +151,32 @@ def main():
             me, other = (l, 1 - l) if L == 2 else (0, None)
             rec = {"config": label, "rank": r, "layout": f"{L}x{q}x{q}", "l_i_j": [l, i, j], **extra,
                    "nnz_A_panel": AP.nnz, "nnz_B_panel": BP.nnz, "panel_build_s": round(build_s, 3)}
+            gather = False
+            if L == 2:   # the grid's choice (grid.hip fiber_gather_ok): the partial's multiplies vs the entries to send
+                Bo = bench._col_slice_block(BP, *halves[other])
+                flops_other = int(torch.diff(AP.cp)[Bo.ir.to(torch.int64)].sum().item()) if Bo.nnz else 0
+                gather = flops_other >= 4.0 * (AP.nnz + Bo.nnz)
+                if gather:
+                    PA, PB = panels(Am, Bm, q, L, other, i, j)
+                    mine_b = bench._col_slice_block(BP, *halves[me])
+                    part_b = bench._col_slice_block(PB, *halves[me])
+                    rec["gather_bytes_sent"] = 12 * (AP.nnz + Bo.nnz) + 8 * (AP.ncol + Bo.ncol + 2)
+                    rec["gather_bytes_recv"] = 12 * (PA.nnz + part_b.nnz) + 8 * (PA.ncol + part_b.ncol + 2)
+                    A2 = bench._hcat([AP, PA] if me == 0 else [PA, AP])
+                    B2 = bench._vstack([mine_b, part_b] if me == 0 else [part_b, mine_b])
+                    del PA, PB, mine_b, part_b
+                del Bo
+            rec["fiber_mode"] = "gather" if gather else ("reduce" if L == 2 else "none")
             for rep in range(2):   # the second repetition is recorded
                 st = {}
                 torch.cuda.synchronize()
                 t0 = time.perf_counter()
-                if L == 2:
+                if gather:
+                    M = be.multiply(A2, B2, SR, st)
+                    torch.cuda.synchronize()
+                    local_ms, merge_ms, codec = 1e3 * (time.perf_counter() - t0), 0.0, None
+                    profs = [ctx.last_profile()]
+                elif L == 2:
                     Po = be.multiply(AP, bench._col_slice_block(BP, *halves[other]), SR, st)
                     t1 = time.perf_counter()
                     p_other = ctx.last_profile()
@@ -187,6 +208,8 @@ def main():
                 del M
                 torch.cuda.empty_cache()
             del AP, BP
+            if gather:
+                del A2, B2
             r0, r1 = cbd.block_range(Am[0], q, i)
             b0, _ = cbd.block_range(Bm[1], q, j)
             h0, h1 = halves[me]
