@@ -20,6 +20,23 @@ import json
 def rank_step(rec, link_gbps, chunks, decode_gbps=5000.0, entry_bytes=12, decode_hidden=0.0):
     """Milliseconds of one rank's step (see the module docstring); returns (total, parts)."""
     bw = link_gbps * 1e9 / 1e3   # bytes per ms
+    if rec["layout"] == "1 GPU":   # the N = 1 anchor (configs 4: expansion + prune on one GPU)
+        t = float(rec["local_ms"]) + float(rec.get("prune_ms", 0.0))
+        return t, {"compute": float(rec["local_ms"]), "prune": float(rec.get("prune_ms", 0.0))}
+    total, parts = rank_step_grid(rec, link_gbps, chunks, decode_gbps, entry_bytes, decode_hidden)
+    pr = rec.get("prune")
+    if pr:   # configs 4: the distributed MCLPruneRecoverySelect after the product: the rank's column group gathered
+        # along the processor column (its unpruned entries from the q - 1 other row blocks), pruned, and the kept
+        # entries scattered back (dist._gather_columns / _scatter_columns)
+        q = int(rec["layout"].split("x")[1])
+        back = pr.get("prune_kept_nnz", 0) * entry_bytes * (q - 1) / q if pr.get("gather_bytes_offrank") else 0.0
+        parts["prune"] = float(pr["prune_ms"]) + (pr.get("gather_bytes_offrank", 0) + back) / bw
+        total += parts["prune"]
+    return total, parts
+
+
+def rank_step_grid(rec, link_gbps, chunks, decode_gbps=5000.0, entry_bytes=12, decode_hidden=0.0):
+    bw = link_gbps * 1e9 / 1e3   # bytes per ms
     L = int(rec["layout"].split("x")[0])
     q = int(rec["layout"].split("x")[1])
     # panels: q pieces of A along the grid row and q of B along the grid column arrive, the own ones do not move
