@@ -86,8 +86,8 @@ def by_kernel(path, counter):
     for f in glob.glob(os.path.join(path, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
             if r["Counter_Name"] == counter:
-                name = r["Kernel_Name"].split("(")[0].split("<")[0].replace("cbg::(anonymous namespace)::", "")
-                name = name.replace("(anonymous namespace)::", "").replace("void ", "").strip()
+                name = r["Kernel_Name"].replace("(anonymous namespace)::", "").replace("cbg::", "")
+                name = name.replace("void ", "").split("(")[0].split("<")[0].strip()
                 tot[name] = tot.get(name, 0.0) + float(r["Counter_Value"])
     return tot
 
