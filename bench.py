@@ -564,6 +564,7 @@ def bench_dist(args, world, rank, local_rank):
         for k, v in st.items():
             if isinstance(v, (int, float)):
                 phases[k] = phases.get(k, 0) + v
+        keep["fiber_mode"] = st.get("fiber_mode", "none")   # the grid's two-layer fiber step (gather / reduce)
         return st.get("multiplies", 0), nz
 
     step()   # first product also sets up libcbgpu's grid (its RCCL communicators); a failure ends the run
@@ -624,6 +625,7 @@ def bench_dist(args, world, rank, local_rank):
     ok_all = all(r["verify"]["bit_exact"] and r["verify"]["piece_nnz_equals_estimate"] and r["verify"]["steps_same_nnz"]
                  for r in recs)
     ok_all = ok_all and int(mults / args.steps) == flops_global and int(nnzc / args.steps) == nnz_global
+    fiber_mode = keep.get("fiber_mode", "none")
     keep.clear()
     del C
     torch.cuda.empty_cache()
@@ -672,6 +674,7 @@ def bench_dist(args, world, rank, local_rank):
                # the whole product's entry checksum (every rank's piece): equal across the layouts of one scale
                "full_output_checksum": f"{int(csum[2].item()) & ((1 << 64) - 1):016x}",
                "grid_transport": ginfo["kind"],
+               "fiber_mode": fiber_mode,
                # members of every communicator as RCCL itself counts them (ncclCommCount)
                "rccl_ranks": ginfo["ranks"] if ginfo["kind"] == "rccl" else None,
                "input": {"generator": "SpParMat3D.from_rmat: each rank builds its own A and B pieces on its GPU "
