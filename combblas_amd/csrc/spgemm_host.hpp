@@ -776,7 +776,8 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
       cap.add(*b, "heavy units");
     CAPCHK(cap);
     k_build_units<<<(H + 255) / 256, 256, 0, st>>>(H, ctx->heavy_cols.as<int32_t>(), ctx->sub.as<int32_t>(), nsub,
-                                                   slog, heavy_unit_cap<SRT>(), heavy_span_cap<SRT>(), span,
+                                                   slog, heavy_unit_cap<SRT>(), heavy_span_cap<SRT>(),
+                                                   heavy_rank_bytes<SRT>(), (int32_t)sizeof(typename SRT::Acc), span,
                                                    colptr, B.cp, units, ctx->ucnt.as<int64_t>(),
                                                    ctx->uspan.as<int2>(), nnz, ctx->nunits.as<int32_t>(),
                                                    ctx->segsz.as<int64_t>(), ctx->icnt.as<int64_t>(),

@@ -1461,6 +1461,15 @@ template <class SRT>
 constexpr int64_t heavy_unit_cap() {
   return SRT::kAddIsError || !CBG_RANK_MODE ? (int64_t)(1 << CBG_HEAVY_LOGT) / 2 : kUnitCap;
 }
+// Round 6: a unit's span also grows with the LDS its values leave free -- a unit of cnt outputs fits the rows-known
+// kernel while cnt*sA (padded) + 4*(span/32 + 2) <= (T+NT)*(sA+4) and span <= 64T (the pair-word directory) -- so a
+// sparse, span-limited unit takes up to 64T rows instead of the cap a full unit needs: s20 heavy 29.6 -> 27.6 ms, s21
+// 201.8 -> 194.3 ms per product, s22 2x2x2 rank 0 83.7 -> 80.7 ms (same-box A/B, profiles/r06l_span_adaptive_ab.txt)
+template <class SRT>
+constexpr int64_t heavy_rank_bytes() {   // 0: no rank mode (the fixed span cap alone)
+  constexpr int64_t T = 1 << CBG_HEAVY_LOGT, NT = CBG_HEAVY_NT, sA = sizeof(typename SRT::Acc);
+  return SRT::kAddIsError || !CBG_RANK_MODE ? 0 : (T + NT) * (sA + 4);
+}
 template <class SRT>
 constexpr int64_t heavy_span_cap() {
   constexpr int64_t T = 1 << CBG_HEAVY_LOGT, NT = CBG_HEAVY_NT, sA = sizeof(typename SRT::Acc);
@@ -1500,7 +1509,7 @@ __global__ void __launch_bounds__(256) k_heavy_sums(int H, const int32_t* __rest
 // unit_cap / span_cap come from the semiring (heavy_unit_caps): rank-mode accumulators hold up to
 // kUnitCap outputs over a bounded span; hash-only semirings (BoolCopy) keep load <= 1/2.
 __global__ void k_build_units(int H, const int32_t* __restrict__ cols, const int32_t* __restrict__ sub, int32_t nsub,
-                              int32_t log, int64_t unit_cap, int64_t span_cap,
+                              int32_t log, int64_t unit_cap, int64_t span_cap, int64_t rank_bytes, int32_t acc_bytes,
                               const int2* __restrict__ span, const int64_t* __restrict__ colptr,
                               const int64_t* __restrict__ Bcp, Unit* __restrict__ units, int64_t* __restrict__ ucnt,
                               int2* __restrict__ uspan, int64_t* __restrict__ nnz, int32_t* __restrict__ nunits,
@@ -1557,7 +1566,13 @@ __global__ void k_build_units(int H, const int32_t* __restrict__ cols, const int
   for (int32_t s = sf; s <= sl; ++s) {
     const int64_t n = c[s];
     if (acc == 0) st = s;   // a unit starts at its first non-empty subwindow (empty gaps span nothing)
-    const bool wide = span_cap > 0 && (((int64_t)(s + 1 - st) << log) > span_cap);
+    const int64_t sub_span = (int64_t)(s + 1 - st) << log;
+    int64_t cap = span_cap;
+    if (rank_bytes > 0) {   // adaptive: the LDS the unit's values leave to its bitmap, within the directory's 64T rows
+      const int64_t cpad = (acc + n + 1) & ~(int64_t)1;
+      cap = min((int64_t)64 << CBG_HEAVY_LOGT, 8 * (rank_bytes - cpad * acc_bytes - 8));
+    }
+    const bool wide = span_cap > 0 && sub_span > cap;
     if (acc > 0 && (acc + n > unit_cap || wide)) {
       emit(st, s, acc);
       st = s;

@@ -14,7 +14,8 @@ if __name__ == "__main__":
     if len(sys.argv) > 2 and sys.argv[1] == "--one":
         sys.path.insert(0, REPO)
         from combblas_amd import _abi
-        _abi.LIB_PATH = os.path.join(HERE, "var", sys.argv[2], "libcbgpu.so")
+        if sys.argv[2] != "main":   # "main": the in-tree product library
+            _abi.LIB_PATH = os.path.join(HERE, "var", sys.argv[2], "libcbgpu.so")
         sys.argv = [os.path.join(REPO, "bench.py")] + sys.argv[3:]
         runpy.run_path(sys.argv[0], run_name="__main__")
         sys.exit(0)
