@@ -98,9 +98,11 @@ constexpr int64_t kHeavy = CBG_HEAVY_MIN;   // nnz(C(:,j)) above which a column 
 #define CBG_RANK_SPAN_CAP 458752   // f64, T=8192, NT=1024, unit cap 6144: <= (9216*12 - 6144*8)/4 words
 #endif
 #ifndef CBG_UNIT_CAP
-// rank mode holds up to T outputs: 7/8 T measured best in round 5 (s20 66.9 -> 66.3 ms, s21 203.4 -> 202.2 ms against
-// 3/4 T; T itself is faster at s20 but slower at s21, profiles/r05s_unit_cap_ab.txt, r05t_unit_cap_ab.txt)
-#define CBG_UNIT_CAP (7 << (CBG_HEAVY_LOGT - 3))
+// rank mode holds up to T outputs.  Round 5 measured 7/8 T best (s20 66.9 -> 66.3 ms, s21 203.4 -> 202.2 ms against
+// 3/4 T; T faster at s20, slower at s21: profiles/r05s_unit_cap_ab.txt, r05t_unit_cap_ab.txt); with the adaptive unit
+// span (round 6) T is ahead everywhere: s20 64.0 -> 63.7 ms, s21 194.7 -> 194.2 ms, s22 2x2x2 rank 0 81.2 -> 80.4 ms
+// (3/4 T: 64.6 / 196.8 / 82.7 ms; profiles/r06m_unit_cap_ab.txt)
+#define CBG_UNIT_CAP (1 << CBG_HEAVY_LOGT)
 #endif
 // smallest subwindow: 2^13 rows, or the heavy table's 2^CBG_HEAVY_LOGT when that is smaller (a one-subwindow unit
 // must fit k_num_heavy's dense table)
