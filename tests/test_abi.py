@@ -132,3 +132,17 @@ def test_rmat_host_equals_reference_fixture_arrays():
         z = load_fixture(f"g500_s{scale}")
         n, cp, ir, val = cb.generate_rmat_host(scale, 16)
         assert np.array_equal(cp, z["A_cp"]) and np.array_equal(ir, z["A_ir"]) and np.array_equal(val, z["A_val"])
+
+
+def test_loader_refuses_another_abi_version(monkeypatch):
+    """The library writes structs the caller allocates (cbg_profile, cbg_grid_stats): _abi.lib() refuses a library whose
+    cbg_abi_version() is not the one these bindings were written for."""
+    from combblas_amd import _abi
+    saved = _abi._lib
+    try:
+        monkeypatch.setattr(_abi, "_lib", None)
+        monkeypatch.setattr(_abi, "ABI_VERSION", _abi.ABI_VERSION + 1)
+        with pytest.raises(OSError, match="cbg_abi_version"):
+            _abi.lib()
+    finally:
+        _abi._lib = saved
