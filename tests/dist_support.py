@@ -450,10 +450,17 @@ def run_rmat_case(rank, world, port, backend_kind, cases, errq):
         be = cbd.GpuBackend(cb.Context(0)) if backend_kind.startswith("gpu") else ScipyBackend()
         from helpers import fixture_product, load_fixture
         for (name, scale) in cases:
-            if name == "single-gpu":   # no fixture: the layouts against the one-GPU product of the same matrix
+            if name in ("single-gpu", "fiber-mode"):   # the layouts against the one-GPU product of the same matrix
                 Ad = cbd.SpParMat3D.from_rmat(grid, scale, 16, cb.G500_SEED, True, be)
                 Bd = cbd.SpParMat3D.from_rmat(grid, scale, 16, cb.G500_SEED, False, be)
-                C = cbd.Mult_AnXBn_SUMMA3D(cb.PlusTimesSRing("f64"), Ad, Bd)
+                st = {}
+                C = cbd.Mult_AnXBn_SUMMA3D(cb.PlusTimesSRing("f64"), Ad, Bd, st)
+                if name == "fiber-mode":   # the grid's two-layer fiber step: gather for A*A, unless switched off
+                    want = "none" if L == 1 else ("reduce" if os.environ.get("CBG_FIBER_GATHER") == "0" else "gather")
+                    got = st.get("fiber_mode", "none")
+                    assert got == want, f"rank {rank}: fiber mode {got}, expected {want}"
+                    if want == "gather":   # the operands crossed the fiber, not partial products
+                        assert st["fiber_bytes"] > 0 and st["merge_ms"] == 0
                 M = be.ctx.generate_rmat(scale, 16, seed=cb.G500_SEED)
                 P = cb.LocalSpGEMMHash(cb.PlusTimesSRing("f64"), M, M)
                 cp, ir, val = P.to_host()

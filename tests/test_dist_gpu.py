@@ -159,3 +159,15 @@ def test_fiber_wire_formats(kind, port, env, monkeypatch):
         monkeypatch.setenv(k, v)
     cases = FIBER_CASES if env == "default" else [c[:-1] + (None,) for c in FIBER_CASES]
     spawn_case(2, kind, cases, port + off, body=run_fiber_case)
+
+
+@pytest.mark.parametrize("fiber", ["auto", "reduce"])
+@pytest.mark.parametrize("world,port", [(2, 29681), (8, 29683)])
+def test_fiber_gather_and_reduction_on_rmat(world, port, fiber, monkeypatch):
+    """Two-layer grids (1x1x2, 2x2x2) over libcbgpu's RCCL grid on an R-MAT s14 A*A: the grid takes the fiber gather of
+    the layer operands (operands on the fiber, no merge) unless CBG_FIBER_GATHER=0 forces the reduction of partial
+    products; either way every rank's piece equals the same block of the one-GPU product (multiplicities: bit-exact)."""
+    from dist_support import run_rmat_case
+    if fiber == "reduce":
+        monkeypatch.setenv("CBG_FIBER_GATHER", "0")
+    spawn_case(world, "gpu-rccl-net", [("fiber-mode", 14)], port + (1 if fiber == "reduce" else 0), body=run_rmat_case)
