@@ -129,6 +129,10 @@ def part_anatomy(A, cp, ir, bcp, bir, pick, C, plog=18, G=4):
     cnt = np.bincount(col * P + (ir >> plog), minlength=A.shape[1] * P).reshape(A.shape[1], P)
     pos = ir - cp[col]                          # entry's position in its column
     tot = dict(parts=0, staged=0, nonempty=0, mult=0, groups=0, lines=0, outputs=0)
+    # word privatisation: the bitmap ORs one LDS instruction issues -- 64 lanes, each on the i-th entry of
+    # its group of G consecutive entries of one segment, lanes on consecutive groups -- against the distinct bitmap
+    # words among them (what a wave-level combine would issue), and against the distinct words inside each group
+    pv = dict(lane_entries=0, words_per_instr=0, words_per_group=0)
     hist = np.zeros(66, np.int64)
     for t, j in enumerate(pick):
         rows = C.indices[C.indptr[t]:C.indptr[t + 1]]
@@ -148,6 +152,18 @@ def part_anatomy(A, cp, ir, bcp, bir, pick, C, plog=18, G=4):
             start = cp[ks] + cnt[ks, :p].sum(axis=1)
             nz = L > 0
             tot["lines"] += int((((start[nz] + L[nz] - 1) * 4) // 64 - (start[nz] * 4) // 64 + 1).sum())
+            if nz.any():   # this part's multiplies in staging order: segments in B order, rows ascending in each
+                segs = [ir[s0:s0 + l] for s0, l in zip(start[nz], L[nz])]
+                words = np.concatenate(segs).astype(np.int64) >> 5
+                gcnt = (L[nz] + G - 1) // G
+                gid = np.concatenate([np.arange(l) // G for l in L[nz]]) + np.repeat(
+                    np.concatenate([[0], np.cumsum(gcnt)[:-1]]), L[nz])
+                ent = np.concatenate([np.arange(l) % G for l in L[nz]])
+                pv["lane_entries"] += len(words)
+                key_g = gid * (1 << 40) + words
+                pv["words_per_group"] += len(np.unique(key_g))
+                key_i = ((gid // 64) * G + ent) * (1 << 40) + words   # (wave step, entry index) -> distinct words
+                pv["words_per_instr"] += len(np.unique(key_i))
     del pos
     print(f"k_sym_part view ({P} parts of 2^{plog} rows over {nrow} rows):")
     for k, v in tot.items():
@@ -158,6 +174,10 @@ def part_anatomy(A, cp, ir, bcp, bir, pick, C, plog=18, G=4):
           f"{tot['mult'] / max(tot['outputs'], 1):.2f}")
     Lr = np.arange(66)
     print("  nonempty part-segment lengths:", {int(l): round(float(hist[l] / max(hist.sum(), 1)), 4) for l in Lr if hist[l]})
+    e = max(pv["lane_entries"], 1)
+    print(f"  word privatisation: bitmap ORs now {pv['lane_entries']} (one per multiply; the read-before-OR skips set "
+          f"bits), distinct words per wave instruction {pv['words_per_instr']} ({pv['words_per_instr'] / e:.4f} of them), "
+          f"distinct words per lane group {pv['words_per_group']} ({pv['words_per_group'] / e:.4f})")
 
 
 if __name__ == "__main__":
