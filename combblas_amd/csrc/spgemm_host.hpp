@@ -815,7 +815,7 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
     cap.add(ctx->useg, "useg");
     k_unit_segs<SRT, CBG_KNOWN_LOGT, CBG_KNOWN_NT><<<H, 256, 0, st>>>(
         ctx->heavy_cols.as<int32_t>(), ctx->nunits.as<int32_t>(), ctx->segoff.as<int64_t>(), units, nsub, A.cp, A.ir,
-        B.cp, B.ir, spl, ctx->useg.as<UnitSeg>(), ctx->uspan.as<int2>());
+        B.cp, B.ir, spl, ctx->useg.as<UnitSeg>());
     // units -> rows-known list + other items (device counts sc[12], sc[13]; units <= items * kItemUnits)
     const int64_t ucap = nitems * kItemUnits + 1;
     HIPCHK(ctx->items.reserve(sizeof(KnownUnit) * ucap));

@@ -1431,14 +1431,24 @@ __global__ void __launch_bounds__(256) k_scan_apply(int64_t n, const int64_t* __
 // split table rows for long A columns
 __global__ void k_split_assign(int64_t ncol, const int64_t* __restrict__ Acp, int32_t* __restrict__ idx,
                                int32_t* __restrict__ longcols, int* __restrict__ nlong) {
-  for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < ncol; k += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t len = Acp[k + 1] - Acp[k];
-    if (len >= kSplitMin) {
-      const int e = atomicAdd(nlong, 1);
-      idx[k] = e;
-      longcols[e] = (int32_t)k;
-    } else {
-      idx[k] = -1;
+  // one counter claim per wavefront (ballot + prefix popcount): a claim per long column serialised on the counter
+  // (0.74 ms for the 2^22 columns of an s22 rank panel)
+  const int lane = lane_id();
+  for (int64_t k0 = blockIdx.x * (int64_t)blockDim.x + (threadIdx.x & ~(kWave - 1)); k0 < ncol;
+       k0 += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t k = k0 + lane;
+    const bool lng = k < ncol && Acp[k + 1] - Acp[k] >= kSplitMin;
+    const uint64_t m = __ballot(lng);
+    int e0 = 0;
+    if (m) {
+      const int lead = __ffsll((unsigned long long)m) - 1;
+      if (lane == lead) e0 = atomicAdd(nlong, __popcll(m));
+      e0 = __shfl(e0, lead, kWave);
+    }
+    if (k < ncol) {
+      const int e = e0 + __popcll(m & ((1ull << lane) - 1ull));
+      idx[k] = lng ? e : -1;
+      if (lng) longcols[e] = (int32_t)k;
     }
   }
 }
@@ -1605,42 +1615,62 @@ __global__ void k_build_units(int H, const int32_t* __restrict__ cols, const int
   icnt[h] = (u + kItemUnits - 1) / kItemUnits;
 }
 
-// Segment table of every unit: for each heavy column, each B nonzero b = (k, B(k,j)) is visited once
-// and its A column's boundaries for all of the column's units are written (one split-table row read,
-// mostly from cache, instead of a dependent lookup chain per (unit, b) inside the numeric kernel).
-// Short A columns are given whole (rows outside a unit are dropped at insert time) unless their row
-// range misses the unit entirely.
+// Segment table of every unit: for each heavy column, each B nonzero b = (k, B(k,j)) is visited once and its A column's
+// boundaries for all of the column's units are written (split-table entries, mostly from cache, instead of a dependent
+// lookup chain per (unit, b) inside the numeric kernel).  Short A columns are given whole (rows outside a unit are
+// dropped at insert time) unless their row range misses the unit entirely.  The column's unit bounds are staged in LDS
+// and four units' split-table entries are loaded at once; a column with fewer B nonzeros than the workgroup's lanes
+// spreads its units over lane groups (~80 B nonzeros per heavy column).  Against one lane per B nonzero walking its
+// units with a scalar load each: s20 63.8 -> 63.6 ms, s22 rank panel 80.6 -> 79.9 ms (profiles/r06s_unit_segs_ab.txt).
 template <class SRT, int LOGT, int NT>
 __global__ void __launch_bounds__(256) k_unit_segs(const int32_t* __restrict__ cols, const int32_t* __restrict__ nunits,
-                                                   const int64_t* __restrict__ segoff, Unit* __restrict__ units,
-                                                   int32_t nsub, const int64_t* __restrict__ Acp,
-                                                   const int32_t* __restrict__ Air, const int64_t* __restrict__ Bcp,
-                                                   const int32_t* __restrict__ Bir, Split sp, UnitSeg* __restrict__ seg,
-                                                   const int2* __restrict__ uspan) {
+                                                       const int64_t* __restrict__ segoff, Unit* __restrict__ units,
+                                                       int32_t nsub, const int64_t* __restrict__ Acp,
+                                                       const int32_t* __restrict__ Air, const int64_t* __restrict__ Bcp,
+                                                       const int32_t* __restrict__ Bir, Split sp, UnitSeg* __restrict__ seg) {
+  __shared__ int2 us[kMaxSub];
   const int h = blockIdx.x;
-  const int32_t j = cols[h];
   const int nu = nunits[h];
+  if (nu == 0) return;   // uniform
+  const int32_t j = cols[h];
   const int64_t bs = Bcp[j], nb = Bcp[j + 1] - bs;
   const int64_t base = segoff[h];
   Unit* U = units + (int64_t)h * nsub;
-  for (int u = threadIdx.x; u < nu; u += blockDim.x) U[u].segbase = base + (int64_t)u * nb;
-  for (int64_t i = threadIdx.x; i < nb; i += blockDim.x) {
+  for (int u = threadIdx.x; u < nu; u += blockDim.x) {
+    U[u].segbase = base + (int64_t)u * nb;
+    us[u] = make_int2(U[u].s0, U[u].s1);
+  }
+  __syncthreads();
+  // lane groups: G groups of nb lanes when nb < 256 (group g takes units g, g+G, ...), else one group striding over nb
+  const int G = nb < (int64_t)blockDim.x ? (int)(blockDim.x / nb) : 1;
+  const int g = nb < (int64_t)blockDim.x ? (int)(threadIdx.x / nb) : 0;
+  if (g >= G) return;
+  const int64_t istep = nb < (int64_t)blockDim.x ? nb : (int64_t)blockDim.x;
+  for (int64_t i = nb < (int64_t)blockDim.x ? (int64_t)threadIdx.x % nb : threadIdx.x; i < nb; i += istep) {
     const int32_t k = Bir[bs + i];
     const int64_t c0 = Acp[k], c1 = Acp[k + 1];
     UnitSeg* out = seg + base + i;
     if (c1 - c0 >= kSplitMin) {
       const int32_t* t = sp.tab + (int64_t)sp.idx[k] * (sp.nsub + 1);
-      for (int u = 0; u < nu; ++u) {
-        const Unit un = U[u];
-        out[(int64_t)u * nb] = UnitSeg{c0 + t[un.s0], c0 + t[un.s1]};
+      for (int u = g; u < nu; u += 4 * G) {
+        int32_t lo[4], hi[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {   // four units' entries in flight together
+          const int2 b2 = us[min(u + q * G, nu - 1)];
+          lo[q] = t[b2.x];
+          hi[q] = t[b2.y];
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (u + q * G < nu) out[(int64_t)(u + q * G) * nb] = UnitSeg{c0 + lo[q], c0 + hi[q]};
       }
     } else {
       // a short column: whole, when its first..last rows overlap the unit (the sweep drops the other rows).
       // Narrowing it by binary search was measured: k_unit_segs 2.5 -> 5.1 ms for 0.6 ms of heavy sweep (r03r)
       const int32_t rf = c1 > c0 ? Air[c0] : 0, rl = c1 > c0 ? Air[c1 - 1] : -1;
-      for (int u = 0; u < nu; ++u) {
-        const Unit un = U[u];
-        const bool hit = c1 > c0 && rl >= ((int64_t)un.s0 << sp.log) && rf < ((int64_t)un.s1 << sp.log);
+      for (int u = g; u < nu; u += G) {
+        const int2 b2 = us[u];
+        const bool hit = c1 > c0 && rl >= ((int64_t)b2.x << sp.log) && rf < ((int64_t)b2.y << sp.log);
         out[(int64_t)u * nb] = hit ? UnitSeg{c0, c1} : UnitSeg{c0, c0};
       }
     }
