@@ -193,6 +193,7 @@ struct cbg_ctx {
   DevBuf oitems;                       // heavy items the rows-known kernel does not take
   DevBuf items2, ubkt;                 // the rows-known units in first-subwindow order + bucket counters (CBG_KNOWN_SORT)
   DevBuf ptab;                         // A's part table for k_sym_part (k_part_table)
+  DevBuf acol;                         // A's (length, first row, last row) per column (k_acol_info)
   DevBuf aos;                          // A's rows and values interleaved (k_num_heavy_known gathers)
   DevBuf gal[9];                       // fused Galerkin product scratch (galerkin.hip)
   void* pin = nullptr;                 // 16 KB of pinned host memory: small read-backs (bin counts, scalars)
@@ -211,7 +212,7 @@ inline void release_workspace(cbg_ctx* c) {
                     &c->ovf_list, &c->split_idx, &c->long_cols, &c->split_tab, &c->heavy_cols, &c->sub, &c->units,
                     &c->ucnt, &c->uspan, &c->ulist, &c->fb_units, &c->fb_list, &c->uovf_list, &c->nunits, &c->segsz,
                     &c->segoff, &c->useg, &c->icnt, &c->itemoff, &c->items, &c->parts, &c->wide_win, &c->hrows,
-                    &c->hmode, &c->hpoff, &c->urows, &c->oitems, &c->aos, &c->ptab, &c->items2, &c->ubkt})
+                    &c->hmode, &c->hpoff, &c->urows, &c->oitems, &c->aos, &c->ptab, &c->items2, &c->ubkt, &c->acol})
     b->release();
   for (DevBuf& b : c->stageA) b.release();
   for (DevBuf& b : c->stageB) b.release();
@@ -536,10 +537,11 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
   HIPCHK(ctx->ovf_list.reserve(sizeof(int32_t) * (N + 1)));
   HIPCHK(ctx->split_idx.reserve(sizeof(int32_t) * (A.ncol + 1)));
   HIPCHK(ctx->long_cols.reserve(sizeof(int32_t) * (A.ncol + 1)));
+  HIPCHK(ctx->acol.reserve(sizeof(int4) * (A.ncol + 1)));
   Captures cap;   // every workspace pointer below is taken after its buffer's last reserve; CAPCHK before launches
   cap.add(ctx->flop, "flop"); cap.add(ctx->span, "span"); cap.add(ctx->cnt, "cnt"); cap.add(ctx->list, "list");
   cap.add(ctx->hist, "hist"); cap.add(ctx->scalars, "scalars"); cap.add(ctx->ovf_list, "ovf_list");
-  cap.add(ctx->split_idx, "split_idx"); cap.add(ctx->long_cols, "long_cols");
+  cap.add(ctx->split_idx, "split_idx"); cap.add(ctx->long_cols, "long_cols"); cap.add(ctx->acol, "acol");
   int64_t* flop = ctx->flop.as<int64_t>();
   int2* span = ctx->span.as<int2>();
   int64_t* nnz = ctx->cnt.as<int64_t>();
@@ -561,13 +563,15 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
   HIPCHK(hipMemsetAsync(hist, 0, sizeof(unsigned long long) * 96, st));   // the symbolic histogram and sc together
   HIPCHK(hipMemsetAsync(nnz, 0, sizeof(int64_t) * N, st));
   {
+    int4* ainfo = ctx->acol.as<int4>();
+    k_acol_info<<<(int)grid_for(A.ncol, 256, kMaxGrid), 256, 0, st>>>(A.ncol, A.cp, A.ir, ainfo);
     const int64_t avg = N > 0 ? (B.nnz + N - 1) / N : 0;   // lanes per column ~ the mean B column length
     if (avg <= 4)
-      k_col_stats<4><<<(int)grid_for(N * 4, 256, kMaxGrid), 256, 0, st>>>(N, A.cp, A.ir, B.cp, B.ir, flop, span, sc);
+      k_col_stats<4><<<(int)grid_for(N * 4, 256, kMaxGrid), 256, 0, st>>>(N, ainfo, B.cp, B.ir, flop, span, sc);
     else if (avg <= 8)
-      k_col_stats<8><<<(int)grid_for(N * 8, 256, kMaxGrid), 256, 0, st>>>(N, A.cp, A.ir, B.cp, B.ir, flop, span, sc);
+      k_col_stats<8><<<(int)grid_for(N * 8, 256, kMaxGrid), 256, 0, st>>>(N, ainfo, B.cp, B.ir, flop, span, sc);
     else
-      k_col_stats<16><<<(int)grid_for(N * 16, 256, kMaxGrid), 256, 0, st>>>(N, A.cp, A.ir, B.cp, B.ir, flop, span, sc);
+      k_col_stats<16><<<(int)grid_for(N * 16, 256, kMaxGrid), 256, 0, st>>>(N, ainfo, B.cp, B.ir, flop, span, sc);
   }
   k_split_assign<<<(int)grid_for(A.ncol, 256, kMaxGrid), 256, 0, st>>>(A.ncol, A.cp, ctx->split_idx.as<int32_t>(),
                                                                         ctx->long_cols.as<int32_t>(), nlong);

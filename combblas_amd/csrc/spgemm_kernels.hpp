@@ -304,13 +304,23 @@ __device__ __forceinline__ void unit_bounds(const int64_t* __restrict__ Acp, con
 }
 
 // ============================================================================ 1. column statistics
+// Every A column's (length, first row, last row) in one 16-byte record, written by one streaming pass over A's column
+// pointers: the statistics then gather one record per B nonzero instead of the two pointers and the first and last
+// rows (three random cache lines; the 2^22 A columns of an s22 rank panel miss the L2 on most of them)
+__global__ void __launch_bounds__(256) k_acol_info(int64_t ncol, const int64_t* __restrict__ Acp,
+                                                   const int32_t* __restrict__ Air, int4* __restrict__ info) {
+  for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < ncol; k += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t a0 = Acp[k], a1 = Acp[k + 1];
+    info[k] = a1 > a0 ? make_int4((int)(a1 - a0), Air[a0], Air[a1 - 1], 0) : make_int4(0, INT32_MAX, -1, 0);
+  }
+}
+
 // flop[j] = sum_{k in B(:,j)} nnz(A(:,k))   (estimateFLOP, mtSpGEMM.h:1117-1135)
 // span[j] = [min, max] row index any of those A columns holds (A columns are row-sorted).
 // LPC lanes per column (4, 8 or 16: the host picks the power of two nearest nnz(B)/ncol, so short columns do
 // not idle most of a 16-lane group).
 template <int LPC>
-__global__ void __launch_bounds__(256) k_col_stats(int64_t ncol, const int64_t* __restrict__ Acp,
-                                                   const int32_t* __restrict__ Air,
+__global__ void __launch_bounds__(256) k_col_stats(int64_t ncol, const int4* __restrict__ ainfo,
                                                    const int64_t* __restrict__ Bcp,
                                                    const int32_t* __restrict__ Bir,
                                                    int64_t* __restrict__ flop, int2* __restrict__ span,
@@ -327,13 +337,10 @@ __global__ void __launch_bounds__(256) k_col_stats(int64_t ncol, const int64_t* 
     int lo = INT32_MAX, hi = -1;
     const int64_t e = Bcp[j + 1];
     for (int64_t p = Bcp[j] + sub; p < e; p += LPC) {
-      const int32_t k = Bir[p];
-      const int64_t a0 = Acp[k], a1 = Acp[k + 1];
-      if (a1 > a0) {
-        f += a1 - a0;
-        lo = min(lo, Air[a0]);
-        hi = max(hi, Air[a1 - 1]);
-      }
+      const int4 a = ainfo[Bir[p]];   // (length, first row, last row); an empty column: (0, INT32_MAX, -1)
+      f += a.x;
+      lo = min(lo, a.y);
+      hi = max(hi, a.z);
     }
 #pragma unroll
     for (int d = LPC / 2; d > 0; d >>= 1) {
