@@ -1527,7 +1527,10 @@ __global__ void __launch_bounds__(256) k_heavy_sums(int H, const int32_t* __rest
 // units of a heavy column: consecutive subwindows while the running count stays <= unit_cap
 // unit_cap / span_cap come from the semiring (heavy_unit_caps): rank-mode accumulators hold up to
 // kUnitCap outputs over a bounded span; hash-only semirings (BoolCopy) keep load <= 1/2.
-__global__ void k_build_units(int H, const int32_t* __restrict__ cols, const int32_t* __restrict__ sub, int32_t nsub,
+// One thread per column walks its subwindow counts in chunks of kBuildChunk, loaded together into the thread's LDS
+// slice (one load latency per chunk instead of one per subwindow).
+constexpr int kBuildChunk = 16;
+__global__ void __launch_bounds__(256) k_build_units(int H, const int32_t* __restrict__ cols, const int32_t* __restrict__ sub, int32_t nsub,
                               int32_t log, int64_t unit_cap, int64_t span_cap, int64_t rank_bytes, int32_t acc_bytes,
                               const int2* __restrict__ span, const int64_t* __restrict__ colptr,
                               const int64_t* __restrict__ Bcp, Unit* __restrict__ units, int64_t* __restrict__ ucnt,
@@ -1582,8 +1585,17 @@ __global__ void k_build_units(int H, const int32_t* __restrict__ cols, const int
     ++u;
     out += n;
   };
+  __shared__ int32_t cs[256 * (kBuildChunk + 1)];   // odd stride: the lanes' slices start in distinct banks
+  int32_t* my = cs + threadIdx.x * (kBuildChunk + 1);
   for (int32_t s = sf; s <= sl; ++s) {
-    const int64_t n = c[s];
+    if (((s - sf) & (kBuildChunk - 1)) == 0) {
+      int32_t r[kBuildChunk];
+#pragma unroll
+      for (int q = 0; q < kBuildChunk; ++q) r[q] = s + q <= sl ? c[s + q] : 0;
+#pragma unroll
+      for (int q = 0; q < kBuildChunk; ++q) my[q] = r[q];
+    }
+    const int64_t n = my[(s - sf) & (kBuildChunk - 1)];
     if (acc == 0) st = s;   // a unit starts at its first non-empty subwindow (empty gaps span nothing)
     const int64_t sub_span = (int64_t)(s + 1 - st) << log;
     int64_t cap = span_cap;

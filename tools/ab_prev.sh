@@ -1,7 +1,8 @@
 #!/bin/bash
-# A/B: k_col_stats gathering one (length, first, last) record per B nonzero (main) vs the two pointers and two rows (tools/var/prev = the previous commit)
+# A/B of the main library against tools/var/prev (the previous commit, `make var VAR=prev` from its sources): GPU parity
+# of the heavy path on main, s20 bench x2, s22 rank shares 0 and 4, rocprofv3 kernel stats of main at s20.  usage: ab_prev.sh <tag>
 set -u
-O=gpurun_out/r06t
+O=gpurun_out/${1:?tag}
 mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 900 python -u -m pytest tests/test_spgemm_gpu.py tests/test_fullsize_gpu.py -m gpu -x -q --timeout 300 \
