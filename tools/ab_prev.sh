@@ -1,11 +1,11 @@
 #!/bin/bash
 # A/B of the main library against tools/var/prev (the previous commit, `make var VAR=prev` from its sources): GPU parity
-# of the heavy path on main, s20 bench x2, s22 rank shares 0 and 4, rocprofv3 kernel stats of main at s20.  usage: ab_prev.sh <tag>
+# of the heavy path on main, s20 bench x2, s22 rank shares 0 and 4, rocprofv3 kernel stats of main at s20.  usage: [TESTS=tests] ab_prev.sh <tag>
 set -u
 O=gpurun_out/${1:?tag}
 mkdir -p $O
 export TMPDIR=/tmp
-timeout -k 10 900 python -u -m pytest tests/test_spgemm_gpu.py tests/test_fullsize_gpu.py -m gpu -x -q --timeout 300 \
+timeout -k 10 1100 python -u -m pytest ${TESTS:-tests/test_spgemm_gpu.py tests/test_fullsize_gpu.py} -m gpu -x -q --timeout 300 \
   --timeout-method thread > $O/tests.log 2>&1 || { tail -15 $O/tests.log; exit 11; }
 tail -2 $O/tests.log
 for r in 1 2; do
