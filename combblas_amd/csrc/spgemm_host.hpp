@@ -564,7 +564,8 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
   HIPCHK(hipMemsetAsync(nnz, 0, sizeof(int64_t) * N, st));
   {
     int4* ainfo = ctx->acol.as<int4>();
-    k_acol_info<<<(int)grid_for(A.ncol, 256, kMaxGrid), 256, 0, st>>>(A.ncol, A.cp, A.ir, ainfo);
+    k_acol_info<<<(int)std::max<int64_t>(1, std::min<int64_t>(kMaxGrid, (A.ncol + 1023) / 1024)), 256, 0, st>>>(
+        A.ncol, A.cp, A.ir, ainfo, ctx->split_idx.as<int32_t>(), ctx->long_cols.as<int32_t>(), nlong);
     const int64_t avg = N > 0 ? (B.nnz + N - 1) / N : 0;   // lanes per column ~ the mean B column length
     if (avg <= 4)
       k_col_stats<4><<<(int)grid_for(N * 4, 256, kMaxGrid), 256, 0, st>>>(N, ainfo, B.cp, B.ir, flop, span, sc);
@@ -573,8 +574,6 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
     else
       k_col_stats<16><<<(int)grid_for(N * 16, 256, kMaxGrid), 256, 0, st>>>(N, ainfo, B.cp, B.ir, flop, span, sc);
   }
-  k_split_assign<<<(int)grid_for(A.ncol, 256, kMaxGrid), 256, 0, st>>>(A.ncol, A.cp, ctx->split_idx.as<int32_t>(),
-                                                                        ctx->long_cols.as<int32_t>(), nlong);
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(ctx->ev[1], st));
 
@@ -818,8 +817,8 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
     spl.useg = ctx->useg.as<UnitSeg>();
     cap.add(ctx->useg, "useg");
     k_unit_segs<SRT, CBG_KNOWN_LOGT, CBG_KNOWN_NT><<<H, 256, 0, st>>>(
-        ctx->heavy_cols.as<int32_t>(), ctx->nunits.as<int32_t>(), ctx->segoff.as<int64_t>(), units, nsub, A.cp, A.ir,
-        B.cp, B.ir, spl, ctx->useg.as<UnitSeg>());
+        ctx->heavy_cols.as<int32_t>(), ctx->nunits.as<int32_t>(), ctx->segoff.as<int64_t>(), units, nsub, A.cp,
+        ctx->acol.as<int4>(), B.cp, B.ir, spl, ctx->useg.as<UnitSeg>());
     // units -> rows-known list + other items (device counts sc[12], sc[13]; units <= items * kItemUnits)
     const int64_t ucap = nitems * kItemUnits + 1;
     HIPCHK(ctx->items.reserve(sizeof(KnownUnit) * ucap));

@@ -304,14 +304,55 @@ __device__ __forceinline__ void unit_bounds(const int64_t* __restrict__ Acp, con
 }
 
 // ============================================================================ 1. column statistics
-// Every A column's (length, first row, last row) in one 16-byte record, written by one streaming pass over A's column
-// pointers: the statistics then gather one record per B nonzero instead of the two pointers and the first and last
-// rows (three random cache lines; the 2^22 A columns of an s22 rank panel miss the L2 on most of them)
+// Every A column's (length, first row, last row, split-table row or -1) in one 16-byte record, written by one streaming
+// pass over A's column pointers: the statistics and the unit segment table gather one record per B nonzero instead of
+// the two pointers, the first and last rows and the split index (up to four random cache lines; the 2^22 A columns of
+// an s22 rank panel miss the L2 on most of them).  The same pass numbers the long columns (>= kSplitMin entries) for
+// the split table: each workgroup takes a contiguous range of columns, counts its long ones, claims their numbers with
+// ONE atomic, then numbers them in order -- a claim per wavefront serialised ~2^16 same-address atomics at the L2
+// (k_split_assign: 0.74 ms for the 2^22 columns of a rank panel, 0.17 ms at s20).
 __global__ void __launch_bounds__(256) k_acol_info(int64_t ncol, const int64_t* __restrict__ Acp,
-                                                   const int32_t* __restrict__ Air, int4* __restrict__ info) {
-  for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < ncol; k += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t a0 = Acp[k], a1 = Acp[k + 1];
-    info[k] = a1 > a0 ? make_int4((int)(a1 - a0), Air[a0], Air[a1 - 1], 0) : make_int4(0, INT32_MAX, -1, 0);
+                                                   const int32_t* __restrict__ Air, int4* __restrict__ info,
+                                                   int32_t* __restrict__ idx, int32_t* __restrict__ longcols,
+                                                   int* __restrict__ nlong) {
+  __shared__ int s_w[256 / kWave];
+  __shared__ int s_base;
+  const int64_t per = (ncol + gridDim.x - 1) / gridDim.x;
+  const int64_t c0 = blockIdx.x * per, c1 = min(ncol, c0 + per);
+  const int lane = lane_id(), w = threadIdx.x / kWave;
+  int cnt = 0;
+  for (int64_t k = c0 + threadIdx.x; k < c1; k += 256) cnt += Acp[k + 1] - Acp[k] >= kSplitMin;
+  cnt = (int)wave_sum64(cnt);
+  if (lane == 0) s_w[w] = cnt;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int t = 0;
+    for (int v = 0; v < 256 / kWave; ++v) t += s_w[v];
+    s_base = t ? atomicAdd(nlong, t) : 0;
+  }
+  __syncthreads();
+  int run = s_base;
+  for (int64_t t0 = c0; t0 < c1; t0 += 256) {
+    const int64_t k = t0 + threadIdx.x;
+    int64_t a0 = 0, a1 = 0;
+    if (k < c1) { a0 = Acp[k]; a1 = Acp[k + 1]; }
+    const bool lng = a1 - a0 >= kSplitMin;
+    const uint64_t m = __ballot(lng);
+    __syncthreads();   // s_w reused
+    if (lane == 0) s_w[w] = __popcll(m);
+    __syncthreads();
+    int before = 0, tile = 0;
+    for (int v = 0; v < 256 / kWave; ++v) {
+      before += v < w ? s_w[v] : 0;
+      tile += s_w[v];
+    }
+    if (k < c1) {
+      const int e = lng ? run + before + __popcll(m & ((1ull << lane) - 1ull)) : -1;
+      idx[k] = e;
+      if (lng) longcols[e] = (int32_t)k;
+      info[k] = a1 > a0 ? make_int4((int)(a1 - a0), Air[a0], Air[a1 - 1], e) : make_int4(0, INT32_MAX, -1, -1);
+    }
+    run += tile;
   }
 }
 
@@ -1435,30 +1476,6 @@ __global__ void __launch_bounds__(256) k_scan_apply(int64_t n, const int64_t* __
 }
 
 // ============================================================================ 5. heavy-column units
-// split table rows for long A columns
-__global__ void k_split_assign(int64_t ncol, const int64_t* __restrict__ Acp, int32_t* __restrict__ idx,
-                               int32_t* __restrict__ longcols, int* __restrict__ nlong) {
-  // one counter claim per wavefront (ballot + prefix popcount): a claim per long column serialised on the counter
-  // (0.74 ms for the 2^22 columns of an s22 rank panel)
-  const int lane = lane_id();
-  for (int64_t k0 = blockIdx.x * (int64_t)blockDim.x + (threadIdx.x & ~(kWave - 1)); k0 < ncol;
-       k0 += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t k = k0 + lane;
-    const bool lng = k < ncol && Acp[k + 1] - Acp[k] >= kSplitMin;
-    const uint64_t m = __ballot(lng);
-    int e0 = 0;
-    if (m) {
-      const int lead = __ffsll((unsigned long long)m) - 1;
-      if (lane == lead) e0 = atomicAdd(nlong, __popcll(m));
-      e0 = __shfl(e0, lead, kWave);
-    }
-    if (k < ncol) {
-      const int e = e0 + __popcll(m & ((1ull << lane) - 1ull));
-      idx[k] = lng ? e : -1;
-      if (lng) longcols[e] = (int32_t)k;
-    }
-  }
-}
 // one wavefront per long column: every subwindow boundary by binary search
 __global__ void __launch_bounds__(256) k_split_fill(int nlong, const int32_t* __restrict__ longcols,
                                                     const int64_t* __restrict__ Acp, const int32_t* __restrict__ Air,
@@ -1645,7 +1662,7 @@ template <class SRT, int LOGT, int NT>
 __global__ void __launch_bounds__(256) k_unit_segs(const int32_t* __restrict__ cols, const int32_t* __restrict__ nunits,
                                                        const int64_t* __restrict__ segoff, Unit* __restrict__ units,
                                                        int32_t nsub, const int64_t* __restrict__ Acp,
-                                                       const int32_t* __restrict__ Air, const int64_t* __restrict__ Bcp,
+                                                       const int4* __restrict__ ainfo, const int64_t* __restrict__ Bcp,
                                                        const int32_t* __restrict__ Bir, Split sp, UnitSeg* __restrict__ seg) {
   __shared__ int2 us[kMaxSub];
   const int h = blockIdx.x;
@@ -1667,10 +1684,12 @@ __global__ void __launch_bounds__(256) k_unit_segs(const int32_t* __restrict__ c
   const int64_t istep = nb < (int64_t)blockDim.x ? nb : (int64_t)blockDim.x;
   for (int64_t i = nb < (int64_t)blockDim.x ? (int64_t)threadIdx.x % nb : threadIdx.x; i < nb; i += istep) {
     const int32_t k = Bir[bs + i];
-    const int64_t c0 = Acp[k], c1 = Acp[k + 1];
+    const int64_t c0 = Acp[k];
+    const int4 ai = ainfo[k];   // (length, first row, last row, split-table row)
+    const int64_t c1 = c0 + ai.x;
     UnitSeg* out = seg + base + i;
-    if (c1 - c0 >= kSplitMin) {
-      const int32_t* t = sp.tab + (int64_t)sp.idx[k] * (sp.nsub + 1);
+    if (ai.w >= 0) {
+      const int32_t* t = sp.tab + (int64_t)ai.w * (sp.nsub + 1);
       for (int u = g; u < nu; u += 4 * G) {
         int32_t lo[4], hi[4];
 #pragma unroll
@@ -1686,7 +1705,7 @@ __global__ void __launch_bounds__(256) k_unit_segs(const int32_t* __restrict__ c
     } else {
       // a short column: whole, when its first..last rows overlap the unit (the sweep drops the other rows).
       // Narrowing it by binary search was measured: k_unit_segs 2.5 -> 5.1 ms for 0.6 ms of heavy sweep (r03r)
-      const int32_t rf = c1 > c0 ? Air[c0] : 0, rl = c1 > c0 ? Air[c1 - 1] : -1;
+      const int32_t rf = ai.y, rl = ai.z;   // (INT32_MAX, -1) for an empty column: never hits
       for (int u = g; u < nu; u += G) {
         const int2 b2 = us[u];
         const bool hit = c1 > c0 && rl >= ((int64_t)b2.x << sp.log) && rf < ((int64_t)b2.y << sp.log);
