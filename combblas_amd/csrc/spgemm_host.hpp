@@ -662,16 +662,18 @@ cbg_status spgemm_impl(cbg_ctx* ctx, const cbg_dcsc_view* Av, const cbg_dcsc_vie
       // the part table of A (k_part_table), unless it would not fit comfortably (CBG_PART_TABLE=0: off)
       static const bool ptab_env = [] { const char* x = std::getenv("CBG_PART_TABLE"); return !(x && x[0] == '0'); }();
       const int32_t P = (int32_t)(((M - 1) >> kPartLog) + 1);
-      const size_t pbytes = sizeof(int32_t) * ((size_t)A.ncol * (P + 1) + 1);
+      int32_t PS = 8;   // row stride in words: a power of two >= P + 3 (k_part_table)
+      while (PS < P + 3) PS <<= 1;
+      const size_t pbytes = sizeof(int32_t) * ((size_t)A.ncol * PS + 1);
       size_t pfree = 0, ptot = 0;
       if (ptab_env && P > 1 && A.ncol > 0 &&
           (pbytes <= ctx->ptab.n || (hipMemGetInfo(&pfree, &ptot) == hipSuccess && pbytes < pfree / 8))) {
         HIPCHK(ctx->ptab.reserve(pbytes));
         cap.add(ctx->ptab, "ptab");
-        k_part_table<<<(int)grid_for(A.ncol, 256, kMaxGrid * 4), 256, 0, st>>>(A.ncol, A.cp, A.ir, P,
+        k_part_table<<<(int)grid_for(A.ncol, 256, kMaxGrid * 4), 256, 0, st>>>(A.ncol, A.cp, A.ir, P, PS,
                                                                                  ctx->ptab.as<int32_t>());
         spl.ptab = ctx->ptab.as<int32_t>();
-        spl.pstride = P + 1;
+        spl.pstride = PS;
       }
       CAPCHK(cap);
       int *nparts = si + 8, *nwin = si + 9;

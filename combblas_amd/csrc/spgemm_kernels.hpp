@@ -136,8 +136,9 @@ struct Split {
   const UnitSeg* useg;  // precomputed unit segments (k_unit_segs)
   const HRow* hrows;    // sorted output rows of heavy columns written by the symbolic pass (or null)
   const UnitRows* urows;// per unit: where its rows lie in hrows (k_build_units)
-  const int32_t* ptab;  // part table (k_part_table): ptab[k*pstride + p] = (first entry with row >= p*2^kPartLog) - cp[k]
-  int32_t pstride;      // parts of the row space + 1 (0: no table)
+  const int32_t* ptab;  // part table (k_part_table): row k = [cp[k] (two words), then for p = 0..P: (first entry with
+                        // row >= p*2^kPartLog) - cp[k]]
+  int32_t pstride;      // words per row: a power of two >= parts + 3 (0: no table)
 };
 
 struct Unit {
@@ -1235,12 +1236,17 @@ k_sym_part(const PartItem* __restrict__ items, const int* __restrict__ count_dev
   // the segment [a0, a1) of B nonzero b (A column Bir[b]) inside part p0 (absolute part index) of the row space
   auto seg_in_part = [&](int32_t k, int32_t p0, int64_t& a0, int64_t& a1) {
     const int32_t pr0 = p0 << kPartLog;
-    const int64_t c0 = Acp[k], c1 = Acp[k + 1];
     if (spl.ptab) {   // every A column narrowed to the part's rows: no gathers of rows outside it
-      const int32_t* t = spl.ptab + (int64_t)k * spl.pstride + p0;
-      a0 = c0 + t[0];
-      a1 = c0 + t[1];
-    } else if (c1 - c0 >= kSplitMin) {
+      // one aligned row per column: its first entry's position, then the part offsets (one cache line, no Acp read)
+      const int32_t* row = spl.ptab + (int64_t)k * spl.pstride;
+      const int2 c = *(const int2*)row;
+      const int64_t c0 = (int64_t)(uint32_t)c.x | ((int64_t)c.y << 32);
+      a0 = c0 + row[2 + p0];
+      a1 = c0 + row[3 + p0];
+      return;
+    }
+    const int64_t c0 = Acp[k], c1 = Acp[k + 1];
+    if (c1 - c0 >= kSplitMin) {
       const int32_t* t = spl.tab + (int64_t)spl.idx[k] * (spl.nsub + 1);
       a0 = c0 + t[pr0 >> spl.log];
       a1 = c0 + t[min(spl.nsub, (int32_t)(((int64_t)pr0 + (1 << kPartLog)) >> spl.log))];
@@ -1368,12 +1374,16 @@ k_sym_part(const PartItem* __restrict__ items, const int* __restrict__ count_dev
 // Part table of A for k_sym_part: for every A column the entry offsets of the 2^kPartLog-row part boundaries (P + 1 per
 // column), so a part's item gathers only the rows inside the part -- without it a short column (no split-table row) is
 // read whole by every part of every wide column it feeds (8 parts at 2^21 rows).  One thread per column: a linear walk
-// over a short column's sorted rows, binary searches in a long one.
+// over a short column's sorted rows, binary searches in a long one.  Row k = [Acp[k] (two words), offsets 0..P], PS
+// words (a power of two >= P + 3), so a part's lookup reads one cache line and no column pointer.
 __global__ void __launch_bounds__(256) k_part_table(int64_t ncol, const int64_t* __restrict__ Acp,
-                                                    const int32_t* __restrict__ Air, int32_t P, int32_t* __restrict__ ptab) {
+                                                    const int32_t* __restrict__ Air, int32_t P, int32_t PS,
+                                                    int32_t* __restrict__ ptab) {
   for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < ncol; k += (int64_t)gridDim.x * blockDim.x) {
     const int64_t c0 = Acp[k], c1 = Acp[k + 1];
-    int32_t* t = ptab + k * (P + 1);
+    int32_t* row = ptab + k * PS;
+    *(int2*)row = make_int2((int32_t)(uint32_t)(c0 & 0xffffffff), (int32_t)(c0 >> 32));
+    int32_t* t = row + 2;
     t[0] = 0;
     if (c1 - c0 <= 64) {
       int64_t i = c0;
